@@ -1,0 +1,137 @@
+/* mmt.h — C-ABI of libmmt_hip.so, the MI355X-native (gfx950) training hot path of the
+ * multimodal transformer of tsnuk/trade-AId-multimodal-transformer.
+ *
+ * The reference exposes no C / FFI boundary on this path: its boundary is the
+ * Python module API that main.py imports. Each entry point below replaces one piece of that
+ * Python surface; the Python host layer (trade-aid-multimodal-transformer_amd/model.py,
+ * mmt_optim.py, training_utils.py) binds them through ctypes exactly as INTEGRATION.md shows.
+ *
+ *   mmt_create / mmt_destroy      <- MultimodalTransformer.__init__ (reference model.py:358-370):
+ *                                    dims from config_utils (model.py:25-27), cross flags from
+ *                                    all_modality_params[i][8] (model.py:196)
+ *   mmt_tensor_count/_info        <- MultimodalTransformer.state_dict() key set and shapes
+ *                                    (reference main.py:470, 635) over one flat fp32 buffer
+ *   mmt_forward                   <- MultimodalTransformer.forward(idx_list, targets_list)
+ *                                    (model.py:380-402): logits per modality + mean CE losses
+ *   mmt_backward[_stage]          <- total_loss.backward() of main.py:646-649 (autograd over
+ *                                    model.py), gradients into a flat fp32 buffer
+ *   mmt_adamw_step                <- torch.optim.AdamW(m.parameters(), lr).step() (main.py:464, 650)
+ *   mmt_eval_direction            <- the per-sample loop of calculate_evaluation_metrics
+ *                                    (training_utils.py:259-304)
+ *   mmt_op_*                      primitive kernels, exported for kernel-level parity tests.
+ *
+ * Conventions: every pointer is a device pointer unless stated; memory is owned by the caller
+ * (PyTorch allocates parameters, gradients, moments, logits and the workspace); the library
+ * never frees caller memory. All work is asynchronous on the caller's HIP stream (`stream` is a
+ * hipStream_t passed as void*). Every function returns 0 (MMT_OK) or a negative mmt_status;
+ * no C++ exception crosses the ABI; mmt_last_error() describes the last failure.
+ */
+#ifndef MMT_H_
+#define MMT_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMT_MAX_MODALITIES 8
+
+enum mmt_status {
+  MMT_OK = 0,
+  MMT_ERR_INVALID = -1,     /* bad argument / shape */
+  MMT_ERR_UNSUPPORTED = -2, /* configuration outside what the kernels implement */
+  MMT_ERR_HIP = -3,         /* a HIP runtime call or launch failed */
+  MMT_ERR_STATE = -4        /* call order violated (e.g. backward without matching forward) */
+};
+
+typedef struct mmt_config {
+  int32_t num_modalities;                       /* M, 1..8 */
+  int32_t n_embd;                               /* C */
+  int32_t n_head;                               /* H, head size C/H in {8,16,24,32,48,64} */
+  int32_t n_layer;                              /* L */
+  int32_t block_size;                           /* T (max sequence length, positional table rows) */
+  int32_t vocab_sizes[MMT_MAX_MODALITIES];      /* V_i >= 1 */
+  int32_t cross_attention[MMT_MAX_MODALITIES];  /* all_modality_params[i][8] */
+  float dropout;                                /* nn.Dropout p (model.py:57,87,107,134,171) */
+  uint64_t seed;                                /* dropout RNG seed */
+} mmt_config;
+
+typedef struct mmt_ctx mmt_ctx;
+
+/* lifecycle */
+mmt_ctx* mmt_create(const mmt_config* cfg); /* NULL on failure, see mmt_create_error() */
+const char* mmt_create_error(void);
+void mmt_destroy(mmt_ctx* ctx);
+const char* mmt_last_error(const mmt_ctx* ctx);
+const char* mmt_version(void);
+
+/* parameter layout: one flat fp32 buffer; each reference state_dict tensor is a contiguous slice */
+int64_t mmt_param_count(const mmt_ctx* ctx);        /* elements of the flat buffer */
+int64_t mmt_param_active_count(const mmt_ctx* ctx); /* prefix that receives gradients */
+int32_t mmt_tensor_count(const mmt_ctx* ctx);
+int mmt_tensor_info(const mmt_ctx* ctx, int32_t i, char* name, int32_t name_cap, int64_t* offset, int32_t* ndim,
+                    int64_t* shape /* [2] */, int32_t* kind /* 0 weight(N(0,.02)) 1 bias(0) 2 ln weight(1) 3 ln bias(0) */);
+
+/* workspace (saved activations + packed bf16 weights + backward scratch) for a batch size */
+int64_t mmt_workspace_bytes(mmt_ctx* ctx, int32_t batch);
+
+/* forward: idx[i], tgt[i] int64 [batch, T] (tgt may be NULL: no loss); logits[i] fp32 [batch, T, V_i];
+ * losses fp32 [M] (mean CE per modality, written only when tgt != NULL); training != 0 enables dropout */
+int mmt_forward(mmt_ctx* ctx, void* stream, int32_t batch, const int64_t* const* idx, const int64_t* const* tgt,
+                const float* params, float* const* logits, float* losses, void* workspace, int32_t training);
+
+/* backward of sum_i loss_grads[i] * loss_i through the last mmt_forward (same workspace/params).
+ * grads: fp32 flat buffer (mmt_param_count elements) — OVERWRITTEN (zeroed then accumulated). */
+int mmt_backward(mmt_ctx* ctx, void* stream, const float* loss_grads, const float* params, float* grads,
+                 void* workspace);
+/* the same, split into stages (post-block, layer L-1 .. layer 0, embeddings) so a caller can
+ * all-reduce each finished gradient range while the next stage computes (DP overlap). */
+int32_t mmt_backward_stage_count(const mmt_ctx* ctx);
+int mmt_backward_stage_range(const mmt_ctx* ctx, int32_t stage, int64_t* begin, int64_t* end);
+int mmt_backward_stage(mmt_ctx* ctx, void* stream, int32_t stage, const float* loss_grads, const float* params,
+                       float* grads, void* workspace);
+
+/* fused AdamW over n elements (torch.optim.AdamW semantics, decoupled decay, bias correction) */
+int mmt_adamw_step(mmt_ctx* ctx, void* stream, float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                   int64_t n, int64_t step, float lr, float beta1, float beta2, float eps, float weight_decay);
+
+/* directional metric for one numeric modality: logits fp32 [batch, T, V]; xb/yb int64 [batch, T];
+ * vocab fp64 [V]; accumulates wins_losses[0..1] (int32) and certainty_sum (fp64) on device */
+int mmt_eval_direction(mmt_ctx* ctx, void* stream, int32_t batch, int32_t T, int32_t V, const float* logits,
+                       const int64_t* xb, const int64_t* yb, const double* vocab, int32_t is_percent,
+                       int32_t* wins_losses, double* certainty_sum);
+
+/* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
+int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t splits, int32_t M, int32_t N,
+                int32_t K, const void* A, int32_t lda, const void* B, int32_t ldb, const float* bias,
+                const void* aux, int32_t ldaux, const float* resid, int32_t ldres, float* o32, int32_t ldc,
+                void* o16, int32_t ldo16, float alpha);
+int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
+                         void* y16, float* mean, float* rstd);
+int mmt_op_layernorm_bwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* mean,
+                         const float* rstd, const float* dy, float* dx, void* dx16, float* dgamma, float* dbeta);
+/* causal attention over nstreams KV streams; layouts as in the engine (row = b*T + t) */
+int mmt_op_attention_fwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams,
+                         const void* q, int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld,
+                         int32_t kv_hstride, void* o, int32_t o_ld, void* const* oj, float* const* lse);
+int mmt_op_attention_bwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams,
+                         const void* q, int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld,
+                         int32_t kv_hstride, const void* o, int32_t o_ld, const void* const* oj,
+                         const float* const* lse, const void* dout, int32_t dout_ld, float* const* dvec, void* dq,
+                         int32_t dq_ld, void* const* dk, void* const* dv, int32_t dkv_ld, int32_t dkv_hstride);
+int mmt_op_qkv2_fwd(void* stream, int32_t R, int32_t nblk, int32_t hs, const void* h1, int32_t ld_h1,
+                    const float* w2, void* out, int32_t ld_out);
+int mmt_op_qkv2_bwd(void* stream, int32_t R, int32_t nblk, int32_t hs, const void* h1, int32_t ld_h1,
+                    const float* w2, const void* dout, int32_t ld_out, void* dh1, float* dw2);
+int mmt_op_colsum(void* stream, int32_t R, int32_t N, const void* x, int32_t ld, float* out, float alpha);
+int mmt_op_cross_entropy(void* stream, int32_t R, int32_t V, const float* logits, const int64_t* tgt,
+                         void* dlogits, int32_t ld_d, float* loss);
+int mmt_op_embedding_fwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx,
+                         const float* tok, const float* pos, float* x);
+int mmt_op_embedding_bwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx,
+                         const float* dx, float* dtok, float* dpos);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMT_H_ */

@@ -1,0 +1,385 @@
+"""CPU ORACLE for the multimodal-transformer training hot path — TEST INFRASTRUCTURE ONLY.
+
+Only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may import this
+module, and only as the checker / the timed CPU baseline. The product path (the HIP library
+behind `trade-aid-multimodal-transformer_amd/`) never calls into it.
+
+What it is: a plain-PyTorch fp32 CPU restatement of the reference algorithm, written per
+head and per modality exactly as the reference module structure computes it (eager ops, one
+`x @ W.T + b` per reference `nn.Linear`), over a state dict keyed with the reference's own
+state_dict names. Autograd supplies the backward (the reference relies on it too).
+
+Pinning: `tests/test_oracle.py` checks this restatement against golden vectors produced by
+importing the reference itself (`tests/golden/gen_golden.py`): logits, losses, every gradient,
+params after 1 and 3 AdamW steps, the directional metric, and the batch start indices.
+
+Reference anchors (paths relative to the reference repo root):
+  model.py:30-73    Head            -> _head
+  model.py:76-92    MultiHeadAttention -> _mha
+  model.py:95-159   CrossAttention  -> _cross
+  model.py:162-175  FeedForward     -> _ffn
+  model.py:178-244  MultimodalBlock -> _block
+  model.py:285-319  MultimodalPreBlock -> forward (embedding + shared positional table)
+  model.py:322-352  MultimodalPostBlock -> forward (LN -> Linear -> tanh -> Linear)
+  model.py:380-402  MultimodalTransformer.forward (+ F.cross_entropy mean per modality)
+  model.py:372-378  _init_weights    -> init_params
+  main.py:464,648-650 torch.optim.AdamW defaults -> adamw_step
+  training_utils.py:33-181 generate_batch_starting_indices -> batch_starting_indices
+  training_utils.py:184-330 _get_direction_sign / calculate_evaluation_metrics -> eval_metrics
+  data_utils.py:293-358 add_rand_to_data_points -> jitter_inplace
+"""
+import math
+import numbers
+import random
+
+import torch
+import torch.nn.functional as F
+
+
+# --------------------------------------------------------------------------------------
+# configuration helpers
+# --------------------------------------------------------------------------------------
+class OracleConfig:
+    def __init__(self, n_embd, n_head, n_layer, block_size, vocab_sizes, cross, dropout=0.0):
+        self.C = int(n_embd)
+        self.H = int(n_head)
+        self.L = int(n_layer)
+        self.T = int(block_size)
+        self.V = [int(v) for v in vocab_sizes]
+        self.M = len(self.V)
+        self.cross = [bool(c) for c in cross]
+        self.dropout = float(dropout)
+        self.hs = self.C // self.H
+
+
+def param_shapes(cfg):
+    """Ordered reference state_dict keys -> shape (tril buffers excluded).
+
+    Mirrors the module construction order of model.py:288-298, 181-212, 325-337 so the key
+    set equals `MultimodalTransformer(...).state_dict()` minus the `.tril` buffers.
+    """
+    C, H, hs = cfg.C, cfg.H, cfg.hs
+    out = {}
+    for i, V in enumerate(cfg.V):
+        out[f"pre_block.token_embedding_tables.{i}.weight"] = (V, C)
+    out["pre_block.position_embedding_table.weight"] = (cfg.T, C)
+    for l in range(cfg.L):
+        p = f"blocks.{l}."
+        for i in range(cfg.M):
+            for h in range(H):
+                for kind in ("key", "query", "value"):
+                    out[f"{p}sa_layers.{i}.heads.{h}.{kind}.0.weight"] = (hs // 2, C)
+                    out[f"{p}sa_layers.{i}.heads.{h}.{kind}.0.bias"] = (hs // 2,)
+                    out[f"{p}sa_layers.{i}.heads.{h}.{kind}.2.weight"] = (hs, hs // 2)
+            out[f"{p}sa_layers.{i}.proj.0.weight"] = (C // 2, hs * H)
+            out[f"{p}sa_layers.{i}.proj.0.bias"] = (C // 2,)
+            out[f"{p}sa_layers.{i}.proj.2.weight"] = (C, C // 2)
+            out[f"{p}sa_layers.{i}.proj.2.bias"] = (C,)
+        for i in range(cfg.M):
+            out[f"{p}ffwd_layers.{i}.net.0.weight"] = (4 * C, C)
+            out[f"{p}ffwd_layers.{i}.net.0.bias"] = (4 * C,)
+            out[f"{p}ffwd_layers.{i}.net.2.weight"] = (C, 4 * C)
+            out[f"{p}ffwd_layers.{i}.net.2.bias"] = (C,)
+        for i in range(cfg.M):
+            out[f"{p}ln1_layers.{i}.weight"] = (C,)
+            out[f"{p}ln1_layers.{i}.bias"] = (C,)
+        for i in range(cfg.M):
+            out[f"{p}ln2_layers.{i}.weight"] = (C,)
+            out[f"{p}ln2_layers.{i}.bias"] = (C,)
+        for i in range(cfg.M):
+            if cfg.cross[i]:
+                nkv = cfg.M - 1
+                for h in range(H):
+                    out[f"{p}cross_attention_layers.{i}.heads.{h}.query.weight"] = (hs, C)
+                    for j in range(nkv):
+                        out[f"{p}cross_attention_layers.{i}.heads.{h}.kv_projections.{j}.weight"] = (2 * hs, C)
+                out[f"{p}cross_attention_layers.{i}.proj.0.weight"] = (C // 2, hs * H)
+                out[f"{p}cross_attention_layers.{i}.proj.0.bias"] = (C // 2,)
+                out[f"{p}cross_attention_layers.{i}.proj.2.weight"] = (C, C // 2)
+                out[f"{p}cross_attention_layers.{i}.proj.2.bias"] = (C,)
+        for i in range(cfg.M):
+            if cfg.cross[i]:
+                out[f"{p}ln_cross_layers.{i}.weight"] = (C,)
+                out[f"{p}ln_cross_layers.{i}.bias"] = (C,)
+    for i in range(cfg.M):
+        out[f"post_block.fin_norm_layers.{i}.weight"] = (C,)
+        out[f"post_block.fin_norm_layers.{i}.bias"] = (C,)
+    for i, V in enumerate(cfg.V):
+        out[f"post_block.soft_score_layers.{i}.0.weight"] = (V // 2, C)
+        out[f"post_block.soft_score_layers.{i}.0.bias"] = (V // 2,)
+        out[f"post_block.soft_score_layers.{i}.2.weight"] = (V, V // 2)
+        out[f"post_block.soft_score_layers.{i}.2.bias"] = (V,)
+    return out
+
+
+def init_params(cfg, generator=None):
+    """model.py:372-378: Linear/Embedding weights ~ N(0, 0.02), biases 0, LayerNorm 1/0."""
+    sd = {}
+    for k, shp in param_shapes(cfg).items():
+        if "ln" in k.split(".")[-2] or "norm" in k:
+            sd[k] = torch.ones(shp) if k.endswith("weight") else torch.zeros(shp)
+        elif k.endswith("bias"):
+            sd[k] = torch.zeros(shp)
+        else:
+            sd[k] = torch.empty(shp).normal_(0.0, 0.02, generator=generator)
+    return sd
+
+
+# --------------------------------------------------------------------------------------
+# forward (per-head eager restatement)
+# --------------------------------------------------------------------------------------
+def _lin(x, w, b=None):
+    y = x @ w.t()
+    return y + b if b is not None else y
+
+
+def _ln(x, w, b):
+    return F.layer_norm(x, (x.shape[-1],), w, b, 1e-5)
+
+
+def _drop(x, p, training, gen):
+    if not training or p == 0.0:
+        return x
+    return F.dropout(x, p, True)
+
+
+def _head(sd, pre, x, p, training):
+    """model.py:60-73. k/q/v = Linear(C,hs/2)+b -> tanh -> Linear(hs/2,hs, no bias)."""
+    T = x.shape[1]
+    def mlp(kind):
+        h = torch.tanh(_lin(x, sd[f"{pre}{kind}.0.weight"], sd[f"{pre}{kind}.0.bias"]))
+        return _lin(h, sd[f"{pre}{kind}.2.weight"])
+    k = mlp("key")
+    q = mlp("query")
+    aff = q @ k.transpose(-2, -1) * k.shape[-1] ** -0.5
+    tril = torch.tril(torch.ones(T, T))
+    aff = aff.masked_fill(tril == 0, float("-inf"))
+    aff = F.softmax(aff, dim=-1)
+    aff = _drop(aff, p, training, None)
+    v = mlp("value")
+    return aff @ v
+
+
+def _proj(sd, pre, x):
+    """model.py:82-86 / 102-106: Linear(C,C/2)+b -> tanh -> Linear(C/2,C)+b."""
+    h = torch.tanh(_lin(x, sd[f"{pre}proj.0.weight"], sd[f"{pre}proj.0.bias"]))
+    return _lin(h, sd[f"{pre}proj.2.weight"], sd[f"{pre}proj.2.bias"])
+
+
+def _mha(sd, pre, x, cfg, training):
+    """model.py:89-92."""
+    out = torch.cat([_head(sd, f"{pre}heads.{h}.", x, cfg.dropout, training) for h in range(cfg.H)], dim=-1)
+    return _drop(_proj(sd, pre, out), cfg.dropout, training, None)
+
+
+def _cross(sd, pre, qx, kv_list, cfg, training):
+    """model.py:109-159: per head, per KV modality separate causal softmax, outputs summed."""
+    hs = cfg.hs
+    T = qx.shape[1]
+    tril = torch.tril(torch.ones(T, T))
+    heads = []
+    for h in range(cfg.H):
+        hp = f"{pre}heads.{h}."
+        q = _lin(qx, sd[f"{hp}query.weight"])
+        outs = []
+        for j, kvx in enumerate(kv_list):
+            kv = _lin(kvx, sd[f"{hp}kv_projections.{j}.weight"])
+            k, v = kv.split(hs, dim=-1)
+            aff = q @ k.transpose(-2, -1) * k.shape[-1] ** -0.5
+            aff = aff.masked_fill(tril == 0, float("-inf"))
+            aff = F.softmax(aff, dim=-1)
+            aff = _drop(aff, cfg.dropout, training, None)
+            outs.append(aff @ v)
+        heads.append(sum(outs))
+    out = torch.cat(heads, dim=-1)
+    return _drop(_proj(sd, pre, out), cfg.dropout, training, None)
+
+
+def _ffn(sd, pre, x, cfg, training):
+    """model.py:167-175."""
+    h = torch.relu(_lin(x, sd[f"{pre}net.0.weight"], sd[f"{pre}net.0.bias"]))
+    return _drop(_lin(h, sd[f"{pre}net.2.weight"], sd[f"{pre}net.2.bias"]), cfg.dropout, training, None)
+
+
+def _block(sd, l, xs, cfg, training):
+    """model.py:214-244."""
+    p = f"blocks.{l}."
+    att = []
+    for i in range(cfg.M):
+        x = xs[i]
+        x = x + _mha(sd, f"{p}sa_layers.{i}.", _ln(x, sd[f"{p}ln1_layers.{i}.weight"], sd[f"{p}ln1_layers.{i}.bias"]), cfg, training)
+        x = x + _ffn(sd, f"{p}ffwd_layers.{i}.", _ln(x, sd[f"{p}ln2_layers.{i}.weight"], sd[f"{p}ln2_layers.{i}.bias"]), cfg, training)
+        att.append(x)
+    out = []
+    for i in range(cfg.M):
+        x = att[i]
+        others = [j for j in range(cfg.M) if j != i]
+        if cfg.cross[i] and others:
+            kv = [att[j] for j in others]
+            xn = _ln(x, sd[f"{p}ln_cross_layers.{i}.weight"], sd[f"{p}ln_cross_layers.{i}.bias"])
+            x = x + _cross(sd, f"{p}cross_attention_layers.{i}.", xn, kv, cfg, training)
+        out.append(x)
+    return out
+
+
+def forward(sd, cfg, idx_list, targets_list=None, training=False):
+    """model.py:380-402. Returns (logits_list, losses_list | None)."""
+    xs = []
+    for i in range(cfg.M):
+        B, T = idx_list[i].shape
+        tok = sd[f"pre_block.token_embedding_tables.{i}.weight"][idx_list[i]]
+        pos = sd["pre_block.position_embedding_table.weight"][torch.arange(T)]
+        xs.append(tok + pos.expand_as(tok))
+    for l in range(cfg.L):
+        xs = _block(sd, l, xs, cfg, training)
+    logits = []
+    for i in range(cfg.M):
+        x = _ln(xs[i], sd[f"post_block.fin_norm_layers.{i}.weight"], sd[f"post_block.fin_norm_layers.{i}.bias"])
+        h = torch.tanh(_lin(x, sd[f"post_block.soft_score_layers.{i}.0.weight"], sd[f"post_block.soft_score_layers.{i}.0.bias"]))
+        logits.append(_lin(h, sd[f"post_block.soft_score_layers.{i}.2.weight"], sd[f"post_block.soft_score_layers.{i}.2.bias"]))
+    if targets_list is None:
+        return logits, None
+    losses = []
+    for i in range(cfg.M):
+        B, T, V = logits[i].shape
+        losses.append(F.cross_entropy(logits[i].view(B * T, V), targets_list[i].reshape(B * T)))
+    return logits, losses
+
+
+def forward_backward(sd, cfg, idx_list, tgt_list):
+    """One train-step forward + backward of sum(losses) (main.py:642-649). Returns logits,
+    losses and grads (None where the reference leaves .grad None)."""
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
+    logits, losses = forward(leaves, cfg, idx_list, tgt_list, training=False)
+    total = sum(losses)
+    total.backward()
+    grads = {k: (v.grad.detach().clone() if v.grad is not None else None) for k, v in leaves.items()}
+    return [l.detach() for l in logits], [l.detach() for l in losses], grads
+
+
+# --------------------------------------------------------------------------------------
+# AdamW (torch.optim.AdamW defaults; main.py:464, 650)
+# --------------------------------------------------------------------------------------
+def adamw_step(params, grads, state, step, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01):
+    """In-place restatement of torch's single-tensor AdamW (decoupled decay, bias-corrected).
+
+    Params whose grad is None are skipped entirely (no decay, no moment update), as torch does.
+    """
+    b1, b2 = betas
+    for k, p in params.items():
+        g = grads.get(k)
+        if g is None:
+            continue
+        st = state.setdefault(k, {"m": torch.zeros_like(p), "v": torch.zeros_like(p)})
+        p.mul_(1 - lr * weight_decay)
+        st["m"].lerp_(g, 1 - b1)
+        st["v"].mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1 = 1 - b1 ** step
+        bc2 = 1 - b2 ** step
+        step_size = lr / bc1
+        denom = (st["v"].sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(st["m"], denom, value=-step_size)
+
+
+# --------------------------------------------------------------------------------------
+# batching (training_utils.py:33-181, 333-384; data_utils.py:293-358)
+# --------------------------------------------------------------------------------------
+def batch_starting_indices(data_size, block_size, batch_size, split, file_lengths, is_percents, generator=None):
+    """Restates generate_batch_starting_indices, consuming the torch RNG identically."""
+    bxy = block_size + 1
+    off = 1 if is_percents else 0
+    if len(file_lengths) == 1:
+        return torch.randint(off, data_size - bxy + 1, (batch_size,), generator=generator)
+    lens = []
+    acc = 0
+    n = len(file_lengths)
+    for f in range(n):
+        this = file_lengths[f] if split == "train" else file_lengths[n - 1 - f]
+        acc += this
+        if acc <= data_size:
+            lens.append(this)
+        if acc > data_size:
+            lens.append(data_size - (acc - this))
+        if acc >= data_size:
+            if split == "val":
+                lens.reverse()
+            break
+    valid = [max(0, L - bxy - off + 1) for L in lens]
+    total = sum(valid)
+    if total <= 0:
+        raise ValueError("No valid starting positions available for the given block size and file lengths.")
+    init = torch.randint(total, (batch_size,), generator=generator)
+    out = torch.empty(batch_size, dtype=torch.long)
+    for i in range(batch_size):
+        cum = 0
+        for k, L in enumerate(lens):
+            if init[i] < cum + valid[k]:
+                out[i] = sum(lens[:k]) + (init[i] - cum) + off
+                break
+            cum += valid[k]
+    return out
+
+
+def jitter_inplace(data, rand_size, vocab_size, rng=random):
+    """add_rand_to_data_points: x += choice({0,±1..±r}) where r < x < V - r, in place."""
+    r = int(rand_size)
+    choices = [0]
+    for a in range(r):
+        choices.extend([a + 1, -(a + 1)])
+    mx = max(choices)
+    for n in range(len(data)):
+        if mx < data[n] < vocab_size - mx:
+            data[n] += rng.choice(choices)
+    return data
+
+
+def direction_sign(cur, prev, is_pct):
+    """training_utils.py:184-212."""
+    if is_pct:
+        return 1 if cur > 0 else (-1 if cur < 0 else 0)
+    if not isinstance(prev, numbers.Number):
+        return None
+    ch = cur - prev
+    return 1 if ch > 0 else (-1 if ch < 0 else 0)
+
+
+def eval_metrics(logits_list, xb_list, yb_list, vocabs, is_pct_list):
+    """calculate_evaluation_metrics (training_utils.py:215-330): per-modality
+    (wins, losses, certainty_sum, processed)."""
+    M = len(vocabs)
+    wins, losses, cert, proc = [0] * M, [0] * M, [0.0] * M, [0] * M
+    for i in range(M):
+        vocab = vocabs[i]
+        pct = bool(is_pct_list[i])
+        numeric = all(isinstance(v, numbers.Number) for v in vocab)
+        min_len = 1 if pct else 2
+        if not (numeric and yb_list[i].ndim >= 2 and yb_list[i].shape[1] >= min_len):
+            continue
+        lg = logits_list[i][:, -1, :]
+        tg = yb_list[i][:, -1]
+        if tg.shape[0] == 0:
+            continue
+        proc[i] = 1
+        for j in range(lg.shape[0]):
+            pi = int(torch.argmax(lg[j]).item())
+            pv = vocab[pi]
+            av = vocab[int(tg[j].item())]
+            prev = None
+            if not pct and xb_list[i].shape[1] >= 1:
+                prev = vocab[int(xb_list[i][j, -1].item())]
+            ps = direction_sign(pv, prev, pct)
+            as_ = direction_sign(av, prev, pct)
+            if ps is not None and as_ is not None:
+                if ps == as_:
+                    wins[i] += 1
+                else:
+                    losses[i] += 1
+                probs = F.softmax(lg[j], dim=-1)
+                s = 0.0
+                for ti, tv in enumerate(vocab):
+                    if isinstance(tv, numbers.Number):
+                        d = direction_sign(tv, prev, pct)
+                        if d is not None and d == ps:
+                            s += probs[ti].item()
+                cert[i] += s
+    return wins, losses, cert, proc

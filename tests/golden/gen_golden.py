@@ -1,0 +1,225 @@
+"""Generate golden fixtures by importing the REFERENCE implementation (this container only).
+
+Runs ONLY in the build container where /root/reference exists. It copies the reference to a
+scratch directory under /tmp, imports its `model.py` / `training_utils.py` / `data_utils.py`,
+injects the config through `config_utils._config_cache` (reference config_utils.py:8-24),
+seeds torch + random, and dumps small .npz fixtures next to this script. Only the fixtures
+(inputs and expected outputs) are committed; no reference source travels.
+
+Fixtures:
+  f_demo   C=32 H=4 L=2 T=4  M=2 V=[57,3]          cross=[T,F]   B=4   (demo dims, C0)
+  f_small  C=64 H=4 L=2 T=32 M=4 V=[57,13,24,5]    cross=[T,F,T,F] B=4
+  f_hs32   C=64 H=2 L=1 T=64  M=4 V=[57,13,24,5]   cross=[T,F,F,F] B=2  (production head size 32)
+  f_m1     C=32 H=4 L=1 T=8  M=1 V=[11]            cross=[T]     B=3   (CA built but unused)
+  f_tiny_v C=32 H=2 L=1 T=8  M=3 V=[2,1,7]         cross=[F,T,F] B=2   (V//2 = 1 and 0)
+
+For each: state_dict (fp32), idx/tgt, logits, per-modality losses, grads of sum(losses),
+and params after 1 and 3 AdamW steps (lr=1e-3, torch defaults) on the same batch.
+Plus: eval-metric fixtures (calculate_evaluation_metrics) and batch-index fixtures
+(generate_batch_starting_indices) with a seeded torch generator.
+
+Usage:  python tests/golden/gen_golden.py
+"""
+import json
+import os
+import random
+import shutil
+import sys
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+SCRATCH = "/tmp/mmt_ref_golden"
+
+
+def _import_reference():
+    if os.path.exists(SCRATCH):
+        shutil.rmtree(SCRATCH)
+    shutil.copytree(REF, SCRATCH)
+    sys.path.insert(0, SCRATCH)
+    import torch  # noqa: F401
+    import config_utils
+    return config_utils
+
+
+CONFIGS = {
+    "f_demo": dict(n_embd=32, n_head=4, n_layer=2, block_size=4, V=[57, 3], cross=[True, False], B=4),
+    "f_small": dict(n_embd=64, n_head=4, n_layer=2, block_size=32, V=[57, 13, 24, 5],
+                    cross=[True, False, True, False], B=4, steps=False),
+    "f_hs32": dict(n_embd=64, n_head=2, n_layer=1, block_size=64, V=[57, 13, 24, 5],
+                   cross=[True, False, False, False], B=2, steps=False),
+    "f_m1": dict(n_embd=32, n_head=4, n_layer=1, block_size=8, V=[11], cross=[True], B=3),
+    "f_tiny_v": dict(n_embd=32, n_head=2, n_layer=1, block_size=8, V=[2, 1, 7], cross=[False, True, False], B=2),
+}
+
+
+def _params_list(cfg):
+    # legacy 12-element list layout (reference schema.py:207-250); index 8 = cross_attention
+    out = []
+    for i, v in enumerate(cfg["V"]):
+        p = [None] * 12
+        p[2] = True
+        p[3] = False
+        p[8] = cfg["cross"][i]
+        p[9] = f"mod{i}"
+        out.append(p)
+    return out
+
+
+def gen_model_fixture(config_utils, name, cfg, seed=1234):
+    import torch
+    import importlib
+    config_utils._config_cache = {
+        "n_embd": cfg["n_embd"], "n_head": cfg["n_head"], "n_layer": cfg["n_layer"],
+        "block_size": cfg["block_size"], "dropout": 0.0, "device": "cpu",
+        "batch_size": cfg["B"], "eval_iters": 1,
+    }
+    import model as ref_model
+    importlib.reload(ref_model)
+    torch.manual_seed(seed)
+    random.seed(seed)
+    torch.set_num_threads(1)
+    M = len(cfg["V"])
+    m = ref_model.MultimodalTransformer(M, list(cfg["V"]), _params_list(cfg))
+    sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    B, T = cfg["B"], cfg["block_size"]
+    g = torch.Generator().manual_seed(seed + 1)
+    idx = [torch.randint(0, v, (B, T), generator=g) for v in cfg["V"]]
+    tgt = [torch.randint(0, v, (B, T), generator=g) for v in cfg["V"]]
+
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    out = {}
+    for step in range(3):
+        logits, losses = m(idx, tgt)
+        total = sum(losses)
+        opt.zero_grad(set_to_none=True)
+        total.backward()
+        if step == 0:
+            for i in range(M):
+                out[f"logits.{i}"] = logits[i].detach().numpy()
+            out["losses"] = np.array([l.item() for l in losses], dtype=np.float32)
+            for k, p in m.named_parameters():
+                if p.grad is not None:
+                    out[f"grad.{k}"] = p.grad.detach().numpy().copy()
+        opt.step()
+        if step == 0 and cfg.get("steps", True):
+            for k, v in m.state_dict().items():
+                if not k.endswith("tril"):
+                    out[f"after1.{k}"] = v.detach().numpy().copy()
+        if step == 2 and cfg.get("steps", True):
+            for k, v in m.state_dict().items():
+                if not k.endswith("tril"):
+                    out[f"after3.{k}"] = v.detach().numpy().copy()
+        if step == 2:
+            with torch.no_grad():
+                _, losses3 = m(idx, tgt)
+            out["losses_after3"] = np.array([l.item() for l in losses3], dtype=np.float32)
+    for k, v in sd0.items():
+        if not k.endswith("tril"):
+            out[f"param.{k}"] = v.numpy()
+    for i in range(M):
+        out[f"idx.{i}"] = idx[i].numpy()
+        out[f"tgt.{i}"] = tgt[i].numpy()
+    meta = dict(cfg)
+    meta["state_dict_keys"] = list(sd0.keys())
+    meta["state_dict_shapes"] = {k: list(v.shape) for k, v in sd0.items()}
+    meta["grad_none"] = [k for k, p in m.named_parameters() if p.grad is None]
+    meta["seed"] = seed
+    out["meta_json"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, "losses", out["losses"], "params", sum(v.numel() for k, v in sd0.items() if not k.endswith("tril")))
+
+
+def gen_metric_fixture(seed=77):
+    """calculate_evaluation_metrics (reference training_utils.py:215-330)."""
+    import torch
+    import training_utils as tu
+    torch.manual_seed(seed)
+    B, T = 16, 6
+    cases = []
+    # value modality (non-percent), numeric vocab incl. duplicates of direction; percent modality; non-numeric
+    vocab0 = [round(1.0 + 0.5 * i, 1) for i in range(9)]           # value data
+    vocab1 = [-2.0, -1.0, -0.5, 0.0, 0.5, 1.0, 2.0]                 # percent data
+    vocab2 = ["a", "b", "c"]                                         # non-numeric -> skipped
+    vocabs = [vocab0, vocab1, vocab2]
+    params = []
+    for i, pct in enumerate([False, True, False]):
+        p = [None] * 12
+        p[3] = pct
+        p[9] = f"m{i}"
+        params.append(p)
+    logits = [torch.randn(B, T, len(v)) for v in vocabs]
+    # force argmax ties on a few rows of modality 0 (first max must win)
+    logits[0][0, -1, :] = 0.0
+    logits[0][1, -1, 2] = 5.0
+    logits[0][1, -1, 6] = 5.0
+    xb = [torch.randint(0, len(v), (B, T)) for v in vocabs]
+    yb = [torch.randint(0, len(v), (B, T)) for v in vocabs]
+    # flat direction cases: prev == actual
+    yb[0][2, -1] = xb[0][2, -1]
+    wins, losses, cert, proc = tu.calculate_evaluation_metrics(logits, xb, yb, 3, vocabs, params, None)
+    out = {}
+    for i in range(3):
+        out[f"logits.{i}"] = logits[i].numpy()
+        out[f"xb.{i}"] = xb[i].numpy()
+        out[f"yb.{i}"] = yb[i].numpy()
+    out["wins"] = np.array(wins)
+    out["losses"] = np.array(losses)
+    out["certainty"] = np.array(cert, dtype=np.float64)
+    out["processed"] = np.array(proc)
+    out["vocab.0"] = np.array(vocab0)
+    out["vocab.1"] = np.array(vocab1)
+    meta = {"percent": [False, True, False], "numeric": [True, True, False], "vocab2": vocab2}
+    out["meta_json"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "eval_metrics.npz"), **out)
+    print("metrics", wins, losses, cert, proc)
+
+
+def gen_index_fixture(seed=99):
+    """generate_batch_starting_indices (reference training_utils.py:33-181) under a seeded torch RNG."""
+    import torch
+    import training_utils as tu
+    cases = [
+        dict(data_size=900, block_size=16, batch_size=32, split="train", file_lengths=[1000], is_percents=False),
+        dict(data_size=9000, block_size=32, batch_size=64, split="train",
+             file_lengths=[1000] * 10, is_percents=True),
+        dict(data_size=1000, block_size=32, batch_size=64, split="val",
+             file_lengths=[1000] * 10, is_percents=True),
+        dict(data_size=2500, block_size=8, batch_size=50, split="val",
+             file_lengths=[700, 300, 1200, 900, 400], is_percents=False),
+        dict(data_size=2100, block_size=8, batch_size=50, split="train",
+             file_lengths=[700, 300, 1200, 900, 400], is_percents=True),
+    ]
+    out = {}
+    for ci, c in enumerate(cases):
+        torch.manual_seed(seed + ci)
+        ix = tu.generate_batch_starting_indices(c["data_size"], c["block_size"], c["batch_size"], c["split"],
+                                                c["file_lengths"], c["is_percents"])
+        out[f"ix.{ci}"] = ix.numpy()
+    meta = {"cases": cases, "seed": seed}
+    out["meta_json"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "batch_indices.npz"), **out)
+    print("indices", [out[f"ix.{i}"][:4] for i in range(len(cases))])
+
+
+def gen_jitter_fixture(seed=5):
+    """add_rand_to_data_points (reference data_utils.py:293-358) with rand_size=True (the has_header quirk)."""
+    import data_utils as du
+    random.seed(seed)
+    data = [int(x) for x in np.random.RandomState(seed).randint(0, 12, size=400)]
+    before = list(data)
+    after = du.add_rand_to_data_points(data, True, 12)
+    out = {"before": np.array(before), "after": np.array(after)}
+    np.savez_compressed(os.path.join(HERE, "jitter.npz"), **out)
+    d = np.array(after) - np.array(before)
+    print("jitter changed", int((d != 0).sum()), "of", len(d))
+
+
+if __name__ == "__main__":
+    cu = _import_reference()
+    for name, cfg in CONFIGS.items():
+        gen_model_fixture(cu, name, cfg)
+    gen_metric_fixture()
+    gen_index_fixture()
+    gen_jitter_fixture()

@@ -1,0 +1,347 @@
+"""Kernel-level parity: each HIP kernel (through the C-ABI mmt_op_* entry points) against a plain
+PyTorch fp32 reference of the same op on the same bf16-rounded inputs.
+
+Tolerances: fp32 outputs of bf16 MFMA products accumulate exactly-representable products in fp32,
+so they match an fp32 reference to ~1e-5 relative; bf16 outputs carry one bf16 rounding
+(rel 2^-8 = 3.9e-3) on top.
+"""
+import ctypes
+
+import pytest
+import torch
+
+import mmt_lib as ML
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _s():
+    return ML.stream_ptr()
+
+
+def _sync():
+    torch.cuda.synchronize()
+
+
+def rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def bf(t):
+    return t.to(torch.bfloat16).contiguous()
+
+
+def pad_cols(t, ld):
+    out = torch.zeros(t.shape[0], ld, dtype=t.dtype, device=t.device)
+    out[:, : t.shape[1]] = t
+    return out
+
+
+def r8(x):
+    return max(8, (x + 7) // 8 * 8)
+
+
+# ------------------------------------------------------------------------------------- GEMM
+GEMM_SHAPES = [(256, 128, 64), (200, 136, 72), (33, 17, 45), (128, 450, 256), (5, 900, 450), (16384 // 64, 384, 256)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("epi", ["store_bf16", "bias_tanh_bf16", "bias_relu_bf16", "bias_resid_f32", "store_f32"])
+def test_gemm_forward_linear(M, N, K, epi):
+    torch.manual_seed(M * 7 + N + K)
+    lda, ldb = r8(K), r8(K)
+    X = torch.randn(M, K, device=DEV)
+    W = torch.randn(N, K, device=DEV) * 0.1
+    bias = torch.randn(N, device=DEV)
+    resid = torch.randn(M, N, device=DEV)
+    Xb, Wb = bf(pad_cols(X, lda)), bf(pad_cols(W, ldb))
+    ref = Xb.float()[:, :K] @ Wb.float()[:, :K].t()
+    ldc = N
+    ldo16 = r8(N)
+    o32 = torch.zeros(M, ldc, device=DEV)
+    o16 = torch.zeros(M, ldo16, dtype=torch.bfloat16, device=DEV)
+    use_bias = epi != "store_bf16"
+    rc = ML.lib().mmt_op_gemm(_s(), 1, 1, ML.EPI[epi], 1, M, N, K, ML.ptr(Xb), lda, ML.ptr(Wb), ldb,
+                              ML.ptr(bias) if use_bias else None, None, 0, ML.ptr(resid), N, ML.ptr(o32), ldc,
+                              ML.ptr(o16), ldo16, 1.0)
+    assert rc == 0
+    _sync()
+    if use_bias:
+        ref = ref + bias
+    if epi == "bias_tanh_bf16":
+        assert rel(o16[:, :N], torch.tanh(ref)) < 1e-2
+    elif epi == "bias_relu_bf16":
+        assert rel(o16[:, :N], torch.relu(ref)) < 1e-2
+    elif epi == "store_bf16":
+        assert rel(o16[:, :N], ref) < 1e-2
+    elif epi == "bias_resid_f32":
+        assert rel(o32, ref + resid) < 1e-5
+    else:
+        assert rel(o32, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 72, 136), (64, 450, 900), (33, 45, 17)])
+@pytest.mark.parametrize("epi", ["dtanh_bf16", "drelu_bf16", "store_f32", "acc_f32", "store_bf16"])
+def test_gemm_backward_data(M, N, K, epi):
+    # dX[M, N] = dY[M, K] @ W[K, N]  (W stored [K rows][N cols], N contiguous)
+    torch.manual_seed(M + 3 * N + K)
+    lda, ldb = r8(K), r8(N)
+    dY = torch.randn(M, K, device=DEV)
+    W = torch.randn(K, N, device=DEV) * 0.1
+    aux = torch.tanh(torch.randn(M, N, device=DEV)) if epi != "drelu_bf16" else torch.randn(M, N, device=DEV)
+    dYb, Wb = bf(pad_cols(dY, lda)), bf(pad_cols(W, ldb))
+    auxb = bf(pad_cols(aux, r8(N)))
+    ref = 0.5 * (dYb.float()[:, :K] @ Wb.float()[:, :N])
+    o32 = torch.randn(M, N, device=DEV)
+    base = o32.clone()
+    o16 = torch.zeros(M, r8(N), dtype=torch.bfloat16, device=DEV)
+    rc = ML.lib().mmt_op_gemm(_s(), 1, 0, ML.EPI[epi], 1, M, N, K, ML.ptr(dYb), lda, ML.ptr(Wb), ldb, None,
+                              ML.ptr(auxb), r8(N), None, 0, ML.ptr(o32), N, ML.ptr(o16), r8(N), 0.5)
+    assert rc == 0
+    _sync()
+    a = auxb.float()[:, :N]
+    if epi == "dtanh_bf16":
+        assert rel(o16[:, :N], ref * (1 - a * a)) < 1e-2
+    elif epi == "drelu_bf16":
+        assert rel(o16[:, :N], ref * (a > 0)) < 1e-2
+    elif epi == "store_bf16":
+        assert rel(o16[:, :N], ref) < 1e-2
+    elif epi == "store_f32":
+        assert rel(o32, ref) < 1e-5
+    else:
+        assert rel(o32, base + ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,R", [(384, 256, 4096), (1024, 256, 2048), (900, 450, 1000), (6, 32, 300), (32, 16, 77)])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_gemm_weight_grad(M, N, R, splits):
+    # dW[M, N] += alpha * dY[R, M]^T @ X[R, N]
+    torch.manual_seed(M + N + R + splits)
+    lda, ldb = r8(M), r8(N)
+    dY = torch.randn(R, M, device=DEV)
+    X = torch.randn(R, N, device=DEV)
+    dYb, Xb = bf(pad_cols(dY, lda)), bf(pad_cols(X, ldb))
+    ref = 0.25 * (dYb.float()[:, :M].t() @ Xb.float()[:, :N])
+    out = torch.ones(M, N, device=DEV)
+    rc = ML.lib().mmt_op_gemm(_s(), 0, 0, ML.EPI["atomic_f32"], splits, M, N, R, ML.ptr(dYb), lda, ML.ptr(Xb), ldb,
+                              None, None, 0, None, 0, ML.ptr(out), N, None, 0, 0.25)
+    assert rc == 0
+    _sync()
+    assert rel(out - 1.0, ref) < 1e-5
+
+
+def test_gemm_identity_asymmetric():
+    # A = I with an asymmetric B catches a transposed C write (guide §3)
+    n = 64
+    A = torch.eye(n, device=DEV)
+    Bm = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n) % 17 - 8
+    o32 = torch.zeros(n, n, device=DEV)
+    rc = ML.lib().mmt_op_gemm(_s(), 1, 1, ML.EPI["store_f32"], 1, n, n, n, ML.ptr(bf(A)), n, ML.ptr(bf(Bm)), n, None,
+                              None, 0, None, 0, ML.ptr(o32), n, None, 0, 1.0)
+    assert rc == 0
+    _sync()
+    torch.testing.assert_close(o32, Bm.t().contiguous())
+
+
+# --------------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("R,C", [(1000, 256), (37, 32), (64, 512), (16, 1024), (9, 64)])
+def test_layernorm(R, C):
+    torch.manual_seed(R + C)
+    x = torch.randn(R, C, device=DEV) * 3 + 1
+    g = torch.randn(C, device=DEV)
+    b = torch.randn(C, device=DEV)
+    y = torch.empty(R, C, dtype=torch.bfloat16, device=DEV)
+    mean = torch.empty(R, device=DEV)
+    rstd = torch.empty(R, device=DEV)
+    L = ML.lib()
+    assert L.mmt_op_layernorm_fwd(_s(), R, C, ML.ptr(x), ML.ptr(g), ML.ptr(b), ML.ptr(y), ML.ptr(mean), ML.ptr(rstd)) == 0
+    xr = x.clone().requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xr, (C,), gr, br, 1e-5)
+    _sync()
+    assert rel(y, ref) < 1e-2
+    dy = torch.randn(R, C, device=DEV)
+    ref.backward(dy)
+    dx = torch.ones(R, C, device=DEV)
+    dx16 = torch.empty(R, C, dtype=torch.bfloat16, device=DEV)
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    assert L.mmt_op_layernorm_bwd(_s(), R, C, ML.ptr(x), ML.ptr(g), ML.ptr(mean), ML.ptr(rstd), ML.ptr(dy), ML.ptr(dx),
+                                  ML.ptr(dx16), ML.ptr(dg), ML.ptr(db)) == 0
+    _sync()
+    assert rel(dx - 1.0, xr.grad) < 1e-5
+    assert rel(dx16, dx) < 1e-2
+    assert rel(dg, gr.grad) < 1e-5
+    assert rel(db, br.grad) < 1e-5
+
+
+# --------------------------------------------------------------------------------- attention
+def _attn_ref(q, ks, vs, scale):
+    # q [B,H,T,hs], ks/vs list of [B,H,T,hs]; sum over streams of causal softmax attention
+    T = q.shape[2]
+    mask = torch.tril(torch.ones(T, T, device=q.device)) == 0
+    out = 0
+    for k, v in zip(ks, vs):
+        a = (q @ k.transpose(-1, -2)) * scale
+        a = a.masked_fill(mask, float("-inf"))
+        out = out + torch.softmax(a, -1) @ v
+    return out
+
+
+@pytest.mark.parametrize("B,T,H,hs,ns", [(2, 64, 2, 32, 1), (3, 37, 4, 16, 1), (2, 4, 4, 8, 1), (2, 100, 2, 64, 1),
+                                         (2, 64, 2, 32, 3), (1, 45, 3, 16, 2), (2, 256, 8, 32, 1), (1, 96, 2, 48, 2)])
+def test_attention_fwd_bwd(B, T, H, hs, ns):
+    torch.manual_seed(B * 1000 + T * 10 + hs + ns)
+    C = H * hs
+    R = B * T
+    # self-attention layout: q/k/v interleaved in one [R, 3C] buffer (engine layout) when ns == 1,
+    # cross-attention layout: q [R, C], per-stream kv [R, 2C] with per-head [K|V] otherwise
+    if ns == 1:
+        qkv = bf(torch.randn(R, 3 * C, device=DEV))
+        q, q_ld = qkv[:, C:], 3 * C
+        ks, vs = [qkv[:, :C]], [qkv[:, 2 * C:]]
+        kv_ld, kv_hs = 3 * C, hs
+        kptr, vptr = [qkv], [qkv[:, 2 * C:]]
+    else:
+        qb = bf(torch.randn(R, C, device=DEV))
+        q, q_ld = qb, C
+        kvs = [bf(torch.randn(R, 2 * C, device=DEV)) for _ in range(ns)]
+        ks = [kv.view(R, H, 2 * hs)[:, :, :hs].reshape(R, C) for kv in kvs]
+        vs = [kv.view(R, H, 2 * hs)[:, :, hs:].reshape(R, C) for kv in kvs]
+        kv_ld, kv_hs = 2 * C, 2 * hs
+        kptr, vptr = kvs, [kv[:, hs:] for kv in kvs]
+
+    def heads(x):
+        return x.float().reshape(B, T, H, hs).permute(0, 2, 1, 3)
+
+    scale = hs ** -0.5
+    qf = heads(q).requires_grad_(True)
+    kf = [heads(k).requires_grad_(True) for k in ks]
+    vf = [heads(v).requires_grad_(True) for v in vs]
+    ref = _attn_ref(qf, kf, vf, scale)
+    o = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
+    oj = [torch.zeros(R, C, dtype=torch.bfloat16, device=DEV) for _ in range(ns)]
+    lse = [torch.zeros(B * H * T, device=DEV) for _ in range(ns)]
+    L = ML.lib()
+    kp = (ctypes.c_void_p * ns)(*[t.data_ptr() for t in kptr])
+    vp = (ctypes.c_void_p * ns)(*[t.data_ptr() for t in vptr])
+    rc = L.mmt_op_attention_fwd(_s(), B, T, H, hs, ns, ML.ptr(q), q_ld, kp, vp, kv_ld, kv_hs, ML.ptr(o), C,
+                                ML.ptr_array(oj), ML.ptr_array(lse))
+    assert rc == 0
+    _sync()
+    out = o.float().reshape(B, T, H, hs).permute(0, 2, 1, 3)
+    assert rel(out, ref) < 1e-2, rel(out, ref)
+    # backward
+    do = bf(torch.randn(R, C, device=DEV))
+    ref.backward(heads(do))
+    dq = torch.zeros(R, C, dtype=torch.bfloat16, device=DEV)
+    if ns == 1:
+        dqkv = torch.zeros(R, 3 * C, dtype=torch.bfloat16, device=DEV)
+        dq_ptr, dq_ld = dqkv[:, C:], 3 * C
+        dkp, dvp = [dqkv], [dqkv[:, 2 * C:]]
+        dkv_ld, dkv_hs = 3 * C, hs
+    else:
+        dkvs = [torch.zeros(R, 2 * C, dtype=torch.bfloat16, device=DEV) for _ in range(ns)]
+        dq_ptr, dq_ld = dq, C
+        dkp, dvp = dkvs, [d[:, hs:] for d in dkvs]
+        dkv_ld, dkv_hs = 2 * C, 2 * hs
+    dvec = [torch.zeros(B * H * T, device=DEV) for _ in range(ns)]
+    rc = L.mmt_op_attention_bwd(_s(), B, T, H, hs, ns, ML.ptr(q), q_ld, kp, vp, kv_ld, kv_hs, ML.ptr(o), C,
+                                ML.ptr_array(oj), ML.ptr_array(lse), ML.ptr(do), C, ML.ptr_array(dvec), ML.ptr(dq_ptr),
+                                dq_ld, (ctypes.c_void_p * ns)(*[t.data_ptr() for t in dkp]),
+                                (ctypes.c_void_p * ns)(*[t.data_ptr() for t in dvp]), dkv_ld, dkv_hs)
+    assert rc == 0
+    _sync()
+    if ns == 1:
+        got_q = dqkv[:, C:2 * C]
+        got_k = [dqkv[:, :C]]
+        got_v = [dqkv[:, 2 * C:]]
+    else:
+        got_q = dq
+        got_k = [d.view(R, H, 2 * hs)[:, :, :hs].reshape(R, C) for d in dkvs]
+        got_v = [d.view(R, H, 2 * hs)[:, :, hs:].reshape(R, C) for d in dkvs]
+    assert rel(heads(got_q), qf.grad) < 2e-2, rel(heads(got_q), qf.grad)
+    for j in range(ns):
+        assert rel(heads(got_k[j]), kf[j].grad) < 2e-2, (j, rel(heads(got_k[j]), kf[j].grad))
+        assert rel(heads(got_v[j]), vf[j].grad) < 2e-2, (j, rel(heads(got_v[j]), vf[j].grad))
+
+
+# ------------------------------------------------------------------------------ small kernels
+@pytest.mark.parametrize("R,H,hs", [(1000, 8, 32), (77, 4, 16), (300, 2, 64), (50, 4, 8)])
+def test_qkv2(R, H, hs):
+    torch.manual_seed(R + H + hs)
+    nblk, hh = 3 * H, hs // 2
+    ld_h1, ld_out = r8(nblk * hh), nblk * hs
+    h1 = torch.tanh(torch.randn(R, nblk * hh, device=DEV))
+    h1b = bf(pad_cols(h1, ld_h1))
+    w2 = torch.randn(nblk, hs, hh, device=DEV) * 0.2
+    out = torch.zeros(R, ld_out, dtype=torch.bfloat16, device=DEV)
+    L = ML.lib()
+    assert L.mmt_op_qkv2_fwd(_s(), R, nblk, hs, ML.ptr(h1b), ld_h1, ML.ptr(w2), ML.ptr(out), ld_out) == 0
+    hin = h1b.float()[:, : nblk * hh].view(R, nblk, hh).requires_grad_(True)
+    wr = w2.clone().requires_grad_(True)
+    ref = torch.einsum("rbi,boi->rbo", hin, wr)
+    _sync()
+    assert rel(out.view(R, nblk, hs), ref) < 1e-2
+    dout = bf(torch.randn(R, ld_out, device=DEV))
+    dh1 = torch.zeros(R, ld_h1, dtype=torch.bfloat16, device=DEV)
+    dw2 = torch.zeros_like(w2)
+    assert L.mmt_op_qkv2_bwd(_s(), R, nblk, hs, ML.ptr(h1b), ld_h1, ML.ptr(w2), ML.ptr(dout), ld_out, ML.ptr(dh1),
+                             ML.ptr(dw2)) == 0
+    ref.backward(dout.float().view(R, nblk, hs))
+    _sync()
+    hv = hin.detach()
+    assert rel(dh1[:, : nblk * hh].view(R, nblk, hh), hin.grad * (1 - hv * hv)) < 1e-2
+    assert rel(dw2, wr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("R,N,ld", [(16384, 1024, 1024), (1000, 450, 456), (77, 13, 16), (300, 6, 8)])
+def test_colsum(R, N, ld):
+    x = bf(torch.randn(R, ld, device=DEV))
+    out = torch.full((N,), 2.0, device=DEV)
+    assert ML.lib().mmt_op_colsum(_s(), R, N, ML.ptr(x), ld, ML.ptr(out), 0.5) == 0
+    _sync()
+    assert rel(out - 2.0, 0.5 * x.float()[:, :N].sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("R,V", [(1000, 900), (77, 13), (64, 2), (33, 1), (500, 144)])
+def test_cross_entropy(R, V):
+    torch.manual_seed(R + V)
+    logits = torch.randn(R, V, device=DEV) * 2
+    tgt = torch.randint(0, V, (R,), device=DEV)
+    ld = r8(V)
+    dl = torch.full((R, ld), 7.0, dtype=torch.bfloat16, device=DEV)
+    loss = torch.zeros(1, device=DEV)
+    assert ML.lib().mmt_op_cross_entropy(_s(), R, V, ML.ptr(logits), ML.ptr(tgt), ML.ptr(dl), ld, ML.ptr(loss)) == 0
+    lr = logits.clone().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr, tgt)
+    ref.backward()
+    _sync()
+    torch.testing.assert_close(loss[0], ref.detach(), rtol=1e-5, atol=1e-5)
+    assert rel(dl[:, :V].float() / R, lr.grad) < 1e-2
+    assert (dl[:, V:].float() == 0).all()
+
+
+@pytest.mark.parametrize("B,T,C,V", [(4, 32, 64, 57), (2, 256, 256, 900), (3, 4, 32, 3)])
+def test_embedding(B, T, C, V):
+    torch.manual_seed(B + T + C + V)
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    tok = torch.randn(V, C, device=DEV)
+    pos = torch.randn(T, C, device=DEV)
+    x = torch.empty(B * T, C, device=DEV)
+    L = ML.lib()
+    assert L.mmt_op_embedding_fwd(_s(), B, T, C, V, ML.ptr(idx), ML.ptr(tok), ML.ptr(pos), ML.ptr(x)) == 0
+    _sync()
+    torch.testing.assert_close(x.view(B, T, C), tok[idx] + pos[None])
+    dx = torch.randn(B * T, C, device=DEV)
+    dtok = torch.zeros(V, C, device=DEV)
+    dpos = torch.zeros(T, C, device=DEV)
+    assert L.mmt_op_embedding_bwd(_s(), B, T, C, V, ML.ptr(idx), ML.ptr(dx), ML.ptr(dtok), ML.ptr(dpos)) == 0
+    _sync()
+    ref_tok = torch.zeros(V, C, device=DEV).index_add_(0, idx.view(-1), dx)
+    torch.testing.assert_close(dtok, ref_tok, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dpos, dx.view(B, T, C).sum(0), rtol=1e-5, atol=1e-5)

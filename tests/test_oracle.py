@@ -1,0 +1,98 @@
+"""Pin the CPU oracle (oracle/mmt_oracle.py) against golden vectors produced by the reference.
+
+These run on CPU (`-m "not gpu"`). Tolerances are fp32-restatement tolerances: the oracle
+computes the same math as the reference in the same fp32 precision but in a different op
+order (functional ops instead of nn.Modules), so agreement is to a few ulps.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import mmt_oracle as O
+from golden_io import MODEL_FIXTURES, load, model_fixture
+
+torch.set_num_threads(1)
+
+
+@pytest.mark.parametrize("name", MODEL_FIXTURES)
+def test_state_dict_keys_match_reference(name):
+    z, meta, cfg, sd, idx, tgt = model_fixture(name)
+    ref_keys = [k for k in meta["state_dict_keys"] if not k.endswith("tril")]
+    shapes = O.param_shapes(cfg)
+    assert sorted(shapes.keys()) == sorted(ref_keys)
+    for k in ref_keys:
+        assert list(shapes[k]) == meta["state_dict_shapes"][k], k
+
+
+@pytest.mark.parametrize("name", MODEL_FIXTURES)
+def test_forward_backward_matches_reference(name):
+    z, meta, cfg, sd, idx, tgt = model_fixture(name)
+    logits, losses, grads = O.forward_backward(sd, cfg, idx, tgt)
+    for i in range(cfg.M):
+        ref = torch.from_numpy(z[f"logits.{i}"])
+        torch.testing.assert_close(logits[i], ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.stack(losses), torch.from_numpy(z["losses"]), rtol=1e-6, atol=1e-6)
+    none_ref = set(meta["grad_none"])
+    for k, g in grads.items():
+        if k in none_ref:
+            assert g is None, k
+            continue
+        ref = torch.from_numpy(z[f"grad.{k}"])
+        torch.testing.assert_close(g, ref, rtol=1e-4, atol=1e-7, msg=lambda m: f"{k}: {m}")
+
+
+@pytest.mark.parametrize("name", [n for n in MODEL_FIXTURES if n not in ("f_small", "f_hs32")])
+def test_adamw_steps_match_reference(name):
+    z, meta, cfg, sd, idx, tgt = model_fixture(name)
+    params = {k: v.clone() for k, v in sd.items()}
+    state = {}
+    for step in range(1, 4):
+        _, _, grads = O.forward_backward(params, cfg, idx, tgt)
+        O.adamw_step(params, grads, state, step, lr=1e-3)
+        tag = {1: "after1", 3: "after3"}.get(step)
+        if tag:
+            for k, p in params.items():
+                ref = torch.from_numpy(z[f"{tag}.{k}"])
+                torch.testing.assert_close(p, ref, rtol=1e-5, atol=2e-6, msg=lambda m: f"{tag} {k}: {m}")
+    _, losses = O.forward(params, cfg, idx, tgt)
+    torch.testing.assert_close(torch.stack(losses), torch.from_numpy(z["losses_after3"]), rtol=1e-5, atol=1e-6)
+
+
+def test_unused_cross_attention_params_not_decayed():
+    # M=1 with cross=True: CrossAttention is built but never called (model.py:198-200, 238)
+    z, meta, cfg, sd, idx, tgt = model_fixture("f_m1")
+    assert any("cross_attention_layers" in k for k in meta["grad_none"])
+    for k in meta["grad_none"]:
+        np.testing.assert_array_equal(z[f"after3.{k}"], z[f"param.{k}"])
+
+
+def test_eval_metrics_match_reference():
+    z, meta = load("eval_metrics")
+    vocabs = [list(z["vocab.0"]), list(z["vocab.1"]), meta["vocab2"]]
+    vocabs[0] = [float(v) for v in vocabs[0]]
+    vocabs[1] = [float(v) for v in vocabs[1]]
+    logits = [torch.from_numpy(z[f"logits.{i}"]) for i in range(3)]
+    xb = [torch.from_numpy(z[f"xb.{i}"]) for i in range(3)]
+    yb = [torch.from_numpy(z[f"yb.{i}"]) for i in range(3)]
+    w, l, c, p = O.eval_metrics(logits, xb, yb, vocabs, meta["percent"])
+    assert w == list(z["wins"]) and l == list(z["losses"]) and p == list(z["processed"])
+    np.testing.assert_allclose(c, z["certainty"], rtol=1e-6)
+
+
+def test_batch_indices_match_reference():
+    z, meta = load("batch_indices")
+    for ci, c in enumerate(meta["cases"]):
+        torch.manual_seed(meta["seed"] + ci)
+        ix = O.batch_starting_indices(c["data_size"], c["block_size"], c["batch_size"], c["split"],
+                                      c["file_lengths"], c["is_percents"])
+        np.testing.assert_array_equal(ix.numpy(), z[f"ix.{ci}"])
+
+
+def test_jitter_matches_reference():
+    z = np.load(f"{O.__file__.rsplit('/', 2)[0]}/tests/golden/jitter.npz")
+    random.seed(5)
+    data = [int(x) for x in z["before"]]
+    O.jitter_inplace(data, True, 12)
+    np.testing.assert_array_equal(np.array(data), z["after"])

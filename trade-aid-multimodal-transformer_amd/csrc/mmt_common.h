@@ -1,0 +1,69 @@
+// Shared device-side definitions for the MI355X (gfx950 / CDNA4) multimodal-transformer kernels.
+//
+// Storage convention: activations and packed weights are bf16 (raw 16-bit storage `bf16_t`),
+// accumulation is fp32 (MFMA f32 accumulators), master params / grads / residual stream fp32.
+// Every bf16 matrix that feeds an MFMA GEMM has a leading dimension that is a multiple of 8
+// elements and a 16-byte aligned base, so operand tiles stage with 16-byte loads.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;  // raw bf16 storage
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+#define MMT_WAVE 64
+#define MMT_MAX_GROUP 8
+
+__device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float(((uint32_t)x) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// LDS transposed read (ds_read_b64_tr_b16): per 16-lane group, 4 rows x 16 columns of 16-bit
+// elements; lane 4q+p supplies the address of row q, columns 4p..4p+3; lane i of the group
+// receives column i of the 4 rows (row q in element q).
+__device__ __forceinline__ s16x4 lds_tr16(const void* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)lds_addr));
+}
+
+__device__ __forceinline__ bf16x8 join4(s16x4 lo, s16x4 hi) {
+  bf16x8 r;
+  r[0] = __builtin_bit_cast(__bf16, lo[0]); r[1] = __builtin_bit_cast(__bf16, lo[1]);
+  r[2] = __builtin_bit_cast(__bf16, lo[2]); r[3] = __builtin_bit_cast(__bf16, lo[3]);
+  r[4] = __builtin_bit_cast(__bf16, hi[0]); r[5] = __builtin_bit_cast(__bf16, hi[1]);
+  r[6] = __builtin_bit_cast(__bf16, hi[2]); r[7] = __builtin_bit_cast(__bf16, hi[3]);
+  return r;
+}
+
+// counter-based hash RNG (dropout masks); identical in forward and backward
+__device__ __forceinline__ uint32_t mmt_hash(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
+  h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+  return h;
+}

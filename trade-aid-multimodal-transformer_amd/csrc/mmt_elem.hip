@@ -1,0 +1,551 @@
+// Memory-bound kernels of the training step (gfx950): LayerNorm fwd/bwd, token+position
+// embedding fwd/bwd, fused softmax-cross-entropy, bias-gradient column sums, per-head Q/K/V
+// stage-2 block-diagonal maps, fp32->bf16 weight packing, fused AdamW, directional metric.
+// All grouped over modalities with blockIdx.z (one launch per op per layer).
+#include "mmt_common.h"
+#include "mmt_kernels.h"
+
+// ============================================================================================
+// LayerNorm (reference: nn.LayerNorm(n_embd), eps 1e-5; model.py:189-190, 210, 330)
+// one wave per row; each lane holds NV float4 of the row in registers
+// ============================================================================================
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnBatch batch, int R, int C) {
+  const LnProblem& P = batch.p[blockIdx.z];
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int C4 = C >> 2;
+  const float* x = P.x + (int64_t)row * C;
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+    v[i] = (c4 < C4) ? reinterpret_cast<const f32x4*>(x)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mean = warp_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+    if (c4 < C4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(warp_sum(q) / C + 1e-5f);
+  bf16_t* y = P.y + (int64_t)row * C;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+    if (c4 < C4) {
+      const f32x4 g = reinterpret_cast<const f32x4*>(P.gamma)[c4];
+      const f32x4 b = reinterpret_cast<const f32x4*>(P.beta)[c4];
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
+      reinterpret_cast<u32x2*>(y)[c4] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+    }
+  }
+  if (lane == 0) { P.mean[row] = mean; P.rstd[row] = rstd; }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnBatch batch, int R, int C) {
+  const LnProblem& P = batch.p[blockIdx.z];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int C4 = C >> 2;
+  f32x4 g[NV], dgam[NV], dbet[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+    g[i] = (c4 < C4) ? reinterpret_cast<const f32x4*>(P.gamma)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    dgam[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dbet[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
+    const float mean = P.mean[row], rstd = P.rstd[row];
+    const f32x4* x = reinterpret_cast<const f32x4*>(P.x + (int64_t)row * C);
+    const f32x4* dy = reinterpret_cast<const f32x4*>(P.dy + (int64_t)row * C);
+    f32x4 xh[NV], gd[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+        const f32x4 xv = x[c4], dv = dy[c4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[i][e] = (xv[e] - mean) * rstd;
+          gd[i][e] = dv[e] * g[i][e];
+          s1 += gd[i][e];
+          s2 += gd[i][e] * xh[i][e];
+          dgam[i][e] += dv[e] * xh[i][e];
+          dbet[i][e] += dv[e];
+        }
+      }
+    }
+    s1 = warp_sum(s1) / C;
+    s2 = warp_sum(s2) / C;
+    f32x4* dx = reinterpret_cast<f32x4*>(P.dx + (int64_t)row * C);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+        f32x4 o = dx[c4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += rstd * (gd[i][e] - s1 - xh[i][e] * s2);
+        dx[c4] = o;
+        if (P.dx16)
+          reinterpret_cast<u32x2*>(P.dx16 + (int64_t)row * C)[c4] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+      }
+    }
+  }
+  // reduce the 4 waves' partial dgamma/dbeta through LDS, then one atomic per column
+  __shared__ float red[2][4][1024];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+    if (c4 < C4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[0][wave][c4 * 4 + e] = dgam[i][e];
+        red[1][wave][c4 * 4 + e] = dbet[i][e];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float a = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    const float b = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    atomicAdd(P.dgamma + c, a);
+    atomicAdd(P.dbeta + c, b);
+  }
+}
+
+hipError_t mmt_launch_ln_fwd(const LnBatch& b, int R, int C, hipStream_t s) {
+  if (C % 4 != 0 || C > 1024 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
+  dim3 grid((R + 3) / 4, 1, b.count);
+  const int nv = (C / 4 + 63) / 64;
+  if (nv <= 1) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, b, R, C);
+  else if (nv <= 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, b, R, C);
+  else hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, b, R, C);
+  return hipGetLastError();
+}
+
+hipError_t mmt_launch_ln_bwd(const LnBatch& b, int R, int C, hipStream_t s) {
+  if (C % 4 != 0 || C > 1024 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
+  int blocks = (R + 3) / 4;
+  if (blocks > 1024) blocks = 1024;
+  dim3 grid(blocks, 1, b.count);
+  const int nv = (C / 4 + 63) / 64;
+  if (nv <= 1) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, s, b, R, C);
+  else if (nv <= 2) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, s, b, R, C);
+  else hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, s, b, R, C);
+  return hipGetLastError();
+}
+
+// ============================================================================================
+// Embedding: x[b,t] = tok[idx[b,t]] + pos[t]   (model.py:308-317); backward scatter-adds
+// ============================================================================================
+__global__ __launch_bounds__(256) void embed_fwd_kernel(EmbBatch batch, int R, int T, int C) {
+  const EmbProblem& P = batch.p[blockIdx.z];
+  const int C4 = C >> 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)R * C4) return;
+  const int r = (int)(i / C4), c4 = (int)(i % C4);
+  const int t = r % T;
+  int64_t id = P.idx[r];
+  id = id < 0 ? 0 : (id >= P.V ? P.V - 1 : id);
+  const f32x4 a = reinterpret_cast<const f32x4*>(P.tok + id * C)[c4];
+  const f32x4 p = reinterpret_cast<const f32x4*>(P.pos + (int64_t)t * C)[c4];
+  reinterpret_cast<f32x4*>(P.x + (int64_t)r * C)[c4] = a + p;
+}
+
+__global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBatch batch, int R, int T, int C) {
+  const EmbProblem& P = batch.p[blockIdx.z];
+  const int C4 = C >> 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)R * C4) return;
+  const int r = (int)(i / C4), c4 = (int)(i % C4);
+  const int t = r % T;
+  int64_t id = P.idx[r];
+  id = id < 0 ? 0 : (id >= P.V ? P.V - 1 : id);
+  const f32x4 d = reinterpret_cast<const f32x4*>(P.dx + (int64_t)r * C)[c4];
+  float* dt = P.dtok + id * C + c4 * 4;
+  float* dp = P.dpos + (int64_t)t * C + c4 * 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    atomicAdd(dt + e, d[e]);
+    atomicAdd(dp + e, d[e]);
+  }
+}
+
+hipError_t mmt_launch_embed_fwd(const EmbBatch& b, int B, int T, int C, hipStream_t s) {
+  if (C % 4 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
+  const int64_t n = (int64_t)B * T * (C / 4);
+  dim3 grid((unsigned)((n + 255) / 256), 1, b.count);
+  hipLaunchKernelGGL(embed_fwd_kernel, grid, dim3(256), 0, s, b, B * T, T, C);
+  return hipGetLastError();
+}
+
+hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStream_t s) {
+  if (C % 4 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
+  const int64_t n = (int64_t)B * T * (C / 4);
+  dim3 grid((unsigned)((n + 255) / 256), 1, b.count);
+  hipLaunchKernelGGL(embed_bwd_kernel, grid, dim3(256), 0, s, b, B * T, T, C);
+  return hipGetLastError();
+}
+
+// ============================================================================================
+// Cross-entropy (F.cross_entropy mean over B*T; model.py:393-400), fused with dlogits:
+//   loss += (logsumexp(x) - x[t]) / R ;  dlogits = softmax(x) - onehot(t)  (bf16, unscaled)
+// one wave per row
+// ============================================================================================
+__global__ __launch_bounds__(256) void ce_fwd_kernel(CeBatch batch, int R) {
+  const CeProblem& P = batch.p[blockIdx.z];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  __shared__ float part[4];
+  float contrib = 0.f;
+  if (row < R) {
+    const float* x = P.logits + (int64_t)row * P.V;
+    float m = -INFINITY;
+    for (int v = lane; v < P.V; v += 64) m = fmaxf(m, x[v]);
+    m = warp_max(m);
+    float sum = 0.f;
+    for (int v = lane; v < P.V; v += 64) sum += __expf(x[v] - m);
+    sum = warp_sum(sum);
+    const float lse = m + __logf(sum);
+    const int t = (int)P.tgt[row];
+    contrib = lse - x[t];
+    bf16_t* d = P.dlogits + (int64_t)row * P.ld_d;
+    for (int v = lane; v < P.ld_d; v += 64) {
+      float g = 0.f;
+      if (v < P.V) g = __expf(x[v] - lse) - (v == t ? 1.f : 0.f);
+      d[v] = f2bf(g);
+    }
+  }
+  if (lane == 0) part[wave] = contrib;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(P.loss, (part[0] + part[1] + part[2] + part[3]) / (float)R);
+}
+
+hipError_t mmt_launch_ce_fwd(const CeBatch& b, int R, hipStream_t s) {
+  if (b.count == 0) return hipSuccess;
+  dim3 grid((R + 3) / 4, 1, b.count);
+  hipLaunchKernelGGL(ce_fwd_kernel, grid, dim3(256), 0, s, b, R);
+  return hipGetLastError();
+}
+
+// ============================================================================================
+// Bias gradients: out[n] += alpha * sum_r x[r, n]   (x bf16 [R, ld])
+// block = 32 column chunks of 8 x 8 row lanes; 256 rows per block
+// ============================================================================================
+__global__ __launch_bounds__(256) void colsum_kernel(ColsumBatch batch, int R) {
+  const ColsumProblem& P = batch.p[blockIdx.z];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + cl) * 8;
+  const int r0 = blockIdx.y * 256;
+  __shared__ float red[8][256 + 8];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < P.N) {
+    const bool full = (c0 + 8 <= P.ld) && ((P.ld & 7) == 0);
+    for (int r = r0 + rl; r < min(R, r0 + 256); r += 8) {
+      const bf16_t* src = P.x + (int64_t)r * P.ld + c0;
+      if (full) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(src);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc[2 * e] += bf2f(v[e] & 0xffff); acc[2 * e + 1] += bf2f(v[e] >> 16); }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) if (c0 + e < P.N) acc[e] += bf2f(src[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][cl * 8 + e] = acc[e];
+  __syncthreads();
+  const int c = threadIdx.x;  // 256 columns of this block
+  const int gc = blockIdx.x * 256 + c;
+  if (gc < P.N) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += red[i][c];
+    float alpha = P.alpha;
+    if (P.alpha_ptr) alpha *= *P.alpha_ptr;
+    atomicAdd(P.out + gc, alpha * s);
+  }
+}
+
+hipError_t mmt_launch_colsum(const ColsumBatch& b, int R, hipStream_t s) {
+  int maxn = 0;
+  for (int g = 0; g < b.count; ++g) maxn = b.p[g].N > maxn ? b.p[g].N : maxn;
+  if (maxn == 0 || b.count == 0) return hipSuccess;
+  dim3 grid((maxn + 255) / 256, (R + 255) / 256, b.count);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, b, R);
+  return hipGetLastError();
+}
+
+// ============================================================================================
+// Per-head Q/K/V stage 2 (model.py:36-50): Linear(hs/2, hs, bias=False) per (kind, head)
+//   out[r, blk*hs + o] = sum_i W2[blk][o][i] * h1[r, blk*hh + i],  hh = hs/2
+// block = one blk x 256 rows; W2[blk] staged in LDS (fp32)
+// ============================================================================================
+template <int HS>
+__global__ __launch_bounds__(256) void qkv2_fwd_kernel(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
+  constexpr int HH = HS / 2;
+  const Qkv2Problem& P = batch.p[blockIdx.z];
+  const int blk = blockIdx.y;
+  __shared__ float w[HS * HH];
+  for (int i = threadIdx.x; i < HS * HH; i += 256) w[i] = P.w2[(int64_t)blk * HS * HH + i];
+  __syncthreads();
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  float in[HH];
+  const bf16_t* src = P.h1 + (int64_t)r * ld_h1 + blk * HH;
+#pragma unroll
+  for (int i = 0; i < HH; ++i) in[i] = bf2f(src[i]);
+  bf16_t* dst = P.out + (int64_t)r * ld_out + blk * HS;
+#pragma unroll
+  for (int o = 0; o < HS; o += 2) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < HH; ++i) { a += w[o * HH + i] * in[i]; b += w[(o + 1) * HH + i] * in[i]; }
+    *reinterpret_cast<uint32_t*>(dst + o) = pack2bf(a, b);
+  }
+}
+
+// backward: dh1 = (W2^T dout) * (1 - h1^2)  and  dW2 += dout^T h1 (per 256-row chunk, atomics)
+template <int HS>
+__global__ __launch_bounds__(256) void qkv2_bwd_kernel(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
+  constexpr int HH = HS / 2;
+  const Qkv2Problem& P = batch.p[blockIdx.z];
+  const int blk = blockIdx.y;
+  const int r0 = blockIdx.x * 256;
+  __shared__ float w[HS * HH];
+  __shared__ bf16_t sd[256][HS];
+  __shared__ bf16_t sh[256][HH];
+  for (int i = threadIdx.x; i < HS * HH; i += 256) w[i] = P.w2[(int64_t)blk * HS * HH + i];
+  {
+    const int r = r0 + threadIdx.x;
+    const bool ok = r < R;
+    const bf16_t* d = P.dout + (int64_t)r * ld_out + blk * HS;
+    const bf16_t* h = P.h1 + (int64_t)r * ld_h1 + blk * HH;
+#pragma unroll
+    for (int o = 0; o < HS; ++o) sd[threadIdx.x][o] = ok ? d[o] : (bf16_t)0;
+#pragma unroll
+    for (int i = 0; i < HH; ++i) sh[threadIdx.x][i] = ok ? h[i] : (bf16_t)0;
+  }
+  __syncthreads();
+  // data grad, thread per row
+  {
+    const int r = r0 + threadIdx.x;
+    if (r < R) {
+      bf16_t* dst = P.dh1 + (int64_t)r * ld_h1 + blk * HH;
+#pragma unroll
+      for (int i = 0; i < HH; ++i) {
+        float a = 0.f;
+#pragma unroll
+        for (int o = 0; o < HS; ++o) a += w[o * HH + i] * bf2f(sd[threadIdx.x][o]);
+        const float t = bf2f(sh[threadIdx.x][i]);
+        dst[i] = f2bf(a * (1.f - t * t));
+      }
+    }
+  }
+  // weight grad partials: outputs (o, i) distributed over threads
+  const int rows = min(256, R - r0);
+  for (int q = threadIdx.x; q < HS * HH; q += 256) {
+    const int o = q / HH, i = q % HH;
+    float a = 0.f;
+    for (int rr = 0; rr < rows; ++rr) a += bf2f(sd[rr][o]) * bf2f(sh[rr][i]);
+    atomicAdd(P.dw2 + (int64_t)blk * HS * HH + q, a);
+  }
+}
+
+template <int HS>
+static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_out, bool bwd, hipStream_t s) {
+  dim3 grid((R + 255) / 256, nblk, b.count);
+  if (bwd) hipLaunchKernelGGL(qkv2_bwd_kernel<HS>, grid, dim3(256), 0, s, b, R, ld_h1, ld_out);
+  else hipLaunchKernelGGL(qkv2_fwd_kernel<HS>, grid, dim3(256), 0, s, b, R, ld_h1, ld_out);
+}
+
+static hipError_t qkv2_dispatch(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, bool bwd,
+                                hipStream_t s) {
+  if (b.count == 0) return hipSuccess;
+  switch (hs) {
+    case 2: qkv2_launch<2>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 4: qkv2_launch<4>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 8: qkv2_launch<8>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 16: qkv2_launch<16>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 32: qkv2_launch<32>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 64: qkv2_launch<64>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t mmt_launch_qkv2_fwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s) {
+  return qkv2_dispatch(b, R, nblk, hs, ld_h1, ld_out, false, s);
+}
+hipError_t mmt_launch_qkv2_bwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s) {
+  return qkv2_dispatch(b, R, nblk, hs, ld_h1, ld_out, true, s);
+}
+
+// ============================================================================================
+// fp32 master weights -> bf16 packed copies with padded leading dimension (pad zero-filled)
+// one block per task (segment, 32-row slab); thread per 8-column chunk
+// ============================================================================================
+__global__ __launch_bounds__(256) void pack_kernel(const PackSeg* __restrict__ segs, int nseg,
+                                                   const int* __restrict__ task_seg, const float* __restrict__ src,
+                                                   bf16_t* __restrict__ dst) {
+  const int seg = task_seg[2 * blockIdx.x];
+  const int row0 = task_seg[2 * blockIdx.x + 1];
+  const PackSeg S = segs[seg];
+  const int chunks = S.dld / 8;
+  for (int q = threadIdx.x; q < 32 * chunks; q += 256) {
+    const int r = row0 + q / chunks;
+    const int c = (q % chunks) * 8;
+    if (r >= S.rows) break;
+    const float* s = src + S.src_off + (int64_t)r * S.cols;
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = (c + 2 * e < S.cols) ? s[c + 2 * e] : 0.f;
+      const float b = (c + 2 * e + 1 < S.cols) ? s[c + 2 * e + 1] : 0.f;
+      w[e] = pack2bf(a, b);
+    }
+    *reinterpret_cast<u32x4*>(dst + S.dst_off + (int64_t)r * S.dld + c) = u32x4{w[0], w[1], w[2], w[3]};
+  }
+}
+
+hipError_t mmt_launch_pack(const PackSeg* segs_dev, int nseg, int64_t ntasks, const int* task_dev, const float* src,
+                           bf16_t* dst, hipStream_t s) {
+  if (ntasks == 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)ntasks), dim3(256), 0, s, segs_dev, nseg, task_dev, src, dst);
+  return hipGetLastError();
+}
+
+__global__ void f2bf_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = f2bf(src[i]);
+}
+hipError_t mmt_launch_f32_to_bf16(const float* src, bf16_t* dst, int64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(f2bf_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, n);
+  return hipGetLastError();
+}
+
+// ============================================================================================
+// AdamW (torch.optim.AdamW defaults, decoupled decay; main.py:464, 650):
+//   p *= 1 - lr*wd; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// ============================================================================================
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, int64_t n4, int64_t n,
+                                                    float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                    float bc2_sqrt) {
+  const float step_size = lr / bc1;
+  const float decay = 1.f - lr * wd;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+    const f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      pp[e] *= decay;
+      mm[e] += (gg[e] - mm[e]) * (1.f - b1);
+      vv[e] = vv[e] * b2 + (1.f - b2) * gg[e] * gg[e];
+      const float denom = sqrtf(vv[e]) / bc2_sqrt + eps;
+      pp[e] -= step_size * mm[e] / denom;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pp;
+    reinterpret_cast<f32x4*>(m)[i] = mm;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+  }
+  // scalar tail
+  const int64_t t = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) {
+    float pp = p[t] * decay;
+    const float gg = g[t];
+    float mm = m[t] + (gg - m[t]) * (1.f - b1);
+    float vv = v[t] * b2 + (1.f - b2) * gg * gg;
+    pp -= step_size * mm / (sqrtf(vv) / bc2_sqrt + eps);
+    p[t] = pp; m[t] = mm; v[t] = vv;
+  }
+}
+
+hipError_t mmt_launch_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                            float eps, float wd, float bc1, float bc2_sqrt, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const int64_t n4 = n / 4;
+  int64_t blocks = (n4 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, n4, n, lr, b1, b2, eps, wd,
+                     bc1, bc2_sqrt);
+  return hipGetLastError();
+}
+
+// ============================================================================================
+// Directional metric (training_utils.py:215-330) for one numeric modality, one wave per sample
+//   pred = vocab[argmax(logits[j, T-1])] (first max wins), act = vocab[y[j,T-1]],
+//   prev = vocab[x[j,T-1]] (value data) ; win if sign(pred-prev) == sign(act-prev)
+//   (percent data: sign(pred) == sign(act)); certainty = softmax mass of same-sign tokens.
+// ============================================================================================
+__device__ __forceinline__ int dsign(double cur, double prev, int pct) {
+  const double c = pct ? cur : cur - prev;
+  return c > 0 ? 1 : (c < 0 ? -1 : 0);
+}
+
+__global__ __launch_bounds__(64) void eval_dir_kernel(const float* __restrict__ logits, const int64_t* __restrict__ xb,
+                                                      const int64_t* __restrict__ yb, const double* __restrict__ vocab,
+                                                      int T, int V, int pct, int* wl, double* cert) {
+  const int j = blockIdx.x;
+  const int lane = threadIdx.x;
+  const float* x = logits + ((int64_t)j * T + (T - 1)) * V;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int v = lane; v < V; v += 64) {
+    const float a = x[v];
+    if (a > best || (a == best && v < bi)) { best = a; bi = v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  const double prev = pct ? 0.0 : vocab[xb[(int64_t)j * T + T - 1]];
+  const double pv = vocab[bi], av = vocab[yb[(int64_t)j * T + T - 1]];
+  const int ps = dsign(pv, prev, pct), as = dsign(av, prev, pct);
+  float m = warp_max(best);
+  float sum = 0.f, same = 0.f;
+  for (int v = lane; v < V; v += 64) {
+    const float e = __expf(x[v] - m);
+    sum += e;
+    if (dsign(vocab[v], prev, pct) == ps) same += e;
+  }
+  sum = warp_sum(sum);
+  same = warp_sum(same);
+  if (lane == 0) {
+    atomicAdd(wl + (ps == as ? 0 : 1), 1);
+    atomicAdd(cert, (double)(same / sum));
+  }
+}
+
+hipError_t mmt_launch_eval_direction(const float* logits, const int64_t* xb, const int64_t* yb, const double* vocab,
+                                     int B, int T, int V, int is_pct, int* wins_losses, double* certainty,
+                                     hipStream_t s) {
+  if (B == 0) return hipSuccess;
+  hipLaunchKernelGGL(eval_dir_kernel, dim3(B), dim3(64), 0, s, logits, xb, yb, vocab, T, V, is_pct, wins_losses,
+                     certainty);
+  return hipGetLastError();
+}

@@ -1,0 +1,991 @@
+// Host engine of libmmt_hip.so: parameter layout, workspace plan and the forward / backward
+// launch sequence of the multimodal transformer training step, behind the C-ABI of include/mmt.h.
+//
+// Reference structure restated (model.py): per layer, per modality i
+//   x1 = x0 + proj(MHA(LN1 x0))           MHA heads: q/k/v = Linear(C,hs/2)+tanh+Linear(hs/2,hs)
+//   x2 = x1 + FFN(LN2 x1)                 FFN = Linear(C,4C)+ReLU+Linear(4C,C)
+//   x3 = x2 + proj(CA(LNc x2, [x2_j]))    only for cross modalities; one softmax per KV stream, summed
+// post: logits = Linear(V/2,V)(tanh(Linear(C,V/2)(LNf x))), loss = mean CE.
+// All modalities' identical-shape ops run as ONE grouped launch (blockIdx.z = modality).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mmt.h"
+#include "mmt_kernels.h"
+
+namespace {
+
+constexpr int MAXM = MMT_MAX_MODALITIES;
+
+inline int64_t rup(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+inline int r8(int x) { return (int)rup(x < 1 ? 1 : x, 8); }
+
+struct Mat {
+  int64_t off = -1;  // fp32 offset of the [rows, cols] weight in the flat param buffer
+  int rows = 0, cols = 0;
+  int64_t pk = 0;    // bf16 element offset in the packed-weight region
+  int ld = 0;        // packed leading dimension (multiple of 8)
+};
+
+struct TensorInfo {
+  std::string name;
+  int64_t off;
+  int nd;
+  int64_t shape[2];
+  int kind;
+};
+
+struct LM {  // parameters of one (layer, modality)
+  int64_t ln1w, ln1b, ln2w, ln2b;
+  Mat W1; int64_t b1; int64_t w2;
+  Mat P0; int64_t bp0; Mat P2; int64_t bp2;
+  Mat F0; int64_t bf0; Mat F2; int64_t bf2;
+  bool cross = false;  // cross-attention active (cross flag and M > 1)
+  int64_t lncw = -1, lncb = -1;
+  Mat Wq; Mat Wkv[MAXM]; Mat C0; int64_t bc0 = -1; Mat C2; int64_t bc2 = -1;
+};
+
+struct PostM {
+  int64_t lnw, lnb;
+  Mat H0; int64_t b0; Mat H2; int64_t b2;
+  int64_t tok;
+};
+
+struct ActLM {  // byte offsets of one (layer, modality)'s saved activations in the workspace
+  size_t a, mean1, rstd1, h1, qkv, o, lse, p1, x1, c, mean2, rstd2, f, x2, x2h;
+  size_t d, meanc, rstdc, qc, kv[MAXM], oc, ocj[MAXM], lsej[MAXM], pc, x3;
+};
+
+struct Plan {
+  int B = -1;
+  size_t total = 0;
+  size_t pack = 0;
+  std::vector<ActLM> act;  // [L*M]
+  size_t xemb[MAXM];
+  size_t lnf16[MAXM], meanf[MAXM], rstdf[MAXM], hh[MAXM], dlog[MAXM];
+  // backward scratch, per modality
+  size_t dres[MAXM], dres16[MAXM], dln[MAXM], gbig[MAXM], gdo[MAXM], gq[MAXM], gqkv[MAXM], gh1[MAXM], gp[MAXM];
+  size_t dvec[MAXM][MAXM];
+  size_t dkv[MAXM][MAXM];
+};
+
+}  // namespace
+
+struct mmt_ctx {
+  mmt_config cfg;
+  int M, C, H, L, T, hs, hh;
+  int V[MAXM];
+  bool any_cross = false;
+  int ncross = 0;
+  std::vector<TensorInfo> tensors;
+  std::vector<LM> lm;  // [L*M]
+  PostM post[MAXM];
+  int64_t pos_off = 0;
+  int64_t nparams = 0, nactive = 0;
+  int64_t emb_begin = 0, emb_end = 0, post_begin = 0, post_end = 0;
+  std::vector<int64_t> layer_begin, layer_end;
+  // weight packing
+  std::vector<PackSeg> segs;
+  std::vector<int> tasks;
+  int64_t pack_elems = 0;
+  PackSeg* d_segs = nullptr;
+  int* d_tasks = nullptr;
+  // state
+  Plan plan;
+  int last_B = -1;
+  bool fwd_ready = false;
+  bool last_training = false;
+  uint64_t step_counter = 0;
+  const int64_t* last_idx[MAXM] = {};  // forward token ids, read by the embedding backward stage
+  std::string err;
+  int ldv[MAXM], ldvh[MAXM];
+};
+
+namespace {
+
+thread_local std::string g_create_err;
+
+int fail(mmt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                             \
+  do {                                                                                                \
+    hipError_t e_ = (expr);                                                                           \
+    if (e_ != hipSuccess) return fail(ctx, MMT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// -------------------------------------------------------------------------------------------
+// parameter layout
+// -------------------------------------------------------------------------------------------
+struct Builder {
+  mmt_ctx* c;
+  int64_t cur = 0;
+  int64_t alloc(int64_t n) {
+    const int64_t o = cur;
+    cur += rup(n > 0 ? n : 0, 16);
+    return o;
+  }
+  void tensor(const std::string& name, int64_t off, int nd, int64_t s0, int64_t s1, int kind) {
+    TensorInfo t;
+    t.name = name; t.off = off; t.nd = nd; t.shape[0] = s0; t.shape[1] = s1; t.kind = kind;
+    c->tensors.push_back(t);
+  }
+  Mat mat(const std::string& name, int rows, int cols, bool emit = true) {
+    Mat m;
+    m.rows = rows; m.cols = cols;
+    m.off = alloc((int64_t)rows * cols);
+    m.ld = r8(cols);
+    if (emit) tensor(name, m.off, 2, rows, cols, 0);
+    return m;
+  }
+  int64_t vec(const std::string& name, int n, int kind) {
+    const int64_t o = alloc(n);
+    tensor(name, o, 1, n, 0, kind);
+    return o;
+  }
+};
+
+void build_cross_params(Builder& b, LM& x, const std::string& p, int C, int H, int hs, int nkv) {
+  x.lncw = -1;
+  x.Wq = b.mat("", H * hs, C, false);
+  for (int h = 0; h < H; ++h)
+    b.tensor(p + "heads." + std::to_string(h) + ".query.weight", x.Wq.off + (int64_t)h * hs * C, 2, hs, C, 0);
+  for (int j = 0; j < nkv; ++j) {
+    x.Wkv[j] = b.mat("", H * 2 * hs, C, false);
+    for (int h = 0; h < H; ++h)
+      b.tensor(p + "heads." + std::to_string(h) + ".kv_projections." + std::to_string(j) + ".weight",
+               x.Wkv[j].off + (int64_t)h * 2 * hs * C, 2, 2 * hs, C, 0);
+  }
+  x.C0 = b.mat(p + "proj.0.weight", C / 2, hs * H);
+  x.bc0 = b.vec(p + "proj.0.bias", C / 2, 1);
+  x.C2 = b.mat(p + "proj.2.weight", C, C / 2);
+  x.bc2 = b.vec(p + "proj.2.bias", C, 1);
+}
+
+void build_layout(mmt_ctx* c) {
+  Builder b{c};
+  const int C = c->C, H = c->H, hs = c->hs, hh = c->hh, M = c->M, L = c->L;
+  c->emb_begin = b.cur;
+  for (int i = 0; i < M; ++i) {
+    c->post[i].tok = b.alloc((int64_t)c->V[i] * C);
+    b.tensor("pre_block.token_embedding_tables." + std::to_string(i) + ".weight", c->post[i].tok, 2, c->V[i], C, 0);
+  }
+  c->pos_off = b.alloc((int64_t)c->T * C);
+  b.tensor("pre_block.position_embedding_table.weight", c->pos_off, 2, c->T, C, 0);
+  c->emb_end = b.cur;
+  c->lm.resize((size_t)L * M);
+  const char* kinds[3] = {"key", "query", "value"};
+  for (int l = 0; l < L; ++l) {
+    c->layer_begin.push_back(b.cur);
+    const std::string bl = "blocks." + std::to_string(l) + ".";
+    for (int i = 0; i < M; ++i) {
+      LM& x = c->lm[(size_t)l * M + i];
+      const std::string p = bl + "sa_layers." + std::to_string(i) + ".";
+      x.W1 = b.mat("", 3 * H * hh, C, false);
+      x.b1 = b.alloc(3 * H * hh);
+      x.w2 = b.alloc((int64_t)3 * H * hs * hh);
+      for (int k = 0; k < 3; ++k)
+        for (int h = 0; h < H; ++h) {
+          const std::string hp = p + "heads." + std::to_string(h) + "." + kinds[k] + ".";
+          const int blk = k * H + h;
+          b.tensor(hp + "0.weight", x.W1.off + (int64_t)blk * hh * C, 2, hh, C, 0);
+          b.tensor(hp + "0.bias", x.b1 + (int64_t)blk * hh, 1, hh, 0, 1);
+          b.tensor(hp + "2.weight", x.w2 + (int64_t)blk * hs * hh, 2, hs, hh, 0);
+        }
+      x.P0 = b.mat(p + "proj.0.weight", C / 2, hs * H);
+      x.bp0 = b.vec(p + "proj.0.bias", C / 2, 1);
+      x.P2 = b.mat(p + "proj.2.weight", C, C / 2);
+      x.bp2 = b.vec(p + "proj.2.bias", C, 1);
+    }
+    for (int i = 0; i < M; ++i) {
+      LM& x = c->lm[(size_t)l * M + i];
+      const std::string p = bl + "ffwd_layers." + std::to_string(i) + ".net.";
+      x.F0 = b.mat(p + "0.weight", 4 * C, C);
+      x.bf0 = b.vec(p + "0.bias", 4 * C, 1);
+      x.F2 = b.mat(p + "2.weight", C, 4 * C);
+      x.bf2 = b.vec(p + "2.bias", C, 1);
+    }
+    for (int i = 0; i < M; ++i) {
+      LM& x = c->lm[(size_t)l * M + i];
+      x.ln1w = b.vec(bl + "ln1_layers." + std::to_string(i) + ".weight", C, 2);
+      x.ln1b = b.vec(bl + "ln1_layers." + std::to_string(i) + ".bias", C, 3);
+      x.ln2w = b.vec(bl + "ln2_layers." + std::to_string(i) + ".weight", C, 2);
+      x.ln2b = b.vec(bl + "ln2_layers." + std::to_string(i) + ".bias", C, 3);
+    }
+    for (int i = 0; i < M; ++i) {
+      LM& x = c->lm[(size_t)l * M + i];
+      if (!(c->cfg.cross_attention[i] && M > 1)) continue;
+      x.cross = true;
+      const std::string p = bl + "cross_attention_layers." + std::to_string(i) + ".";
+      build_cross_params(b, x, p, C, H, hs, M - 1);
+      x.lncw = b.vec(bl + "ln_cross_layers." + std::to_string(i) + ".weight", C, 2);
+      x.lncb = b.vec(bl + "ln_cross_layers." + std::to_string(i) + ".bias", C, 3);
+    }
+    c->layer_end.push_back(b.cur);
+  }
+  c->post_begin = b.cur;
+  for (int i = 0; i < M; ++i) {
+    c->post[i].lnw = b.vec("post_block.fin_norm_layers." + std::to_string(i) + ".weight", C, 2);
+    c->post[i].lnb = b.vec("post_block.fin_norm_layers." + std::to_string(i) + ".bias", C, 3);
+  }
+  for (int i = 0; i < M; ++i) {
+    const std::string p = "post_block.soft_score_layers." + std::to_string(i) + ".";
+    const int V = c->V[i], V2 = V / 2;
+    c->post[i].H0 = b.mat(p + "0.weight", V2, C);
+    c->post[i].b0 = b.vec(p + "0.bias", V2, 1);
+    c->post[i].H2 = b.mat(p + "2.weight", V, V2);
+    c->post[i].b2 = b.vec(p + "2.bias", V, 1);
+  }
+  c->post_end = b.cur;
+  c->nactive = b.cur;
+  // parameters that never receive a gradient: a CrossAttention built with zero KV modalities (M == 1,
+  // model.py:198-200, 238). torch's AdamW skips them (no decay): they live past the active prefix.
+  for (int l = 0; l < L; ++l)
+    for (int i = 0; i < M; ++i) {
+      if (!(c->cfg.cross_attention[i] && M == 1)) continue;
+      LM dummy;
+      const std::string bl = "blocks." + std::to_string(l) + ".";
+      build_cross_params(b, dummy, bl + "cross_attention_layers." + std::to_string(i) + ".", C, H, hs, 0);
+      b.vec(bl + "ln_cross_layers." + std::to_string(i) + ".weight", C, 2);
+      b.vec(bl + "ln_cross_layers." + std::to_string(i) + ".bias", C, 3);
+    }
+  c->nparams = b.cur;
+
+  // packed bf16 weights: every GEMM weight matrix with a padded leading dimension
+  int64_t pk = 0;
+  auto add = [&](Mat& m) {
+    if (m.off < 0 || m.rows == 0) return;
+    m.pk = pk;
+    pk += rup((int64_t)m.rows * m.ld, 64);
+    PackSeg s;
+    s.src_off = m.off; s.dst_off = m.pk; s.rows = m.rows; s.cols = m.cols; s.dld = m.ld; s.pad_ = 0;
+    const int si = (int)c->segs.size();
+    c->segs.push_back(s);
+    for (int r0 = 0; r0 < m.rows; r0 += 32) { c->tasks.push_back(si); c->tasks.push_back(r0); }
+  };
+  for (auto& x : c->lm) {
+    add(x.W1); add(x.P0); add(x.P2); add(x.F0); add(x.F2);
+    if (x.cross) {
+      add(x.Wq);
+      for (int j = 0; j < M - 1; ++j) add(x.Wkv[j]);
+      add(x.C0); add(x.C2);
+    }
+  }
+  for (int i = 0; i < M; ++i) { add(c->post[i].H0); add(c->post[i].H2); }
+  c->pack_elems = pk;
+  for (int i = 0; i < M; ++i) {
+    c->ldv[i] = r8(c->V[i]);
+    c->ldvh[i] = r8(c->V[i] / 2);
+  }
+}
+
+// -------------------------------------------------------------------------------------------
+// workspace plan for batch B
+// -------------------------------------------------------------------------------------------
+void make_plan(mmt_ctx* c, int B) {
+  Plan& p = c->plan;
+  p = Plan();
+  p.B = B;
+  size_t cur = 0;
+  auto A = [&](size_t bytes) { const size_t o = cur; cur += (size_t)rup((int64_t)bytes, 256); return o; };
+  const int64_t R = (int64_t)B * c->T;
+  const int C = c->C, M = c->M, H = c->H;
+  const size_t f4 = 4, b2 = 2;
+  const int ldh1 = r8(3 * H * c->hh), ldp = r8(C / 2);
+  const size_t bhT = (size_t)B * H * c->T;
+  p.pack = A((size_t)c->pack_elems * b2);
+  p.act.resize((size_t)c->L * M);
+  for (int i = 0; i < M; ++i) p.xemb[i] = A(R * C * f4);
+  for (int l = 0; l < c->L; ++l)
+    for (int i = 0; i < M; ++i) {
+      ActLM& a = p.act[(size_t)l * M + i];
+      const LM& x = c->lm[(size_t)l * M + i];
+      a.a = A(R * C * b2); a.mean1 = A(R * f4); a.rstd1 = A(R * f4);
+      a.h1 = A(R * ldh1 * b2); a.qkv = A(R * 3 * C * b2); a.o = A(R * C * b2); a.lse = A(bhT * f4);
+      a.p1 = A(R * ldp * b2); a.x1 = A(R * C * f4);
+      a.c = A(R * C * b2); a.mean2 = A(R * f4); a.rstd2 = A(R * f4);
+      a.f = A(R * 4 * C * b2); a.x2 = A(R * C * f4);
+      a.x2h = c->any_cross ? A(R * C * b2) : 0;
+      if (x.cross) {
+        a.d = A(R * C * b2); a.meanc = A(R * f4); a.rstdc = A(R * f4); a.qc = A(R * C * b2);
+        for (int j = 0; j < M - 1; ++j) {
+          a.kv[j] = A(R * 2 * C * b2);
+          a.ocj[j] = A(R * C * b2);
+          a.lsej[j] = A(bhT * f4);
+        }
+        a.oc = A(R * C * b2); a.pc = A(R * ldp * b2); a.x3 = A(R * C * f4);
+      }
+    }
+  int maxvh = 8, maxv = 8;
+  for (int i = 0; i < M; ++i) { maxvh = std::max(maxvh, c->ldvh[i]); maxv = std::max(maxv, c->ldv[i]); }
+  for (int i = 0; i < M; ++i) {
+    p.lnf16[i] = A(R * C * b2); p.meanf[i] = A(R * f4); p.rstdf[i] = A(R * f4);
+    p.hh[i] = A(R * c->ldvh[i] * b2); p.dlog[i] = A(R * c->ldv[i] * b2);
+  }
+  for (int i = 0; i < M; ++i) {
+    p.dres[i] = A(R * C * f4); p.dres16[i] = A(R * C * b2); p.dln[i] = A(R * C * f4);
+    p.gbig[i] = A(R * std::max(4 * C, maxvh) * b2);
+    p.gdo[i] = A(R * C * b2); p.gq[i] = A(R * C * b2); p.gqkv[i] = A(R * 3 * C * b2);
+    p.gh1[i] = A(R * ldh1 * b2); p.gp[i] = A(R * ldp * b2);
+    for (int j = 0; j < M; ++j) p.dvec[i][j] = A(bhT * f4);
+    if (c->any_cross && c->cfg.cross_attention[i])
+      for (int j = 0; j < M - 1; ++j) p.dkv[i][j] = A(R * 2 * C * b2);
+  }
+  p.total = cur;
+}
+
+template <class T>
+inline T* at(void* ws, size_t off) { return reinterpret_cast<T*>(reinterpret_cast<char*>(ws) + off); }
+
+// grouped-GEMM helpers ------------------------------------------------------------------------
+GemmProblem gp_fwd(const bf16_t* X, int ldx, const bf16_t* Wpk, const Mat& W, int R) {
+  GemmProblem g{};
+  g.A = X; g.lda = ldx; g.B = Wpk + W.pk; g.ldb = W.ld;
+  g.M = R; g.N = W.rows; g.K = W.cols; g.alpha = 1.f;
+  return g;
+}
+// dX = dY W : dY [R, W.rows] (ld ldy), result [R, W.cols]
+GemmProblem gp_dx(const bf16_t* dY, int ldy, const bf16_t* Wpk, const Mat& W, int R) {
+  GemmProblem g{};
+  g.A = dY; g.lda = ldy; g.B = Wpk + W.pk; g.ldb = W.ld;
+  g.M = R; g.N = W.cols; g.K = W.rows; g.alpha = 1.f;
+  return g;
+}
+// dW += dY^T X : out [W.rows, W.cols] fp32 in the grad buffer
+GemmProblem gp_dw(const bf16_t* dY, int ldy, const bf16_t* X, int ldx, float* grads, const Mat& W, int R) {
+  GemmProblem g{};
+  g.A = dY; g.lda = ldy; g.B = X; g.ldb = ldx;
+  g.M = W.rows; g.N = W.cols; g.K = R; g.o32 = grads + W.off; g.ldc = W.cols; g.alpha = 1.f;
+  return g;
+}
+
+int dw_splits(const GemmBatch& gb, int R) {
+  int tiles = 0;
+  for (int g = 0; g < gb.count; ++g)
+    tiles += ((gb.p[g].M + 127) / 128) * ((gb.p[g].N + 127) / 128);
+  if (tiles <= 0) return 1;
+  int s = 512 / tiles;
+  const int maxs = std::max(1, R / 512);
+  return std::max(1, std::min(s, maxs));
+}
+
+struct Runner {
+  mmt_ctx* c;
+  hipStream_t s;
+  void* ws;
+  const float* params;
+  const bf16_t* wpk;
+  int B, R;
+  int rc = MMT_OK;
+
+  bool ok(hipError_t e, const char* what) {
+    if (e != hipSuccess && rc == MMT_OK) rc = fail(c, MMT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return e == hipSuccess;
+  }
+  void gemm(const GemmBatch& b, bool akc, bool bkc, int epi, int splits, const char* what) {
+    if (rc == MMT_OK) ok(mmt_launch_gemm(b, akc, bkc, epi, splits, s), what);
+  }
+  void dwgemm(const GemmBatch& b, const char* what) {
+    if (rc == MMT_OK) ok(mmt_launch_gemm(b, false, false, EPI_ATOMIC_F32, dw_splits(b, R), s), what);
+  }
+  template <class T> T* W(size_t off) { return at<T>(ws, off); }
+  const float* P(int64_t off) { return params + off; }
+};
+
+// -------------------------------------------------------------------------------------------
+// forward
+// -------------------------------------------------------------------------------------------
+int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t* const* tgt, float* const* logits,
+                float* losses) {
+  const int M = c->M, C = c->C, H = c->H, hs = c->hs, R = r.R, B = r.B, T = c->T;
+  const int ldh1 = r8(3 * H * c->hh), ldp = r8(C / 2);
+  const float scale = 1.0f / std::sqrt((float)hs);
+  Plan& p = c->plan;
+  bf16_t* wpk = r.W<bf16_t>(p.pack);
+  r.wpk = wpk;
+  if (!r.ok(mmt_launch_pack(c->d_segs, (int)c->segs.size(), (int64_t)c->tasks.size() / 2, c->d_tasks, r.params, wpk,
+                            r.s), "pack"))
+    return r.rc;
+  {
+    EmbBatch eb{};
+    eb.count = M;
+    for (int i = 0; i < M; ++i) {
+      eb.p[i].idx = idx[i]; eb.p[i].tok = r.P(c->post[i].tok); eb.p[i].pos = r.P(c->pos_off);
+      eb.p[i].x = r.W<float>(p.xemb[i]); eb.p[i].V = c->V[i];
+    }
+    r.ok(mmt_launch_embed_fwd(eb, B, T, C, r.s), "embed_fwd");
+  }
+  std::vector<const float*> xin(M);
+  for (int i = 0; i < M; ++i) xin[i] = r.W<float>(p.xemb[i]);
+  for (int l = 0; l < c->L && r.rc == MMT_OK; ++l) {
+    const LM* x = &c->lm[(size_t)l * M];
+    const ActLM* a = &p.act[(size_t)l * M];
+    LnBatch lb{}; lb.count = M;
+    for (int i = 0; i < M; ++i) {
+      lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].beta = r.P(x[i].ln1b);
+      lb.p[i].y = r.W<bf16_t>(a[i].a); lb.p[i].mean = r.W<float>(a[i].mean1); lb.p[i].rstd = r.W<float>(a[i].rstd1);
+    }
+    r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "ln1_fwd");
+    GemmBatch g{}; g.count = M;
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].a), C, wpk, x[i].W1, R);
+      g.p[i].bias = r.P(x[i].b1); g.p[i].o16 = r.W<bf16_t>(a[i].h1); g.p[i].ldo16 = ldh1;
+    }
+    r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "qkv1");
+    Qkv2Batch qb{}; qb.count = M;
+    for (int i = 0; i < M; ++i) {
+      qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].out = r.W<bf16_t>(a[i].qkv);
+    }
+    r.ok(mmt_launch_qkv2_fwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_fwd");
+    AttnBatch ab{}; ab.count = M;
+    for (int i = 0; i < M; ++i) {
+      AttnProblem& q = ab.p[i];
+      bf16_t* qkv = r.W<bf16_t>(a[i].qkv);
+      q.q = qkv + C; q.q_ld = 3 * C; q.k[0] = qkv; q.v[0] = qkv + 2 * C; q.kv_ld = 3 * C; q.kv_hstride = hs;
+      q.o = r.W<bf16_t>(a[i].o); q.o_ld = C; q.lse[0] = r.W<float>(a[i].lse); q.nstreams = 1;
+    }
+    r.ok(mmt_launch_attn_fwd(ab, B, T, H, hs, scale, r.s), "attn_fwd");
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].o), C, wpk, x[i].P0, R);
+      g.p[i].bias = r.P(x[i].bp0); g.p[i].o16 = r.W<bf16_t>(a[i].p1); g.p[i].ldo16 = ldp;
+    }
+    r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "proj0");
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].p1), ldp, wpk, x[i].P2, R);
+      g.p[i].bias = r.P(x[i].bp2); g.p[i].resid = xin[i]; g.p[i].ldres = C;
+      g.p[i].o32 = r.W<float>(a[i].x1); g.p[i].ldc = C;
+    }
+    r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "proj2");
+    for (int i = 0; i < M; ++i) {
+      lb.p[i].x = r.W<float>(a[i].x1); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].beta = r.P(x[i].ln2b);
+      lb.p[i].y = r.W<bf16_t>(a[i].c); lb.p[i].mean = r.W<float>(a[i].mean2); lb.p[i].rstd = r.W<float>(a[i].rstd2);
+    }
+    r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "ln2_fwd");
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].c), C, wpk, x[i].F0, R);
+      g.p[i].bias = r.P(x[i].bf0); g.p[i].o16 = r.W<bf16_t>(a[i].f); g.p[i].ldo16 = 4 * C;
+    }
+    r.gemm(g, true, true, EPI_BIAS_RELU_BF16, 1, "ffn0");
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].f), 4 * C, wpk, x[i].F2, R);
+      g.p[i].bias = r.P(x[i].bf2); g.p[i].resid = r.W<float>(a[i].x1); g.p[i].ldres = C;
+      g.p[i].o32 = r.W<float>(a[i].x2); g.p[i].ldc = C;
+      if (c->any_cross) { g.p[i].o16 = r.W<bf16_t>(a[i].x2h); g.p[i].ldo16 = C; }
+    }
+    r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "ffn2");
+    std::vector<const float*> xout(M);
+    for (int i = 0; i < M; ++i) xout[i] = r.W<float>(a[i].x2);
+    if (c->any_cross) {
+      std::vector<int> cx;
+      for (int i = 0; i < M; ++i) if (x[i].cross) cx.push_back(i);
+      LnBatch lc{}; lc.count = (int)cx.size();
+      GemmBatch gq{}; gq.count = (int)cx.size();
+      for (size_t u = 0; u < cx.size(); ++u) {
+        const int i = cx[u];
+        lc.p[u].x = r.W<float>(a[i].x2); lc.p[u].gamma = r.P(x[i].lncw); lc.p[u].beta = r.P(x[i].lncb);
+        lc.p[u].y = r.W<bf16_t>(a[i].d); lc.p[u].mean = r.W<float>(a[i].meanc); lc.p[u].rstd = r.W<float>(a[i].rstdc);
+        gq.p[u] = gp_fwd(r.W<bf16_t>(a[i].d), C, wpk, x[i].Wq, R);
+        gq.p[u].o16 = r.W<bf16_t>(a[i].qc); gq.p[u].ldo16 = C;
+      }
+      r.ok(mmt_launch_ln_fwd(lc, R, C, r.s), "lnc_fwd");
+      r.gemm(gq, true, true, EPI_STORE_BF16, 1, "ca_q");
+      // KV projections of the other modalities' post-FFN states, grouped up to 8 per launch
+      GemmBatch gk{}; gk.count = 0;
+      for (int i : cx) {
+        int jj = 0;
+        for (int j = 0; j < M; ++j) {
+          if (j == i) continue;
+          gk.p[gk.count] = gp_fwd(r.W<bf16_t>(a[j].x2h), C, wpk, x[i].Wkv[jj], R);
+          gk.p[gk.count].o16 = r.W<bf16_t>(a[i].kv[jj]); gk.p[gk.count].ldo16 = 2 * C;
+          ++gk.count; ++jj;
+          if (gk.count == MMT_MAX_GROUP) { r.gemm(gk, true, true, EPI_STORE_BF16, 1, "ca_kv"); gk.count = 0; }
+        }
+      }
+      if (gk.count) r.gemm(gk, true, true, EPI_STORE_BF16, 1, "ca_kv");
+      AttnBatch cb{}; cb.count = (int)cx.size();
+      for (size_t u = 0; u < cx.size(); ++u) {
+        const int i = cx[u];
+        AttnProblem& q = cb.p[u];
+        q.q = r.W<bf16_t>(a[i].qc); q.q_ld = C;
+        for (int j = 0; j < M - 1; ++j) {
+          bf16_t* kv = r.W<bf16_t>(a[i].kv[j]);
+          q.k[j] = kv; q.v[j] = kv + hs; q.oj[j] = r.W<bf16_t>(a[i].ocj[j]); q.lse[j] = r.W<float>(a[i].lsej[j]);
+        }
+        q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(a[i].oc); q.o_ld = C; q.nstreams = M - 1;
+      }
+      r.ok(mmt_launch_attn_fwd(cb, B, T, H, hs, scale, r.s), "ca_attn_fwd");
+      GemmBatch g0{}; g0.count = (int)cx.size();
+      GemmBatch g2{}; g2.count = (int)cx.size();
+      for (size_t u = 0; u < cx.size(); ++u) {
+        const int i = cx[u];
+        g0.p[u] = gp_fwd(r.W<bf16_t>(a[i].oc), C, wpk, x[i].C0, R);
+        g0.p[u].bias = r.P(x[i].bc0); g0.p[u].o16 = r.W<bf16_t>(a[i].pc); g0.p[u].ldo16 = ldp;
+        g2.p[u] = gp_fwd(r.W<bf16_t>(a[i].pc), ldp, wpk, x[i].C2, R);
+        g2.p[u].bias = r.P(x[i].bc2); g2.p[u].resid = r.W<float>(a[i].x2); g2.p[u].ldres = C;
+        g2.p[u].o32 = r.W<float>(a[i].x3); g2.p[u].ldc = C;
+        xout[i] = r.W<float>(a[i].x3);
+      }
+      r.gemm(g0, true, true, EPI_BIAS_TANH_BF16, 1, "ca_proj0");
+      r.gemm(g2, true, true, EPI_BIAS_RESID_F32, 1, "ca_proj2");
+    }
+    xin = xout;
+  }
+  if (r.rc != MMT_OK) return r.rc;
+  // post block + CE
+  LnBatch lf{}; lf.count = M;
+  GemmBatch h0{}; h0.count = M;
+  GemmBatch h2{}; h2.count = M;
+  for (int i = 0; i < M; ++i) {
+    lf.p[i].x = xin[i]; lf.p[i].gamma = r.P(c->post[i].lnw); lf.p[i].beta = r.P(c->post[i].lnb);
+    lf.p[i].y = r.W<bf16_t>(p.lnf16[i]); lf.p[i].mean = r.W<float>(p.meanf[i]); lf.p[i].rstd = r.W<float>(p.rstdf[i]);
+    h0.p[i] = gp_fwd(r.W<bf16_t>(p.lnf16[i]), C, wpk, c->post[i].H0, R);
+    h0.p[i].bias = r.P(c->post[i].b0); h0.p[i].o16 = r.W<bf16_t>(p.hh[i]); h0.p[i].ldo16 = c->ldvh[i];
+    h2.p[i] = gp_fwd(r.W<bf16_t>(p.hh[i]), c->ldvh[i], wpk, c->post[i].H2, R);
+    h2.p[i].bias = r.P(c->post[i].b2); h2.p[i].o32 = logits[i]; h2.p[i].ldc = c->V[i];
+  }
+  r.ok(mmt_launch_ln_fwd(lf, R, C, r.s), "lnf_fwd");
+  r.gemm(h0, true, true, EPI_BIAS_TANH_BF16, 1, "head0");
+  r.gemm(h2, true, true, EPI_STORE_F32, 1, "head2");
+  if (tgt && r.rc == MMT_OK) {
+    r.ok(hipMemsetAsync(losses, 0, sizeof(float) * M, r.s), "memset losses");
+    CeBatch cb{}; cb.count = M;
+    for (int i = 0; i < M; ++i) {
+      cb.p[i].logits = logits[i]; cb.p[i].tgt = tgt[i]; cb.p[i].dlogits = r.W<bf16_t>(p.dlog[i]);
+      cb.p[i].loss = losses + i; cb.p[i].V = c->V[i]; cb.p[i].ld_d = c->ldv[i];
+    }
+    r.ok(mmt_launch_ce_fwd(cb, R, r.s), "ce_fwd");
+  }
+  return r.rc;
+}
+
+// -------------------------------------------------------------------------------------------
+// backward stages: 0 = post block, 1..L = layers L-1..0, L+1 = embeddings
+// -------------------------------------------------------------------------------------------
+void colsum_add(Runner& r, ColsumBatch& cb, int u, const bf16_t* x, int ld, float* out, int N, const float* aptr,
+                float alpha) {
+  cb.p[u].x = x; cb.p[u].ld = ld; cb.p[u].out = out; cb.p[u].N = N; cb.p[u].alpha_ptr = aptr; cb.p[u].alpha = alpha;
+}
+
+int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads, float* grads) {
+  const int M = c->M, C = c->C, H = c->H, hs = c->hs, R = r.R, B = r.B, T = c->T, L = c->L;
+  const int ldh1 = r8(3 * H * c->hh), ldp = r8(C / 2);
+  const float scale = 1.0f / std::sqrt((float)hs);
+  Plan& p = c->plan;
+  const bf16_t* wpk = r.W<bf16_t>(p.pack);
+  if (stage == 0) {
+    HIPCHK(c, hipMemsetAsync(grads, 0, sizeof(float) * c->nparams, r.s));
+    const float invR = 1.0f / (float)R;
+    GemmBatch dw{}; dw.count = M;
+    GemmBatch dx{}; dx.count = M;
+    ColsumBatch cs{}; cs.count = M;
+    for (int i = 0; i < M; ++i) {
+      const PostM& q = c->post[i];
+      const bf16_t* dl = r.W<bf16_t>(p.dlog[i]);
+      dw.p[i] = gp_dw(dl, c->ldv[i], r.W<bf16_t>(p.hh[i]), c->ldvh[i], grads, q.H2, R);
+      dw.p[i].alpha_ptr = loss_grads + i; dw.p[i].alpha = invR;
+      colsum_add(r, cs, i, dl, c->ldv[i], grads + q.b2, c->V[i], loss_grads + i, invR);
+      dx.p[i] = gp_dx(dl, c->ldv[i], wpk, q.H2, R);
+      dx.p[i].alpha_ptr = loss_grads + i; dx.p[i].alpha = invR;
+      dx.p[i].aux = r.W<bf16_t>(p.hh[i]); dx.p[i].ldaux = c->ldvh[i];
+      dx.p[i].o16 = r.W<bf16_t>(p.gbig[i]); dx.p[i].ldo16 = c->ldvh[i];
+    }
+    r.dwgemm(dw, "head2_dw");
+    r.ok(mmt_launch_colsum(cs, R, r.s), "head2_db");
+    r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "head2_dx");
+    for (int i = 0; i < M; ++i) {
+      const PostM& q = c->post[i];
+      const bf16_t* g = r.W<bf16_t>(p.gbig[i]);
+      dw.p[i] = gp_dw(g, c->ldvh[i], r.W<bf16_t>(p.lnf16[i]), C, grads, q.H0, R);
+      colsum_add(r, cs, i, g, c->ldvh[i], grads + q.b0, c->V[i] / 2, nullptr, 1.f);
+      dx.p[i] = gp_dx(g, c->ldvh[i], wpk, q.H0, R);
+      dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
+    }
+    r.dwgemm(dw, "head0_dw");
+    r.ok(mmt_launch_colsum(cs, R, r.s), "head0_db");
+    r.gemm(dx, true, false, EPI_STORE_F32, 1, "head0_dx");
+    LnBatch lb{}; lb.count = M;
+    std::vector<const float*> xfin(M);
+    for (int i = 0; i < M; ++i) {
+      const ActLM& a = p.act[(size_t)(L - 1) * M + i];
+      xfin[i] = (L == 0) ? r.W<float>(p.xemb[i]) : (c->lm[(size_t)(L - 1) * M + i].cross ? r.W<float>(a.x3) : r.W<float>(a.x2));
+      r.ok(hipMemsetAsync(r.W<float>(p.dres[i]), 0, sizeof(float) * (size_t)R * C, r.s), "memset dres");
+      lb.p[i].x = xfin[i]; lb.p[i].gamma = r.P(c->post[i].lnw); lb.p[i].mean = r.W<float>(p.meanf[i]);
+      lb.p[i].rstd = r.W<float>(p.rstdf[i]); lb.p[i].dy = r.W<float>(p.dln[i]); lb.p[i].dx = r.W<float>(p.dres[i]);
+      lb.p[i].dx16 = r.W<bf16_t>(p.dres16[i]);
+      lb.p[i].dgamma = grads + c->post[i].lnw; lb.p[i].dbeta = grads + c->post[i].lnb;
+    }
+    r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "lnf_bwd");
+    return r.rc;
+  }
+  // layer stage
+  const int l = L - stage;
+  const LM* x = &c->lm[(size_t)l * M];
+  const ActLM* a = &p.act[(size_t)l * M];
+  std::vector<const float*> xin(M);
+  for (int i = 0; i < M; ++i) {
+    if (l == 0) xin[i] = r.W<float>(p.xemb[i]);
+    else {
+      const ActLM& pa = p.act[(size_t)(l - 1) * M + i];
+      xin[i] = c->lm[(size_t)(l - 1) * M + i].cross ? r.W<float>(pa.x3) : r.W<float>(pa.x2);
+    }
+  }
+  if (c->any_cross) {
+    std::vector<int> cx;
+    for (int i = 0; i < M; ++i) if (x[i].cross) cx.push_back(i);
+    const int nc = (int)cx.size();
+    GemmBatch dw{}; dw.count = nc;
+    GemmBatch dx{}; dx.count = nc;
+    ColsumBatch cs{}; cs.count = nc;
+    for (int u = 0; u < nc; ++u) {
+      const int i = cx[u];
+      const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
+      dw.p[u] = gp_dw(g, C, r.W<bf16_t>(a[i].pc), ldp, grads, x[i].C2, R);
+      colsum_add(r, cs, u, g, C, grads + x[i].bc2, C, nullptr, 1.f);
+      dx.p[u] = gp_dx(g, C, wpk, x[i].C2, R);
+      dx.p[u].aux = r.W<bf16_t>(a[i].pc); dx.p[u].ldaux = ldp; dx.p[u].o16 = r.W<bf16_t>(p.gp[i]); dx.p[u].ldo16 = ldp;
+    }
+    r.dwgemm(dw, "ca_proj2_dw");
+    r.ok(mmt_launch_colsum(cs, R, r.s), "ca_proj2_db");
+    r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "ca_proj2_dx");
+    for (int u = 0; u < nc; ++u) {
+      const int i = cx[u];
+      const bf16_t* g = r.W<bf16_t>(p.gp[i]);
+      dw.p[u] = gp_dw(g, ldp, r.W<bf16_t>(a[i].oc), C, grads, x[i].C0, R);
+      colsum_add(r, cs, u, g, ldp, grads + x[i].bc0, C / 2, nullptr, 1.f);
+      dx.p[u] = gp_dx(g, ldp, wpk, x[i].C0, R);
+      dx.p[u].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[u].ldo16 = C;
+    }
+    r.dwgemm(dw, "ca_proj0_dw");
+    r.ok(mmt_launch_colsum(cs, R, r.s), "ca_proj0_db");
+    r.gemm(dx, true, false, EPI_STORE_BF16, 1, "ca_proj0_dx");
+    AttnBatch ab{}; ab.count = nc;
+    for (int u = 0; u < nc; ++u) {
+      const int i = cx[u];
+      AttnProblem& q = ab.p[u];
+      q.q = r.W<bf16_t>(a[i].qc); q.q_ld = C;
+      for (int j = 0; j < M - 1; ++j) {
+        bf16_t* kv = r.W<bf16_t>(a[i].kv[j]);
+        q.k[j] = kv; q.v[j] = kv + hs; q.oj[j] = r.W<bf16_t>(a[i].ocj[j]); q.lse[j] = r.W<float>(a[i].lsej[j]);
+        q.dvec[j] = r.W<float>(p.dvec[i][j]);
+        bf16_t* dkv = r.W<bf16_t>(p.dkv[i][j]);
+        q.dk[j] = dkv; q.dv[j] = dkv + hs;
+      }
+      q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(a[i].oc); q.o_ld = C; q.nstreams = M - 1;
+      q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dq = r.W<bf16_t>(p.gq[i]); q.dq_ld = C;
+      q.dkv_ld = 2 * C; q.dkv_hstride = 2 * hs;
+    }
+    r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "ca_attn_bwd");
+    for (int u = 0; u < nc; ++u) {
+      const int i = cx[u];
+      const bf16_t* g = r.W<bf16_t>(p.gq[i]);
+      dw.p[u] = gp_dw(g, C, r.W<bf16_t>(a[i].d), C, grads, x[i].Wq, R);
+      dx.p[u] = gp_dx(g, C, wpk, x[i].Wq, R);
+      dx.p[u].o32 = r.W<float>(p.dln[i]); dx.p[u].ldc = C;
+    }
+    r.dwgemm(dw, "ca_q_dw");
+    r.gemm(dx, true, false, EPI_STORE_F32, 1, "ca_q_dx");
+    LnBatch lc{}; lc.count = nc;
+    for (int u = 0; u < nc; ++u) {
+      const int i = cx[u];
+      lc.p[u].x = r.W<float>(a[i].x2); lc.p[u].gamma = r.P(x[i].lncw); lc.p[u].mean = r.W<float>(a[i].meanc);
+      lc.p[u].rstd = r.W<float>(a[i].rstdc); lc.p[u].dy = r.W<float>(p.dln[i]); lc.p[u].dx = r.W<float>(p.dres[i]);
+      lc.p[u].dgamma = grads + x[i].lncw; lc.p[u].dbeta = grads + x[i].lncb;
+    }
+    r.ok(mmt_launch_ln_bwd(lc, R, C, r.s), "lnc_bwd");
+    // KV projections: dWkv += dkv^T x2_j ; dres[j] += dkv Wkv (one launch per query modality:
+    // different query modalities accumulate into the same dres[j])
+    for (int i : cx) {
+      GemmBatch kw{}; kw.count = 0;
+      GemmBatch kx{}; kx.count = 0;
+      int jj = 0;
+      for (int j = 0; j < M; ++j) {
+        if (j == i) continue;
+        const bf16_t* g = r.W<bf16_t>(p.dkv[i][jj]);
+        kw.p[kw.count++] = gp_dw(g, 2 * C, r.W<bf16_t>(a[j].x2h), C, grads, x[i].Wkv[jj], R);
+        GemmProblem d = gp_dx(g, 2 * C, wpk, x[i].Wkv[jj], R);
+        d.o32 = r.W<float>(p.dres[j]); d.ldc = C;
+        kx.p[kx.count++] = d;
+        ++jj;
+        if (kw.count == MMT_MAX_GROUP) {
+          r.dwgemm(kw, "ca_kv_dw"); r.gemm(kx, true, false, EPI_ACC_F32, 1, "ca_kv_dx");
+          kw.count = 0; kx.count = 0;
+        }
+      }
+      if (kw.count) { r.dwgemm(kw, "ca_kv_dw"); r.gemm(kx, true, false, EPI_ACC_F32, 1, "ca_kv_dx"); }
+    }
+    for (int i = 0; i < M; ++i)
+      r.ok(mmt_launch_f32_to_bf16(r.W<float>(p.dres[i]), r.W<bf16_t>(p.dres16[i]), (int64_t)R * C, r.s), "dres16");
+  }
+  if (r.rc != MMT_OK) return r.rc;
+  // FFN
+  GemmBatch dw{}; dw.count = M;
+  GemmBatch dx{}; dx.count = M;
+  ColsumBatch cs{}; cs.count = M;
+  LnBatch lb{}; lb.count = M;
+  for (int i = 0; i < M; ++i) {
+    const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
+    dw.p[i] = gp_dw(g, C, r.W<bf16_t>(a[i].f), 4 * C, grads, x[i].F2, R);
+    colsum_add(r, cs, i, g, C, grads + x[i].bf2, C, nullptr, 1.f);
+    dx.p[i] = gp_dx(g, C, wpk, x[i].F2, R);
+    dx.p[i].aux = r.W<bf16_t>(a[i].f); dx.p[i].ldaux = 4 * C; dx.p[i].o16 = r.W<bf16_t>(p.gbig[i]); dx.p[i].ldo16 = 4 * C;
+  }
+  r.dwgemm(dw, "ffn2_dw");
+  r.ok(mmt_launch_colsum(cs, R, r.s), "ffn2_db");
+  r.gemm(dx, true, false, EPI_DRELU_BF16, 1, "ffn2_dx");
+  for (int i = 0; i < M; ++i) {
+    const bf16_t* g = r.W<bf16_t>(p.gbig[i]);
+    dw.p[i] = gp_dw(g, 4 * C, r.W<bf16_t>(a[i].c), C, grads, x[i].F0, R);
+    colsum_add(r, cs, i, g, 4 * C, grads + x[i].bf0, 4 * C, nullptr, 1.f);
+    dx.p[i] = gp_dx(g, 4 * C, wpk, x[i].F0, R);
+    dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
+  }
+  r.dwgemm(dw, "ffn0_dw");
+  r.ok(mmt_launch_colsum(cs, R, r.s), "ffn0_db");
+  r.gemm(dx, true, false, EPI_STORE_F32, 1, "ffn0_dx");
+  for (int i = 0; i < M; ++i) {
+    lb.p[i].x = r.W<float>(a[i].x1); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].mean = r.W<float>(a[i].mean2);
+    lb.p[i].rstd = r.W<float>(a[i].rstd2); lb.p[i].dy = r.W<float>(p.dln[i]); lb.p[i].dx = r.W<float>(p.dres[i]);
+    lb.p[i].dx16 = r.W<bf16_t>(p.dres16[i]); lb.p[i].dgamma = grads + x[i].ln2w; lb.p[i].dbeta = grads + x[i].ln2b;
+  }
+  r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln2_bwd");
+  // SA output projection
+  for (int i = 0; i < M; ++i) {
+    const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
+    dw.p[i] = gp_dw(g, C, r.W<bf16_t>(a[i].p1), ldp, grads, x[i].P2, R);
+    colsum_add(r, cs, i, g, C, grads + x[i].bp2, C, nullptr, 1.f);
+    dx.p[i] = gp_dx(g, C, wpk, x[i].P2, R);
+    dx.p[i].aux = r.W<bf16_t>(a[i].p1); dx.p[i].ldaux = ldp; dx.p[i].o16 = r.W<bf16_t>(p.gp[i]); dx.p[i].ldo16 = ldp;
+  }
+  r.dwgemm(dw, "proj2_dw");
+  r.ok(mmt_launch_colsum(cs, R, r.s), "proj2_db");
+  r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "proj2_dx");
+  for (int i = 0; i < M; ++i) {
+    const bf16_t* g = r.W<bf16_t>(p.gp[i]);
+    dw.p[i] = gp_dw(g, ldp, r.W<bf16_t>(a[i].o), C, grads, x[i].P0, R);
+    colsum_add(r, cs, i, g, ldp, grads + x[i].bp0, C / 2, nullptr, 1.f);
+    dx.p[i] = gp_dx(g, ldp, wpk, x[i].P0, R);
+    dx.p[i].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[i].ldo16 = C;
+  }
+  r.dwgemm(dw, "proj0_dw");
+  r.ok(mmt_launch_colsum(cs, R, r.s), "proj0_db");
+  r.gemm(dx, true, false, EPI_STORE_BF16, 1, "proj0_dx");
+  AttnBatch ab{}; ab.count = M;
+  for (int i = 0; i < M; ++i) {
+    AttnProblem& q = ab.p[i];
+    bf16_t* qkv = r.W<bf16_t>(a[i].qkv);
+    bf16_t* gq = r.W<bf16_t>(p.gqkv[i]);
+    q.q = qkv + C; q.q_ld = 3 * C; q.k[0] = qkv; q.v[0] = qkv + 2 * C; q.kv_ld = 3 * C; q.kv_hstride = hs;
+    q.o = r.W<bf16_t>(a[i].o); q.o_ld = C; q.lse[0] = r.W<float>(a[i].lse); q.nstreams = 1;
+    q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dvec[0] = r.W<float>(p.dvec[i][0]);
+    q.dq = gq + C; q.dq_ld = 3 * C; q.dk[0] = gq; q.dv[0] = gq + 2 * C; q.dkv_ld = 3 * C; q.dkv_hstride = hs;
+  }
+  r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "attn_bwd");
+  Qkv2Batch qb{}; qb.count = M;
+  for (int i = 0; i < M; ++i) {
+    qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].dout = r.W<bf16_t>(p.gqkv[i]);
+    qb.p[i].dh1 = r.W<bf16_t>(p.gh1[i]); qb.p[i].dw2 = grads + x[i].w2;
+  }
+  r.ok(mmt_launch_qkv2_bwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_bwd");
+  for (int i = 0; i < M; ++i) {
+    const bf16_t* g = r.W<bf16_t>(p.gh1[i]);
+    dw.p[i] = gp_dw(g, ldh1, r.W<bf16_t>(a[i].a), C, grads, x[i].W1, R);
+    colsum_add(r, cs, i, g, ldh1, grads + x[i].b1, 3 * H * c->hh, nullptr, 1.f);
+    dx.p[i] = gp_dx(g, ldh1, wpk, x[i].W1, R);
+    dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
+  }
+  r.dwgemm(dw, "qkv1_dw");
+  r.ok(mmt_launch_colsum(cs, R, r.s), "qkv1_db");
+  r.gemm(dx, true, false, EPI_STORE_F32, 1, "qkv1_dx");
+  for (int i = 0; i < M; ++i) {
+    lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].mean = r.W<float>(a[i].mean1);
+    lb.p[i].rstd = r.W<float>(a[i].rstd1); lb.p[i].dy = r.W<float>(p.dln[i]); lb.p[i].dx = r.W<float>(p.dres[i]);
+    lb.p[i].dx16 = r.W<bf16_t>(p.dres16[i]); lb.p[i].dgamma = grads + x[i].ln1w; lb.p[i].dbeta = grads + x[i].ln1b;
+  }
+  r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln1_bwd");
+  return r.rc;
+}
+
+int check_cfg(const mmt_config* cfg, std::string& msg) {
+  if (!cfg) { msg = "null config"; return MMT_ERR_INVALID; }
+  const int M = cfg->num_modalities;
+  if (M < 1 || M > MAXM) { msg = "num_modalities must be 1..8"; return MMT_ERR_INVALID; }
+  if (cfg->n_embd <= 0 || cfg->n_head <= 0 || cfg->n_layer < 0 || cfg->block_size <= 0) {
+    msg = "n_embd, n_head, block_size must be positive and n_layer >= 0"; return MMT_ERR_INVALID;
+  }
+  if (cfg->n_embd % cfg->n_head) { msg = "n_embd must be divisible by n_head"; return MMT_ERR_UNSUPPORTED; }
+  const int hs = cfg->n_embd / cfg->n_head;
+  if (!(hs == 8 || hs == 16 || hs == 24 || hs == 32 || hs == 48 || hs == 64)) {
+    msg = "head size n_embd/n_head must be one of 8,16,24,32,48,64 (got " + std::to_string(hs) + ")";
+    return MMT_ERR_UNSUPPORTED;
+  }
+  if (cfg->n_embd % 8 || cfg->n_embd > 1024) { msg = "n_embd must be a multiple of 8 and <= 1024"; return MMT_ERR_UNSUPPORTED; }
+  for (int i = 0; i < M; ++i)
+    if (cfg->vocab_sizes[i] < 1) { msg = "vocab sizes must be >= 1"; return MMT_ERR_INVALID; }
+  if (cfg->dropout < 0.f || cfg->dropout >= 1.f) { msg = "dropout must be in [0, 1)"; return MMT_ERR_INVALID; }
+  return MMT_OK;
+}
+
+int ensure_device_tables(mmt_ctx* c) {
+  if (c->d_segs || c->segs.empty()) return MMT_OK;
+  HIPCHK(c, hipMalloc(&c->d_segs, sizeof(PackSeg) * c->segs.size()));
+  HIPCHK(c, hipMalloc(&c->d_tasks, sizeof(int) * c->tasks.size()));
+  HIPCHK(c, hipMemcpy(c->d_segs, c->segs.data(), sizeof(PackSeg) * c->segs.size(), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_tasks, c->tasks.data(), sizeof(int) * c->tasks.size(), hipMemcpyHostToDevice));
+  return MMT_OK;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+const char* mmt_version(void) { return "mmt_hip 0.1 gfx950"; }
+const char* mmt_create_error(void) { return g_create_err.c_str(); }
+
+mmt_ctx* mmt_create(const mmt_config* cfg) {
+  std::string msg;
+  if (check_cfg(cfg, msg) != MMT_OK) { g_create_err = msg; return nullptr; }
+  mmt_ctx* c = new (std::nothrow) mmt_ctx();
+  if (!c) { g_create_err = "out of memory"; return nullptr; }
+  c->cfg = *cfg;
+  c->M = cfg->num_modalities; c->C = cfg->n_embd; c->H = cfg->n_head; c->L = cfg->n_layer; c->T = cfg->block_size;
+  c->hs = c->C / c->H; c->hh = c->hs / 2;
+  for (int i = 0; i < c->M; ++i) {
+    c->V[i] = cfg->vocab_sizes[i];
+    if (cfg->cross_attention[i] && c->M > 1) { c->any_cross = true; ++c->ncross; }
+  }
+  if (c->M - 1 > MMT_MAX_STREAMS) { g_create_err = "too many KV streams"; delete c; return nullptr; }
+  build_layout(c);
+  return c;
+}
+
+void mmt_destroy(mmt_ctx* c) {
+  if (!c) return;
+  if (c->d_segs) (void)hipFree(c->d_segs);
+  if (c->d_tasks) (void)hipFree(c->d_tasks);
+  delete c;
+}
+
+const char* mmt_last_error(const mmt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+int64_t mmt_param_count(const mmt_ctx* c) { return c ? c->nparams : 0; }
+int64_t mmt_param_active_count(const mmt_ctx* c) { return c ? c->nactive : 0; }
+int32_t mmt_tensor_count(const mmt_ctx* c) { return c ? (int32_t)c->tensors.size() : 0; }
+
+int mmt_tensor_info(const mmt_ctx* c, int32_t i, char* name, int32_t cap, int64_t* off, int32_t* nd, int64_t* shape,
+                    int32_t* kind) {
+  if (!c || i < 0 || i >= (int32_t)c->tensors.size()) return MMT_ERR_INVALID;
+  const TensorInfo& t = c->tensors[i];
+  if (name && cap > 0) {
+    std::strncpy(name, t.name.c_str(), cap - 1);
+    name[cap - 1] = 0;
+  }
+  if (off) *off = t.off;
+  if (nd) *nd = t.nd;
+  if (shape) { shape[0] = t.shape[0]; shape[1] = t.shape[1]; }
+  if (kind) *kind = t.kind;
+  return MMT_OK;
+}
+
+int64_t mmt_workspace_bytes(mmt_ctx* c, int32_t batch) {
+  if (!c || batch < 1) return -1;
+  make_plan(c, batch);
+  c->last_B = batch;
+  c->fwd_ready = false;
+  return (int64_t)c->plan.total;
+}
+
+int mmt_forward(mmt_ctx* c, void* stream, int32_t batch, const int64_t* const* idx, const int64_t* const* tgt,
+                const float* params, float* const* logits, float* losses, void* workspace, int32_t training) {
+  if (!c) return MMT_ERR_INVALID;
+  if (batch < 1 || !idx || !params || !logits || !workspace) return fail(c, MMT_ERR_INVALID, "mmt_forward: null argument");
+  if (training && c->cfg.dropout > 0.f)
+    return fail(c, MMT_ERR_UNSUPPORTED, "dropout > 0 in training mode is not implemented by this build");
+  if (c->plan.B != batch) make_plan(c, batch);
+  int rc = ensure_device_tables(c);
+  if (rc) return rc;
+  Runner r{c, (hipStream_t)stream, workspace, params, nullptr, batch, batch * c->T};
+  c->fwd_ready = false;
+  for (int i = 0; i < c->M; ++i) c->last_idx[i] = idx[i];
+  rc = run_forward(c, r, idx, tgt, logits, losses);
+  if (rc == MMT_OK && tgt) c->fwd_ready = true;
+  c->last_training = training != 0;
+  return rc;
+}
+
+int32_t mmt_backward_stage_count(const mmt_ctx* c) { return c ? c->L + 2 : 0; }
+
+int mmt_backward_stage_range(const mmt_ctx* c, int32_t stage, int64_t* begin, int64_t* end) {
+  if (!c || stage < 0 || stage > c->L + 1) return MMT_ERR_INVALID;
+  int64_t b, e;
+  if (stage == 0) { b = c->post_begin; e = c->post_end; }
+  else if (stage == c->L + 1) { b = c->emb_begin; e = c->emb_end; }
+  else { const int l = c->L - stage; b = c->layer_begin[l]; e = c->layer_end[l]; }
+  if (begin) *begin = b;
+  if (end) *end = e;
+  return MMT_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* loss_grads, const float* params,
+                       float* grads, void* workspace) {
+  if (!c) return MMT_ERR_INVALID;
+  if (!c->fwd_ready) return fail(c, MMT_ERR_STATE, "mmt_backward: no forward with targets to differentiate");
+  if (stage < 0 || stage > c->L + 1) return fail(c, MMT_ERR_INVALID, "bad backward stage");
+  Runner r{c, (hipStream_t)stream, workspace, params, nullptr, c->plan.B, c->plan.B * c->T};
+  if (stage == c->L + 1) {
+    EmbBatch eb{}; eb.count = c->M;
+    for (int i = 0; i < c->M; ++i) {
+      eb.p[i].idx = c->last_idx[i]; eb.p[i].dx = r.W<float>(c->plan.dres[i]);
+      eb.p[i].dtok = grads + c->post[i].tok; eb.p[i].dpos = grads + c->pos_off; eb.p[i].V = c->V[i];
+    }
+    r.ok(mmt_launch_embed_bwd(eb, r.B, c->T, c->C, r.s), "embed_bwd");
+    return r.rc;
+  }
+  return run_backward_stage(c, r, stage, loss_grads, grads);
+}
+
+int mmt_backward(mmt_ctx* c, void* stream, const float* loss_grads, const float* params, float* grads,
+                 void* workspace) {
+  if (!c) return MMT_ERR_INVALID;
+  for (int s = 0; s < c->L + 2; ++s) {
+    const int rc = mmt_backward_stage(c, stream, s, loss_grads, params, grads, workspace);
+    if (rc) return rc;
+  }
+  return MMT_OK;
+}
+
+int mmt_adamw_step(mmt_ctx* c, void* stream, float* params, const float* grads, float* m, float* v, int64_t n,
+                   int64_t step, float lr, float b1, float b2, float eps, float wd) {
+  if (step < 1 || !params || !grads || !m || !v) return fail(c, MMT_ERR_INVALID, "mmt_adamw_step: bad argument");
+  const double bc1 = 1.0 - std::pow((double)b1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)b2, (double)step);
+  const hipError_t e = mmt_launch_adamw(params, grads, m, v, n, lr, b1, b2, eps, wd, (float)bc1,
+                                        (float)std::sqrt(bc2), (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, MMT_ERR_HIP, std::string("adamw: ") + hipGetErrorString(e));
+  return MMT_OK;
+}
+
+int mmt_eval_direction(mmt_ctx* c, void* stream, int32_t batch, int32_t T, int32_t V, const float* logits,
+                       const int64_t* xb, const int64_t* yb, const double* vocab, int32_t is_percent,
+                       int32_t* wins_losses, double* certainty_sum) {
+  const hipError_t e = mmt_launch_eval_direction(logits, xb, yb, vocab, batch, T, V, is_percent, wins_losses,
+                                                 certainty_sum, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(c, MMT_ERR_HIP, std::string("eval_direction: ") + hipGetErrorString(e));
+  return MMT_OK;
+}
+
+}  // extern "C"
+

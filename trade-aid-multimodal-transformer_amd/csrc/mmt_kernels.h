@@ -1,0 +1,167 @@
+// Host-visible launcher declarations for the gfx950 kernels (internal to libmmt_hip.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef MMT_MAX_GROUP
+#define MMT_MAX_GROUP 8
+#endif
+typedef uint16_t bf16_t;
+
+// ------------------------------------------------------------------------------------------
+// GEMM: C[M,N] (epi)= alpha * sum_k A(m,k) B(k,n), bf16 operands, fp32 MFMA accumulation.
+//   A(m,k) = a_kc ? A[m*lda + k] : A[k*lda + m]
+//   B(k,n) = b_kc ? B[n*ldb + k] : B[k*ldb + n]
+// Forward linear   Y = X W^T : a_kc=1, b_kc=1
+// Backward data   dX = dY W  : a_kc=1, b_kc=0
+// Weight grad     dW = dY^T X: a_kc=0, b_kc=0 (split-K, atomic fp32 accumulate)
+// ------------------------------------------------------------------------------------------
+enum MmtEpi {
+  EPI_STORE_BF16 = 0,   // o16 = alpha*acc (+bias)
+  EPI_BIAS_TANH_BF16,   // o16 = tanh(alpha*acc + bias)
+  EPI_BIAS_RELU_BF16,   // o16 = relu(alpha*acc + bias)
+  EPI_BIAS_RESID_F32,   // o32 = resid + alpha*acc + bias ; o16 (optional) = bf16 copy
+  EPI_STORE_F32,        // o32 = alpha*acc (+bias)
+  EPI_DTANH_BF16,       // o16 = alpha*acc * (1 - aux^2)
+  EPI_DRELU_BF16,       // o16 = aux > 0 ? alpha*acc : 0
+  EPI_ACC_F32,          // o32 += alpha*acc
+  EPI_ATOMIC_F32,       // atomicAdd(o32, alpha*acc)
+  EPI_COUNT
+};
+
+struct GemmProblem {
+  const bf16_t* A;
+  const bf16_t* B;
+  const float* bias;
+  const bf16_t* aux;
+  const float* resid;
+  float* o32;
+  bf16_t* o16;
+  const float* alpha_ptr;  // optional device scalar multiplier
+  float alpha;
+  int M, N, K;
+  int lda, ldb, ldc, ldaux, ldres, ldo16;
+};
+
+struct GemmBatch {
+  GemmProblem p[MMT_MAX_GROUP];
+  int count;
+};
+
+hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, int splits, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
+// LayerNorm (eps = 1e-5, weight+bias). Row-major [R, C] fp32 in, bf16 out; saves mean/rstd.
+// ------------------------------------------------------------------------------------------
+struct LnProblem {
+  const float* x;       // [R, C]
+  const float* gamma;
+  const float* beta;
+  bf16_t* y;            // [R, C] (ld = C)
+  float* mean;          // [R]
+  float* rstd;          // [R]
+  // backward
+  const float* dy;      // [R, C] fp32
+  float* dx;            // [R, C] fp32, ACCUMULATED (dx += ...)
+  bf16_t* dx16;         // optional bf16 copy of the accumulated dx
+  float* dgamma;        // atomic accumulate
+  float* dbeta;
+};
+struct LnBatch { LnProblem p[MMT_MAX_GROUP]; int count; };
+hipError_t mmt_launch_ln_fwd(const LnBatch& b, int R, int C, hipStream_t s);
+hipError_t mmt_launch_ln_bwd(const LnBatch& b, int R, int C, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
+// Causal attention, one wave per 32-row tile, 32x32x16 bf16 MFMA, fp32 online softmax.
+// Q rows (b*T+t) at q + row*q_ld + head*hs ; stream j K/V at k[j]/v[j] + row*kv_ld + head*kv_hstride.
+// Output O (sum over streams of the per-stream normalised outputs) at o + row*o_ld + head*hs.
+// ------------------------------------------------------------------------------------------
+#define MMT_MAX_STREAMS 8
+struct AttnProblem {
+  const bf16_t* q; int q_ld;
+  const bf16_t* k[MMT_MAX_STREAMS];
+  const bf16_t* v[MMT_MAX_STREAMS];
+  int kv_ld, kv_hstride;
+  bf16_t* o; int o_ld;
+  bf16_t* oj[MMT_MAX_STREAMS];   // per-stream normalised outputs (nullable when nstreams == 1)
+  float* lse[MMT_MAX_STREAMS];   // [B*H*T] per stream
+  // backward
+  const bf16_t* dout; int dout_ld;
+  float* dvec[MMT_MAX_STREAMS];  // rowsum(dO * O_j) per stream [B*H*T]
+  bf16_t* dq; int dq_ld;
+  bf16_t* dk[MMT_MAX_STREAMS];
+  bf16_t* dv[MMT_MAX_STREAMS];
+  int dkv_ld, dkv_hstride;
+  int nstreams;
+};
+struct AttnBatch { AttnProblem p[MMT_MAX_GROUP]; int count; };
+hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
+hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
+// Per-head Q/K/V stage 2: block-diagonal [hs/2 -> hs] maps (model.py:39,44,49), nblk = 3*H.
+//   out[r, blk*hs + o] = sum_i W2[blk][o][i] * h1[r, blk*hs/2 + i]
+// ------------------------------------------------------------------------------------------
+struct Qkv2Problem {
+  const bf16_t* h1;    // [R, nblk*hs/2] (ld = ld_h1)
+  const float* w2;     // [nblk][hs][hs/2] fp32 master weights
+  bf16_t* out;         // [R, nblk*hs] (ld = ld_out)
+  // backward
+  const bf16_t* dout;  // [R, nblk*hs]
+  bf16_t* dh1;         // [R, nblk*hs/2] = (W2^T dout) * (1 - h1^2)
+  float* dw2;          // atomic accumulate [nblk][hs][hs/2]
+};
+struct Qkv2Batch { Qkv2Problem p[MMT_MAX_GROUP]; int count; };
+hipError_t mmt_launch_qkv2_fwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s);
+hipError_t mmt_launch_qkv2_bwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s);
+
+// ------------------------------------------------------------------------------------------
+// Misc elementwise / reduction kernels
+// ------------------------------------------------------------------------------------------
+struct EmbProblem {
+  const int64_t* idx;   // [B*T]
+  const float* tok;     // [V, C]
+  const float* pos;     // [T, C]
+  float* x;             // [B*T, C]
+  const float* dx;      // backward: [B*T, C]
+  float* dtok;          // atomic
+  float* dpos;          // atomic
+  int V;
+};
+struct EmbBatch { EmbProblem p[MMT_MAX_GROUP]; int count; };
+hipError_t mmt_launch_embed_fwd(const EmbBatch& b, int B, int T, int C, hipStream_t s);
+hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStream_t s);
+
+struct CeProblem {
+  const float* logits;   // [R, V]
+  const int64_t* tgt;    // [R]
+  bf16_t* dlogits;       // [R, ld_d] = softmax - onehot (pad columns zeroed)
+  float* loss;           // scalar, atomic accumulate of mean
+  int V, ld_d;
+};
+struct CeBatch { CeProblem p[MMT_MAX_GROUP]; int count; };
+hipError_t mmt_launch_ce_fwd(const CeBatch& b, int R, hipStream_t s);
+
+struct ColsumProblem {
+  const bf16_t* x;       // [R, ld]
+  float* out;            // [N] atomic accumulate alpha * sum_r x[r, n]
+  const float* alpha_ptr;
+  float alpha;
+  int N, ld;
+};
+struct ColsumBatch { ColsumProblem p[MMT_MAX_GROUP]; int count; };
+hipError_t mmt_launch_colsum(const ColsumBatch& b, int R, hipStream_t s);
+
+// fp32 -> bf16 copy of a list of matrices (rows x cols, src ld = cols, dst ld = dld, pad zeroed).
+// task_dev holds (segment, first row) pairs; each task (one block) packs 32 rows.
+struct PackSeg { int64_t src_off; int64_t dst_off; int rows; int cols; int dld; int pad_; };
+hipError_t mmt_launch_pack(const PackSeg* segs_dev, int nseg, int64_t ntasks, const int* task_dev, const float* src,
+                           bf16_t* dst, hipStream_t s);
+hipError_t mmt_launch_f32_to_bf16(const float* src, bf16_t* dst, int64_t n, hipStream_t s);
+
+hipError_t mmt_launch_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                            float eps, float wd, float bc1, float bc2_sqrt, hipStream_t s);
+
+hipError_t mmt_launch_eval_direction(const float* logits, const int64_t* xb, const int64_t* yb, const double* vocab,
+                                     int B, int T, int V, int is_pct, int* wins_losses, double* certainty,
+                                     hipStream_t s);

@@ -1,0 +1,147 @@
+// Single-problem C-ABI wrappers over the kernel launchers (include/mmt.h, mmt_op_*), used by the
+// kernel-level parity tests. Same kernels the engine launches, one group member.
+#include <hip/hip_runtime.h>
+
+#include "mmt.h"
+#include "mmt_kernels.h"
+
+static int st(hipError_t e) { return e == hipSuccess ? MMT_OK : MMT_ERR_HIP; }
+
+extern "C" {
+
+int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t splits, int32_t M, int32_t N,
+                int32_t K, const void* A, int32_t lda, const void* B, int32_t ldb, const float* bias, const void* aux,
+                int32_t ldaux, const float* resid, int32_t ldres, float* o32, int32_t ldc, void* o16, int32_t ldo16,
+                float alpha) {
+  if (epi < 0 || epi >= EPI_COUNT || M < 0 || N < 0 || K < 0) return MMT_ERR_INVALID;
+  if ((lda & 7) || (ldb & 7)) return MMT_ERR_INVALID;  // 16-byte operand staging
+  GemmBatch b{};
+  b.count = 1;
+  GemmProblem& p = b.p[0];
+  p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb; p.bias = bias;
+  p.aux = (const bf16_t*)aux; p.ldaux = ldaux; p.resid = resid; p.ldres = ldres; p.o32 = o32; p.ldc = ldc;
+  p.o16 = (bf16_t*)o16; p.ldo16 = ldo16; p.alpha = alpha; p.M = M; p.N = N; p.K = K;
+  const hipError_t e = mmt_launch_gemm(b, a_kc != 0, b_kc != 0, epi, splits, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return MMT_ERR_UNSUPPORTED;
+  return st(e);
+}
+
+int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
+                         void* y16, float* mean, float* rstd) {
+  LnBatch b{};
+  b.count = 1;
+  b.p[0].x = x; b.p[0].gamma = gamma; b.p[0].beta = beta; b.p[0].y = (bf16_t*)y16; b.p[0].mean = mean; b.p[0].rstd = rstd;
+  return st(mmt_launch_ln_fwd(b, R, C, (hipStream_t)stream));
+}
+
+int mmt_op_layernorm_bwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* mean,
+                         const float* rstd, const float* dy, float* dx, void* dx16, float* dgamma, float* dbeta) {
+  LnBatch b{};
+  b.count = 1;
+  LnProblem& p = b.p[0];
+  p.x = x; p.gamma = gamma; p.mean = (float*)mean; p.rstd = (float*)rstd; p.dy = dy; p.dx = dx; p.dx16 = (bf16_t*)dx16;
+  p.dgamma = dgamma; p.dbeta = dbeta;
+  return st(mmt_launch_ln_bwd(b, R, C, (hipStream_t)stream));
+}
+
+static void fill_attn(AttnProblem& p, int nstreams, const void* q, int q_ld, const void* const* k, const void* const* v,
+                      int kv_ld, int kv_hstride) {
+  p.q = (const bf16_t*)q; p.q_ld = q_ld; p.kv_ld = kv_ld; p.kv_hstride = kv_hstride; p.nstreams = nstreams;
+  for (int j = 0; j < nstreams; ++j) { p.k[j] = (const bf16_t*)k[j]; p.v[j] = (const bf16_t*)v[j]; }
+}
+
+int mmt_op_attention_fwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams, const void* q,
+                         int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld, int32_t kv_hstride,
+                         void* o, int32_t o_ld, void* const* oj, float* const* lse) {
+  if (nstreams < 1 || nstreams > MMT_MAX_STREAMS) return MMT_ERR_INVALID;
+  AttnBatch b{};
+  b.count = 1;
+  AttnProblem& p = b.p[0];
+  fill_attn(p, nstreams, q, q_ld, k, v, kv_ld, kv_hstride);
+  p.o = (bf16_t*)o; p.o_ld = o_ld;
+  for (int j = 0; j < nstreams; ++j) {
+    p.oj[j] = oj ? (bf16_t*)oj[j] : nullptr;
+    p.lse[j] = lse[j];
+  }
+  const float scale = 1.0f / __builtin_sqrtf((float)hs);
+  const hipError_t e = mmt_launch_attn_fwd(b, B, T, H, hs, scale, (hipStream_t)stream);
+  return e == hipErrorInvalidValue ? MMT_ERR_UNSUPPORTED : st(e);
+}
+
+int mmt_op_attention_bwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams, const void* q,
+                         int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld, int32_t kv_hstride,
+                         const void* o, int32_t o_ld, const void* const* oj, const float* const* lse, const void* dout,
+                         int32_t dout_ld, float* const* dvec, void* dq, int32_t dq_ld, void* const* dk, void* const* dv,
+                         int32_t dkv_ld, int32_t dkv_hstride) {
+  if (nstreams < 1 || nstreams > MMT_MAX_STREAMS) return MMT_ERR_INVALID;
+  AttnBatch b{};
+  b.count = 1;
+  AttnProblem& p = b.p[0];
+  fill_attn(p, nstreams, q, q_ld, k, v, kv_ld, kv_hstride);
+  p.o = (bf16_t*)o; p.o_ld = o_ld;
+  for (int j = 0; j < nstreams; ++j) {
+    p.oj[j] = oj ? (bf16_t*)oj[j] : nullptr;
+    p.lse[j] = (float*)lse[j];
+    p.dvec[j] = dvec[j];
+    p.dk[j] = (bf16_t*)dk[j];
+    p.dv[j] = (bf16_t*)dv[j];
+  }
+  p.dout = (const bf16_t*)dout; p.dout_ld = dout_ld; p.dq = (bf16_t*)dq; p.dq_ld = dq_ld;
+  p.dkv_ld = dkv_ld; p.dkv_hstride = dkv_hstride;
+  const float scale = 1.0f / __builtin_sqrtf((float)hs);
+  const hipError_t e = mmt_launch_attn_bwd(b, B, T, H, hs, scale, (hipStream_t)stream);
+  return e == hipErrorInvalidValue ? MMT_ERR_UNSUPPORTED : st(e);
+}
+
+int mmt_op_qkv2_fwd(void* stream, int32_t R, int32_t nblk, int32_t hs, const void* h1, int32_t ld_h1, const float* w2,
+                    void* out, int32_t ld_out) {
+  Qkv2Batch b{};
+  b.count = 1;
+  b.p[0].h1 = (const bf16_t*)h1; b.p[0].w2 = w2; b.p[0].out = (bf16_t*)out;
+  const hipError_t e = mmt_launch_qkv2_fwd(b, R, nblk, hs, ld_h1, ld_out, (hipStream_t)stream);
+  return e == hipErrorInvalidValue ? MMT_ERR_UNSUPPORTED : st(e);
+}
+
+int mmt_op_qkv2_bwd(void* stream, int32_t R, int32_t nblk, int32_t hs, const void* h1, int32_t ld_h1, const float* w2,
+                    const void* dout, int32_t ld_out, void* dh1, float* dw2) {
+  Qkv2Batch b{};
+  b.count = 1;
+  b.p[0].h1 = (const bf16_t*)h1; b.p[0].w2 = w2; b.p[0].dout = (const bf16_t*)dout; b.p[0].dh1 = (bf16_t*)dh1;
+  b.p[0].dw2 = dw2;
+  const hipError_t e = mmt_launch_qkv2_bwd(b, R, nblk, hs, ld_h1, ld_out, (hipStream_t)stream);
+  return e == hipErrorInvalidValue ? MMT_ERR_UNSUPPORTED : st(e);
+}
+
+int mmt_op_colsum(void* stream, int32_t R, int32_t N, const void* x, int32_t ld, float* out, float alpha) {
+  ColsumBatch b{};
+  b.count = 1;
+  b.p[0].x = (const bf16_t*)x; b.p[0].ld = ld; b.p[0].out = out; b.p[0].N = N; b.p[0].alpha = alpha;
+  return st(mmt_launch_colsum(b, R, (hipStream_t)stream));
+}
+
+int mmt_op_cross_entropy(void* stream, int32_t R, int32_t V, const float* logits, const int64_t* tgt, void* dlogits,
+                         int32_t ld_d, float* loss) {
+  CeBatch b{};
+  b.count = 1;
+  b.p[0].logits = logits; b.p[0].tgt = tgt; b.p[0].dlogits = (bf16_t*)dlogits; b.p[0].loss = loss; b.p[0].V = V;
+  b.p[0].ld_d = ld_d;
+  return st(mmt_launch_ce_fwd(b, R, (hipStream_t)stream));
+}
+
+int mmt_op_embedding_fwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx, const float* tok,
+                         const float* pos, float* x) {
+  EmbBatch b{};
+  b.count = 1;
+  b.p[0].idx = idx; b.p[0].tok = tok; b.p[0].pos = pos; b.p[0].x = x; b.p[0].V = V;
+  return st(mmt_launch_embed_fwd(b, B, T, C, (hipStream_t)stream));
+}
+
+int mmt_op_embedding_bwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx, const float* dx,
+                         float* dtok, float* dpos) {
+  EmbBatch b{};
+  b.count = 1;
+  b.p[0].idx = idx; b.p[0].dx = dx; b.p[0].dtok = dtok; b.p[0].dpos = dpos; b.p[0].V = V;
+  return st(mmt_launch_embed_bwd(b, B, T, C, (hipStream_t)stream));
+}
+
+}  // extern "C"

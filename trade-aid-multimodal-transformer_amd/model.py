@@ -1,0 +1,262 @@
+"""model.py — drop-in `MultimodalTransformer` backed by the gfx950 HIP library (libmmt_hip.so).
+
+Same constructor, forward signature, state_dict keys/shapes and train()/eval() behaviour as the
+reference (model.py:355-402 of tsnuk/trade-AId-multimodal-transformer):
+
+    m = MultimodalTransformer(num_modalities, vocab_sizes, all_modality_params).to("cuda")
+    logits_list, losses_list = m(idx_list, targets_list)
+    sum(losses_list).backward()
+
+Differences that are by design:
+  * all parameters live in ONE flat fp32 `nn.Parameter` (`flat_params`); `state_dict()` /
+    `load_state_dict()` expose and accept exactly the reference's per-head keys (including
+    the `.tril` buffers, emitted as one shared tensor), so reference checkpoints round-trip;
+  * compute runs in bf16 on MFMA with fp32 accumulation, fp32 master weights/residual stream;
+  * forward/backward run only on a ROCm device (there is no CPU path: the CPU oracle lives in
+    oracle/ and is test infrastructure only);
+  * logits are outputs without autograd history (the reference training loop differentiates
+    only the losses; main.py:646-649);
+  * sequences must be exactly block_size long (the training/eval batches always are).
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+
+import mmt_lib as ML
+from config_utils import _get_block_size, _get_dropout, _get_n_embd, _get_n_head, _get_n_layer
+
+
+class _MmtStep(torch.autograd.Function):
+    """One forward through the C-ABI; its backward is mmt_backward into a fresh flat grad."""
+
+    @staticmethod
+    def forward(ctx, flat, owner, training, n_mod, *tensors):
+        idx = list(tensors[:n_mod])
+        tgt = list(tensors[n_mod:]) if len(tensors) > n_mod else None
+        logits, losses = owner._launch_forward(flat, idx, tgt, training)
+        ctx.owner = owner
+        ctx.gen = owner._gen
+        ctx.keep = (idx, tgt)  # the engine reads the token ids again in the embedding backward
+        ctx.n_tensors = len(tensors)
+        ctx.set_materialize_grads(False)
+        ctx.mark_non_differentiable(*logits)
+        if losses is None:
+            return tuple(logits)
+        return (*logits, losses)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        g_losses = grads[-1]
+        nones = (None,) * (3 + ctx.n_tensors)
+        if g_losses is None:
+            return nones
+        owner = ctx.owner
+        if owner._gen != ctx.gen:
+            raise RuntimeError("MultimodalTransformer: backward of a stale forward (another forward ran in between); "
+                               "the saved activations live in one workspace per model")
+        grad = owner._launch_backward(g_losses)
+        return (grad,) + nones
+
+
+class MultimodalTransformer(nn.Module):
+    """Reference model.py:355-402 (see module docstring)."""
+
+    def __init__(self, num_modalities, vocab_sizes, all_modality_params):
+        super().__init__()
+        self.num_modalities = int(num_modalities)
+        self.vocab_sizes = [int(v) for v in vocab_sizes]
+        self.all_modality_params = all_modality_params
+        M = self.num_modalities
+        if not (1 <= M <= ML.MAX_MOD):
+            raise ValueError("num_modalities must be 1..8")
+        self.n_embd, self.n_head, self.n_layer = _get_n_embd(), _get_n_head(), _get_n_layer()
+        self.block_size, self.dropout_p = _get_block_size(), float(_get_dropout())
+        cfg = ML.MmtConfig()
+        cfg.num_modalities = M
+        cfg.n_embd, cfg.n_head, cfg.n_layer, cfg.block_size = self.n_embd, self.n_head, self.n_layer, self.block_size
+        for i in range(M):
+            cfg.vocab_sizes[i] = self.vocab_sizes[i]
+            cfg.cross_attention[i] = 1 if all_modality_params[i][8] else 0  # model.py:196
+        cfg.dropout = self.dropout_p
+        cfg.seed = 0
+        L = ML.lib()
+        ctx = L.mmt_create(ctypes.byref(cfg))
+        if not ctx:
+            raise ML.MmtError("mmt_create failed: " + L.mmt_create_error().decode())
+        self._ctx = ctypes.c_void_p(ctx)
+        n = L.mmt_param_count(self._ctx)
+        self._n_active = L.mmt_param_active_count(self._ctx)
+        self._tensors = []
+        name = ctypes.create_string_buffer(256)
+        off, nd, shape, kind = ML.c_i64(), ML.c_i32(), (ML.c_i64 * 2)(), ML.c_i32()
+        for i in range(L.mmt_tensor_count(self._ctx)):
+            ML.check(L.mmt_tensor_info(self._ctx, i, name, 256, ctypes.byref(off), ctypes.byref(nd), shape,
+                                       ctypes.byref(kind)), self._ctx, "mmt_tensor_info")
+            shp = tuple(shape[d] for d in range(nd.value))
+            self._tensors.append((name.value.decode(), off.value, shp, kind.value))
+        self._tril_keys = self._make_tril_keys()
+        flat = torch.zeros(n, dtype=torch.float32)
+        self._init_flat(flat)
+        self.flat_params = nn.Parameter(flat)
+        self.flat_params._mmt_active = self._n_active  # AdamW updates only this prefix
+        self._ws = None
+        self._ws_batch = -1
+        self._ws_bytes = {}
+        self._gen = 0
+        self._last = None
+
+    # ------------------------------------------------------------------ layout / state_dict
+    def _make_tril_keys(self):
+        keys = []
+        for l in range(self.n_layer):
+            for i in range(self.num_modalities):
+                for h in range(self.n_head):
+                    keys.append(f"blocks.{l}.sa_layers.{i}.heads.{h}.tril")
+            for i in range(self.num_modalities):
+                if self.all_modality_params[i][8]:
+                    for h in range(self.n_head):
+                        keys.append(f"blocks.{l}.cross_attention_layers.{i}.heads.{h}.tril")
+        return keys
+
+    def _init_flat(self, flat):
+        """model.py:372-378: Linear/Embedding weights N(0, 0.02), biases 0; LayerNorm 1 / 0."""
+        for name, off, shp, kind in self._tensors:
+            n = 1
+            for s in shp:
+                n *= s
+            v = flat[off:off + n]
+            if kind == 0:
+                v.normal_(0.0, 0.02)
+            elif kind == 2:
+                v.fill_(1.0)
+            else:
+                v.zero_()
+
+    def _view(self, off, shp, base=None):
+        base = self.flat_params if base is None else base
+        n = 1
+        for s in shp:
+            n *= s
+        return base[off:off + n].view(shp)
+
+    def named_reference_tensors(self):
+        """(reference state_dict key, view into flat_params) for every parameter."""
+        for name, off, shp, _ in self._tensors:
+            yield name, self._view(off, shp)
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        base = self.flat_params if keep_vars else self.flat_params.detach()
+        for name, off, shp, _ in self._tensors:
+            destination[prefix + name] = self._view(off, shp, base)
+        if self._tril_keys:
+            T = self.block_size
+            tril = torch.tril(torch.ones(T, T, device=self.flat_params.device))
+            for k in self._tril_keys:
+                destination[prefix + k] = tril  # one shared storage (saved once by torch.save)
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        known = set()
+        with torch.no_grad():
+            for name, off, shp, _ in self._tensors:
+                key = prefix + name
+                known.add(key)
+                if key not in state_dict:
+                    missing_keys.append(key)
+                    continue
+                src = state_dict[key]
+                if tuple(src.shape) != tuple(shp):
+                    error_msgs.append(f"size mismatch for {key}: copying a param with shape {tuple(src.shape)}, "
+                                      f"the shape in current model is {tuple(shp)}.")
+                    continue
+                self._view(off, shp).copy_(src)
+        T = self.block_size
+        for k in self._tril_keys:
+            key = prefix + k
+            known.add(key)
+            if key not in state_dict:
+                missing_keys.append(key)
+            elif tuple(state_dict[key].shape) != (T, T):
+                error_msgs.append(f"size mismatch for {key}: {tuple(state_dict[key].shape)} vs {(T, T)}")
+        if strict:
+            for key in state_dict.keys():
+                if key.startswith(prefix) and key not in known:
+                    unexpected_keys.append(key)
+        self._gen += 1
+
+    # ------------------------------------------------------------------ execution
+    def _workspace(self, B, device):
+        if B not in self._ws_bytes:
+            self._ws_bytes[B] = ML.lib().mmt_workspace_bytes(self._ctx, B)
+            if self._ws_bytes[B] < 0:
+                raise ML.MmtError("mmt_workspace_bytes failed")
+        if self._ws is None or self._ws_batch != B or self._ws.device != device:
+            self._ws = None
+            self._ws = torch.empty(self._ws_bytes[B], dtype=torch.uint8, device=device)
+            self._ws_batch = B
+        return self._ws
+
+    def _launch_forward(self, flat, idx, tgt, training):
+        L = ML.lib()
+        dev = flat.device
+        B, T = idx[0].shape
+        ws = self._workspace(B, dev)
+        logits = [torch.empty(B, T, V, dtype=torch.float32, device=dev) for V in self.vocab_sizes]
+        losses = torch.empty(self.num_modalities, dtype=torch.float32, device=dev) if tgt is not None else None
+        idx_arr = ML.ptr_array(idx)
+        tgt_arr = ML.ptr_array(tgt) if tgt is not None else None
+        rc = L.mmt_forward(self._ctx, ML.stream_ptr(dev), B, idx_arr, tgt_arr, ML.ptr(flat), ML.ptr_array(logits),
+                           ML.ptr(losses), ML.ptr(ws), 1 if training else 0)
+        ML.check(rc, self._ctx, "mmt_forward")
+        self._gen += 1
+        self._last = (flat, idx, tgt)
+        return logits, losses
+
+    def _launch_backward(self, g_losses):
+        L = ML.lib()
+        flat = self._last[0]
+        g = g_losses.detach().to(dtype=torch.float32).contiguous()
+        grad = torch.empty_like(flat)
+        rc = L.mmt_backward(self._ctx, ML.stream_ptr(flat.device), ML.ptr(g), ML.ptr(flat), ML.ptr(grad),
+                            ML.ptr(self._ws))
+        ML.check(rc, self._ctx, "mmt_backward")
+        return grad
+
+    def forward(self, idx_list, targets_list=None):
+        """model.py:380-402: returns (logits_list, losses_list | None)."""
+        M = self.num_modalities
+        if len(idx_list) != M:
+            raise ValueError(f"expected {M} index tensors, got {len(idx_list)}")
+        flat = self.flat_params
+        if flat.device.type != "cuda":
+            raise RuntimeError("MultimodalTransformer (libmmt_hip) runs only on a ROCm GPU: call .to('cuda') "
+                               "(there is no CPU path)")
+        B, T = idx_list[0].shape
+        if T != self.block_size:
+            raise NotImplementedError(f"sequence length {T} != block_size {self.block_size}")
+        idx = [t.to(device=flat.device, dtype=torch.long).contiguous() for t in idx_list]
+        for t in idx:
+            if tuple(t.shape) != (B, T):
+                raise ValueError("all modalities must share the [B, T] batch shape")
+        tensors = list(idx)
+        if targets_list is not None:
+            tensors += [t.to(device=flat.device, dtype=torch.long).contiguous() for t in targets_list]
+        training = bool(self.training and self.dropout_p > 0.0)
+        outs = _MmtStep.apply(flat, self, training, M, *tensors)
+        logits = list(outs[:M])
+        if targets_list is None:
+            return logits, None
+        losses = outs[M]
+        return logits, [losses[i] for i in range(M)]
+
+    def generate(self, idx_list, max_new_tokens=1, modality_to_generate=0):
+        raise NotImplementedError("generate (model.py:404-446) is outside this build's hot path (SURVEY.md §8f)")
+
+    def __del__(self):
+        try:
+            if getattr(self, "_ctx", None):
+                ML.lib().mmt_destroy(self._ctx)
+                self._ctx = None
+        except Exception:
+            pass
