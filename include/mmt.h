@@ -101,6 +101,26 @@ int mmt_eval_direction(mmt_ctx* ctx, void* stream, int32_t batch, int32_t T, int
                        const int64_t* xb, const int64_t* yb, const double* vocab, int32_t is_percent,
                        int32_t* wins_losses, double* certainty_sum);
 
+/* live kernel timing: HIP events on the caller's stream around every engine launch labelled
+ * `label` (e.g. "ffn0", "ffn0_dw", "attn_fwd"); NULL or "" disables. mmt_probe_read waits for
+ * the recorded events and returns the summed device time and the number of launches. */
+int mmt_probe_set(mmt_ctx* ctx, const char* label);
+int mmt_probe_read(mmt_ctx* ctx, double* total_ms, int64_t* launches);
+
+/* ---- device-resident batcher: get_batch (training_utils.py:333-384) on HBM token streams ---- */
+/* in-place random walk of one int32 training stream (data_utils.py:342-351 as reached through
+ * training_utils.py:350-360): x += uniform{0,+-1..+-r} where r < x < V - r */
+int mmt_batch_jitter(void* stream, int32_t* data, int64_t n, int32_t rand_size, int32_t vocab_size, uint64_t seed,
+                     uint64_t counter);
+/* batch start indices uniform over valid positions (generate_batch_starting_indices,
+ * training_utils.py:33-181): cum_valid / file_start int64 [nfiles] describe the split */
+int mmt_batch_indices(void* stream, int32_t batch, const int64_t* cum_valid, const int64_t* file_start, int32_t nfiles,
+                      int32_t first_offset, uint64_t seed, uint64_t counter, int64_t* ix);
+/* x[m] = data[m][ix : ix+T], y[m] = data[m][ix+1 : ix+T+1] (int64 [batch, T]); data/x/y are host
+ * arrays of nmod device pointers */
+int mmt_batch_gather(void* stream, int32_t nmod, const int32_t* const* data, const int64_t* ix, int32_t batch,
+                     int32_t T, int64_t* const* x, int64_t* const* y);
+
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
 int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t splits, int32_t M, int32_t N,
                 int32_t K, const void* A, int32_t lda, const void* B, int32_t ldb, const float* bias,

@@ -139,7 +139,8 @@ def test_gemm_identity_asymmetric():
     A = torch.eye(n, device=DEV)
     Bm = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n) % 17 - 8
     o32 = torch.zeros(n, n, device=DEV)
-    rc = ML.lib().mmt_op_gemm(_s(), 1, 1, ML.EPI["store_f32"], 1, n, n, n, ML.ptr(bf(A)), n, ML.ptr(bf(Bm)), n, None,
+    Ab, Bb = bf(A), bf(Bm)  # keep both alive for the launch
+    rc = ML.lib().mmt_op_gemm(_s(), 1, 1, ML.EPI["store_f32"], 1, n, n, n, ML.ptr(Ab), n, ML.ptr(Bb), n, None,
                               None, 0, None, 0, ML.ptr(o32), n, None, 0, 1.0)
     assert rc == 0
     _sync()
@@ -202,7 +203,7 @@ def test_attention_fwd_bwd(B, T, H, hs, ns):
     # cross-attention layout: q [R, C], per-stream kv [R, 2C] with per-head [K|V] otherwise
     if ns == 1:
         qkv = bf(torch.randn(R, 3 * C, device=DEV))
-        q, q_ld = qkv[:, C:], 3 * C
+        q, q_ld = qkv[:, C:2 * C], 3 * C
         ks, vs = [qkv[:, :C]], [qkv[:, 2 * C:]]
         kv_ld, kv_hs = 3 * C, hs
         kptr, vptr = [qkv], [qkv[:, 2 * C:]]

@@ -47,18 +47,18 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 // LDS transposed read (ds_read_b64_tr_b16): per 16-lane group, 4 rows x 16 columns of 16-bit
 // elements; lane 4q+p supplies the address of row q, columns 4p..4p+3; lane i of the group
 // receives column i of the 4 rows (row q in element q).
+// `lds_addr` must point into a __shared__ array; the explicit cast is an addrspacecast
+// (generic -> LDS), never an integer truncation of the flat address.
 __device__ __forceinline__ s16x4 lds_tr16(const void* lds_addr) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)lds_addr));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lds_addr));
 }
 
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+// whole-vector shuffle + bitcast: element-wise scalar bit_casts of the tr16 result were
+// mis-lowered by hipcc (ROCm 7.2) into duplicated register halves
 __device__ __forceinline__ bf16x8 join4(s16x4 lo, s16x4 hi) {
-  bf16x8 r;
-  r[0] = __builtin_bit_cast(__bf16, lo[0]); r[1] = __builtin_bit_cast(__bf16, lo[1]);
-  r[2] = __builtin_bit_cast(__bf16, lo[2]); r[3] = __builtin_bit_cast(__bf16, lo[3]);
-  r[4] = __builtin_bit_cast(__bf16, hi[0]); r[5] = __builtin_bit_cast(__bf16, hi[1]);
-  r[6] = __builtin_bit_cast(__bf16, hi[2]); r[7] = __builtin_bit_cast(__bf16, hi[3]);
-  return r;
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 // counter-based hash RNG (dropout masks); identical in forward and backward

@@ -104,6 +104,8 @@ struct mmt_ctx {
   uint64_t step_counter = 0;
   const int64_t* last_idx[MAXM] = {};  // forward token ids, read by the embedding backward stage
   std::string err;
+  std::string probe_label;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> probe_events;
   int ldv[MAXM], ldvh[MAXM];
 };
 
@@ -390,11 +392,30 @@ struct Runner {
     if (e != hipSuccess && rc == MMT_OK) rc = fail(c, MMT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
     return e == hipSuccess;
   }
+  // live kernel timing (mmt_probe_set): HIP events on this stream around launches with a matching label
+  bool probing(const char* what) const { return !c->probe_label.empty() && c->probe_label == what; }
+  void probe_begin(const char* what) {
+    if (!probing(what)) return;
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+    hipEventRecord(a, s);
+    c->probe_events.push_back({a, b});
+  }
+  void probe_end(const char* what) {
+    if (!probing(what) || c->probe_events.empty()) return;
+    hipEventRecord(c->probe_events.back().second, s);
+  }
   void gemm(const GemmBatch& b, bool akc, bool bkc, int epi, int splits, const char* what) {
-    if (rc == MMT_OK) ok(mmt_launch_gemm(b, akc, bkc, epi, splits, s), what);
+    if (rc != MMT_OK) return;
+    probe_begin(what);
+    ok(mmt_launch_gemm(b, akc, bkc, epi, splits, s), what);
+    probe_end(what);
   }
   void dwgemm(const GemmBatch& b, const char* what) {
-    if (rc == MMT_OK) ok(mmt_launch_gemm(b, false, false, EPI_ATOMIC_F32, dw_splits(b, R), s), what);
+    if (rc != MMT_OK) return;
+    probe_begin(what);
+    ok(mmt_launch_gemm(b, false, false, EPI_ATOMIC_F32, dw_splits(b, R), s), what);
+    probe_end(what);
   }
   template <class T> T* W(size_t off) { return at<T>(ws, off); }
   const float* P(int64_t off) { return params + off; }
@@ -452,7 +473,9 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       q.q = qkv + C; q.q_ld = 3 * C; q.k[0] = qkv; q.v[0] = qkv + 2 * C; q.kv_ld = 3 * C; q.kv_hstride = hs;
       q.o = r.W<bf16_t>(a[i].o); q.o_ld = C; q.lse[0] = r.W<float>(a[i].lse); q.nstreams = 1;
     }
+    r.probe_begin("attn_fwd");
     r.ok(mmt_launch_attn_fwd(ab, B, T, H, hs, scale, r.s), "attn_fwd");
+    r.probe_end("attn_fwd");
     for (int i = 0; i < M; ++i) {
       g.p[i] = gp_fwd(r.W<bf16_t>(a[i].o), C, wpk, x[i].P0, R);
       g.p[i].bias = r.P(x[i].bp0); g.p[i].o16 = r.W<bf16_t>(a[i].p1); g.p[i].ldo16 = ldp;
@@ -521,7 +544,9 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         }
         q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(a[i].oc); q.o_ld = C; q.nstreams = M - 1;
       }
+      r.probe_begin("ca_attn_fwd");
       r.ok(mmt_launch_attn_fwd(cb, B, T, H, hs, scale, r.s), "ca_attn_fwd");
+      r.probe_end("ca_attn_fwd");
       GemmBatch g0{}; g0.count = (int)cx.size();
       GemmBatch g2{}; g2.count = (int)cx.size();
       for (size_t u = 0; u < cx.size(); ++u) {
@@ -682,7 +707,9 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dq = r.W<bf16_t>(p.gq[i]); q.dq_ld = C;
       q.dkv_ld = 2 * C; q.dkv_hstride = 2 * hs;
     }
+    r.probe_begin("ca_attn_bwd");
     r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "ca_attn_bwd");
+    r.probe_end("ca_attn_bwd");
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
       const bf16_t* g = r.W<bf16_t>(p.gq[i]);
@@ -787,7 +814,9 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dvec[0] = r.W<float>(p.dvec[i][0]);
     q.dq = gq + C; q.dq_ld = 3 * C; q.dk[0] = gq; q.dv[0] = gq + 2 * C; q.dkv_ld = 3 * C; q.dkv_hstride = hs;
   }
+  r.probe_begin("attn_bwd");
   r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "attn_bwd");
+  r.probe_end("attn_bwd");
   Qkv2Batch qb{}; qb.count = M;
   for (int i = 0; i < M; ++i) {
     qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].dout = r.W<bf16_t>(p.gqkv[i]);
@@ -873,6 +902,7 @@ void mmt_destroy(mmt_ctx* c) {
   if (!c) return;
   if (c->d_segs) (void)hipFree(c->d_segs);
   if (c->d_tasks) (void)hipFree(c->d_tasks);
+  for (auto& e : c->probe_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   delete c;
 }
 
@@ -989,3 +1019,27 @@ int mmt_eval_direction(mmt_ctx* c, void* stream, int32_t batch, int32_t T, int32
 
 }  // extern "C"
 
+
+// live per-kernel timing: HIP events around every launch labelled `label` (e.g. "ffn0", "ffn0_dw",
+// "attn_fwd"), on the caller's stream, so bench.py can price one kernel inside the timed region.
+extern "C" int mmt_probe_set(mmt_ctx* c, const char* label) {
+  if (!c) return MMT_ERR_INVALID;
+  for (auto& e : c->probe_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  c->probe_events.clear();
+  c->probe_label = label ? label : "";
+  return MMT_OK;
+}
+
+extern "C" int mmt_probe_read(mmt_ctx* c, double* total_ms, int64_t* launches) {
+  if (!c) return MMT_ERR_INVALID;
+  double tot = 0.0;
+  for (auto& e : c->probe_events) {
+    float ms = 0.f;
+    if (hipEventSynchronize(e.second) != hipSuccess) return fail(c, MMT_ERR_HIP, "probe event sync");
+    if (hipEventElapsedTime(&ms, e.first, e.second) != hipSuccess) return fail(c, MMT_ERR_HIP, "probe elapsed");
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = (int64_t)c->probe_events.size();
+  return MMT_OK;
+}

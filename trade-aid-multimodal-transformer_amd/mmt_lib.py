@@ -63,6 +63,12 @@ _SIGS = {
     "mmt_backward_stage": (c_i32, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mmt_adamw_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32]),
     "mmt_eval_direction": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "mmt_probe_set": (c_i32, [c_vp, c_cp]),
+    "mmt_probe_read": (c_i32, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
+    "mmt_batch_jitter":(c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64]),
+    "mmt_batch_indices": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64, c_vp]),
+    "mmt_batch_gather": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), c_vp, c_i32, c_i32, ctypes.POINTER(c_vp),
+                                 ctypes.POINTER(c_vp)]),
     "mmt_op_gemm": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp,
                             c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32]),
     "mmt_op_layernorm_fwd": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -1,0 +1,404 @@
+"""training_utils.py — drop-in for the reference's batch generation, evaluation loop and
+directional metric (reference training_utils.py:33-534), re-designed for a GPU step rate.
+
+Same public names, arguments, module globals (set by main.py, reference main.py:387-396), print
+lines and log lines. What changed underneath:
+  * generate_batch_starting_indices draws its indices with the SAME torch.randint calls as the
+    reference (bit-identical under a seeded torch RNG) but maps them to file positions with a
+    vectorised searchsorted instead of a per-sample Python loop (training_utils.py:156-178);
+  * get_batch keeps the reference's in-place +-1 random walk of the training set, driven by
+    all_modality_params[r][2] (`has_header`, the reference quirk at training_utils.py:353; see
+    DESIGN.md), but jitters and slices with numpy over int64 arrays and hands the batch to the
+    GPU through pinned host buffers (non_blocking copies);
+  * calculate_evaluation_metrics runs the per-sample argmax / direction / softmax-certainty loop
+    (training_utils.py:259-304) as one HIP kernel per modality (mmt_eval_direction) with a single
+    device->host copy, instead of B*V `.item()` syncs.
+"""
+import numbers
+import os
+import random
+from datetime import datetime
+
+import numpy as np
+import torch
+
+import mmt_lib as ML
+from config_utils import _get_batch_size, _get_block_size, _get_config, _get_device, _get_eval_iters
+
+__all__ = ["generate_batch_starting_indices", "get_batch", "estimate_loss", "calculate_evaluation_metrics"]
+
+
+# ------------------------------------------------------------------------------------------
+# batch start indices (reference training_utils.py:33-181)
+# ------------------------------------------------------------------------------------------
+def _split_file_lengths(data_size, split, file_lengths):
+    lens = []
+    acc = 0
+    n = len(file_lengths)
+    for f in range(n):
+        this = file_lengths[f] if split == "train" else file_lengths[n - 1 - f]
+        acc += this
+        if acc <= data_size:
+            lens.append(this)
+        if acc > data_size:
+            lens.append(data_size - (acc - this))
+        if acc >= data_size:
+            if split == "val":
+                lens.reverse()
+            break
+    return lens
+
+
+def generate_batch_starting_indices(data_size, block_size, batch_size, split, file_lengths, is_percents):
+    """Random start indices whose [i, i+block_size] window stays inside one file of the split."""
+    if not isinstance(data_size, int) or data_size <= 0:
+        raise TypeError("'data_size' must be a positive integer.")
+    if not isinstance(block_size, int) or block_size <= 0:
+        raise TypeError("'block_size' must be a positive integer.")
+    if block_size >= data_size:
+        raise ValueError("'block_size' cannot be equal to or greater than 'data_size'.")
+    if not isinstance(batch_size, int) or batch_size <= 0:
+        raise TypeError("'batch_size' must be a positive integer.")
+    if not isinstance(split, str) or split not in ("train", "val"):
+        raise ValueError("'split' must be 'train' or 'val'.")
+    if not isinstance(file_lengths, list) or not len(file_lengths) >= 1:
+        raise TypeError("'file_lengths' must be a list containing at least 1 element.")
+    if not isinstance(is_percents, bool):
+        raise TypeError("'is_percents' must be a boolean.")
+    bxy = block_size + 1
+    off = 1 if is_percents else 0
+    if len(file_lengths) == 1:
+        return torch.randint(off, data_size - bxy + 1, (batch_size,))
+    lens = np.asarray(_split_file_lengths(data_size, split, file_lengths), dtype=np.int64)
+    valid = np.maximum(0, lens - bxy - off + 1)
+    total = int(valid.sum())
+    if total <= 0:
+        raise ValueError("No valid starting positions available for the given block size and file lengths.")
+    init = torch.randint(total, (batch_size,)).numpy()
+    cum_valid = np.cumsum(valid)
+    k = np.searchsorted(cum_valid, init, side="right")  # first file whose cumulative count exceeds init
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    prev = np.concatenate([[0], cum_valid[:-1]])
+    return torch.from_numpy(starts[k] + (init - prev[k]) + off).to(torch.long)
+
+
+# ------------------------------------------------------------------------------------------
+# get_batch (reference training_utils.py:333-384 + data_utils.py:293-358)
+# ------------------------------------------------------------------------------------------
+_pinned = {}
+
+
+def _as_array(r):
+    """Train sets arrive as Python lists (reference main.py:374). Convert once, IN PLACE in the
+    shared list object, so the random walk keeps mutating the one training set as in the reference."""
+    t = all_train_sets[r]
+    if isinstance(t, np.ndarray):
+        return t
+    arr = np.asarray(t.tolist() if isinstance(t, torch.Tensor) else t, dtype=np.int64)
+    all_train_sets[r] = arr
+    return arr
+
+
+def jitter_(arr, rand_size, vocab_size, rng):
+    """Vectorised add_rand_to_data_points: x += uniform choice of {0, +-1 .. +-r} where r < x < V - r."""
+    r = int(rand_size)
+    if r < 1 or r > 3:
+        raise ValueError("rand_size must be an integer between 1 and 3, or null.")
+    elig = (arr > r) & (arr < vocab_size - r)
+    choice = rng.integers(0, 2 * r + 1, size=arr.shape[0])
+    delta = np.where(choice == 0, 0, np.where(choice % 2 == 1, (choice + 1) // 2, -(choice // 2)))
+    arr += np.where(elig, delta, 0)
+    return arr
+
+
+_RING = 4
+_ring_pos = [0]
+_ring_events = [None] * _RING
+
+
+def _pinned_buf(key, shape):
+    b = _pinned.get(key)
+    if b is None or tuple(b.shape) != tuple(shape):
+        b = torch.empty(shape, dtype=torch.long, pin_memory=torch.cuda.is_available())
+        _pinned[key] = b
+    return b
+
+
+def _ring_slot():
+    """Pick the next pinned-buffer set; wait only for the async H2D copy issued from it _RING calls ago."""
+    slot = _ring_pos[0]
+    _ring_pos[0] = (slot + 1) % _RING
+    ev = _ring_events[slot]
+    if ev is not None:
+        ev.synchronize()
+    return slot
+
+
+class DeviceBatcher:
+    """get_batch for token streams resident in HBM: the training streams live on the GPU as int32,
+    the +-r random walk, the start indices and the window gather are HIP kernels
+    (mmt_batch_jitter / mmt_batch_indices / mmt_batch_gather): no host work, no PCIe per step."""
+
+    def __init__(self, train_sets, val_sets, vocab_sizes, rand_sizes, file_lengths, is_percents, block_size,
+                 batch_size, device, seed=0):
+        self.device = torch.device(device)
+        self.T, self.B = int(block_size), int(batch_size)
+        self.rand = list(rand_sizes)
+        self.V = [int(v) for v in vocab_sizes]
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.counter = 0
+
+        def dev32(a):
+            a = a.numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+            return torch.from_numpy(a.astype(np.int32)).to(self.device)
+
+        self.data = {"train": [dev32(t) for t in train_sets], "val": [dev32(v) for v in val_sets]}
+        self.maps = {}
+        bxy = self.T + 1
+        off = 1 if is_percents else 0
+        for split in ("train", "val"):
+            n = int(self.data[split][0].numel())
+            if len(file_lengths) == 1:
+                lens = np.array([n], dtype=np.int64)
+                valid = np.array([max(0, n - bxy - off + 1)], dtype=np.int64)
+            else:
+                lens = np.asarray(_split_file_lengths(n, split, file_lengths), dtype=np.int64)
+                valid = np.maximum(0, lens - bxy - off + 1)
+            if valid.sum() <= 0:
+                raise ValueError("No valid starting positions available for the given block size and file lengths.")
+            starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+            self.maps[split] = (torch.from_numpy(np.cumsum(valid)).to(self.device),
+                                torch.from_numpy(starts).to(self.device), len(lens), off)
+
+    def next(self, split, is_training):
+        L = ML.lib()
+        s = ML.stream_ptr(self.device)
+        self.counter += 1
+        if is_training == 1:
+            for r, t in enumerate(self.data["train"]):
+                if self.rand[r] is not None:
+                    ML.check(L.mmt_batch_jitter(s, ML.ptr(t), t.numel(), int(self.rand[r]), self.V[r], self.seed,
+                                                self.counter * 64 + r), None, "mmt_batch_jitter")
+        cum, starts, nf, off = self.maps[split]
+        ix = torch.empty(self.B, dtype=torch.long, device=self.device)
+        ML.check(L.mmt_batch_indices(s, self.B, ML.ptr(cum), ML.ptr(starts), nf, off, self.seed ^ 0x5EED,
+                                     self.counter, ML.ptr(ix)), None, "mmt_batch_indices")
+        data = self.data[split]
+        xs = [torch.empty(self.B, self.T, dtype=torch.long, device=self.device) for _ in data]
+        ys = [torch.empty(self.B, self.T, dtype=torch.long, device=self.device) for _ in data]
+        ML.check(L.mmt_batch_gather(s, len(data), ML.ptr_array(data), ML.ptr(ix), self.B, self.T, ML.ptr_array(xs),
+                                    ML.ptr_array(ys)), None, "mmt_batch_gather")
+        return xs, ys
+
+
+_device_batcher = [None]
+use_device_batcher = True
+
+
+def _get_device_batcher():
+    b = _device_batcher[0]
+    key = (id(all_train_sets), id(all_val_sets), _get_block_size(), _get_batch_size(), str(_get_device()))
+    if b is None or b[0] != key:
+        inst = DeviceBatcher(all_train_sets, all_val_sets, [len(v) for v in all_vocabularies],
+                             [p[2] for p in all_modality_params], file_lengths, is_percents, _get_block_size(),
+                             _get_batch_size(), _get_device(), seed=random.getrandbits(63))
+        b = (key, inst)
+        _device_batcher[0] = b
+    return b[1]
+
+
+def get_batch(split, is_training):
+    """Returns (xb_list, yb_list), each M tensors [batch_size, block_size] int64 on the device."""
+    T = _get_block_size()
+    B = _get_batch_size()
+    dev = _get_device()
+    if use_device_batcher and dev != "cpu" and torch.cuda.is_available():
+        return _get_device_batcher().next(split, is_training)
+    if is_training == 1:
+        for r in range(num_modalities):
+            rs = all_modality_params[r][2]  # reference quirk: has_header, not randomness_size
+            if rs is not None:
+                rng = np.random.default_rng(random.getrandbits(64))
+                jitter_(_as_array(r), rs, len(all_vocabularies[r]), rng)
+    if split == "train":
+        data = [_as_array(r) for r in range(num_modalities)]
+    else:
+        data = [v.numpy() if isinstance(v, torch.Tensor) else np.asarray(v) for v in all_val_sets]
+    ix = generate_batch_starting_indices(len(data[0]), T, B, split, file_lengths, is_percents).numpy()
+    win = ix[:, None] + np.arange(T + 1)[None, :]
+    xb_list, yb_list = [], []
+    on_gpu = dev != "cpu" and torch.cuda.is_available()
+    slot = _ring_slot() if on_gpu else 0
+    for r in range(num_modalities):
+        w = data[r][win]
+        xb = _pinned_buf(("x", r, slot), (B, T))
+        yb = _pinned_buf(("y", r, slot), (B, T))
+        xb.numpy()[...] = w[:, :T]
+        yb.numpy()[...] = w[:, 1:]
+        if on_gpu:
+            xb_list.append(xb.to(dev, non_blocking=True))
+            yb_list.append(yb.to(dev, non_blocking=True))
+        else:
+            xb_list.append(xb.clone())
+            yb_list.append(yb.clone())
+    if on_gpu:
+        ev = torch.cuda.Event()
+        ev.record()
+        _ring_events[slot] = ev
+    return xb_list, yb_list
+
+
+# ------------------------------------------------------------------------------------------
+# directional metric (reference training_utils.py:184-330)
+# ------------------------------------------------------------------------------------------
+_vocab_dev = {}
+
+
+def _get_direction_sign(current_value, previous_value, is_percentage_data):
+    if is_percentage_data:
+        return 1 if current_value > 0 else (-1 if current_value < 0 else 0)
+    if not isinstance(previous_value, numbers.Number):
+        return None
+    change = current_value - previous_value
+    return 1 if change > 0 else (-1 if change < 0 else 0)
+
+
+def _numeric_vocab(vocab, device):
+    key = (id(vocab), len(vocab), str(device))
+    hit = _vocab_dev.get(key)
+    if hit is not None:
+        return hit
+    numeric = all(isinstance(v, numbers.Number) for v in vocab)
+    t = torch.tensor([float(v) for v in vocab], dtype=torch.float64, device=device) if numeric else None
+    _vocab_dev[key] = (numeric, t)
+    return numeric, t
+
+
+def calculate_evaluation_metrics(logits_list, xb_list, yb_list, num_modalities, all_vocabularies, all_modality_params,
+                                 all_file_info):
+    """Per modality: (wins, losses, certainty_sum, batches_processed) of the last-token direction."""
+    wins = [0] * num_modalities
+    losses = [0] * num_modalities
+    cert = [0.0] * num_modalities
+    proc = [0] * num_modalities
+    pending = []
+    for i in range(num_modalities):
+        if not (len(logits_list) > i and len(yb_list) > i):
+            continue
+        vocab = all_vocabularies[i]
+        is_pct = bool(all_modality_params[i][3])
+        lg = logits_list[i]
+        numeric, vt = _numeric_vocab(vocab, lg.device)
+        min_len = 1 if is_pct else 2
+        if not (numeric and yb_list[i].ndim >= 2 and yb_list[i].shape[1] >= min_len):
+            continue
+        B, T, V = lg.shape
+        if B == 0:
+            continue
+        if lg.device.type != "cuda":
+            raise RuntimeError("calculate_evaluation_metrics runs on the GPU (mmt_eval_direction); no CPU path")
+        proc[i] = 1
+        acc_i = torch.zeros(2, dtype=torch.int32, device=lg.device)
+        acc_c = torch.zeros(1, dtype=torch.float64, device=lg.device)
+        xb = xb_list[i].contiguous()
+        yb = yb_list[i].contiguous()
+        lgc = lg.contiguous()
+        rc = ML.lib().mmt_eval_direction(None, ML.stream_ptr(lg.device), B, T, V, ML.ptr(lgc), ML.ptr(xb),
+                                         ML.ptr(yb), ML.ptr(vt), 1 if is_pct else 0, ML.ptr(acc_i), ML.ptr(acc_c))
+        ML.check(rc, None, "mmt_eval_direction")
+        pending.append((i, acc_i, acc_c, (lgc, xb, yb)))
+    for i, acc_i, acc_c, _keep in pending:
+        w, l = acc_i.tolist()
+        wins[i], losses[i] = w, l
+        cert[i] = float(acc_c.item())
+    return wins, losses, cert, proc
+
+
+# ------------------------------------------------------------------------------------------
+# estimate_loss (reference training_utils.py:387-520)
+# ------------------------------------------------------------------------------------------
+def estimate_loss(current_step=None, max_steps=None):
+    out = {}
+    m.eval()
+    for state in ["train", "val"]:
+        now = datetime.now()
+        current_time = now.strftime("%H:%M:%S")
+        step_info = f"Step {current_step}/{max_steps} | " if current_step is not None else ""
+        batch_calc = f" * {_get_batch_size()} batches = {_get_eval_iters() * _get_batch_size()} samples"
+        print(f"Evaluation: {step_info}{state.title()} set ({_get_eval_iters()} iterations{batch_calc}) | {current_time}")
+        tot_proc = [0] * num_modalities
+        tot_ok = [0] * num_modalities
+        tot_bad = [0] * num_modalities
+        tot_cert = [0.0] * num_modalities
+        loss_sum = None
+        n_losses = 0
+        with torch.no_grad():
+            for k in range(_get_eval_iters()):
+                xb_list, yb_list = get_batch(state, 0)
+                logits_list, losses_list = m(xb_list, yb_list)
+                if losses_list and all(l is not None for l in losses_list):
+                    s = sum(losses_list)
+                    loss_sum = s if loss_sum is None else loss_sum + s  # stays on device: one sync below
+                    n_losses += 1
+                else:
+                    print(f"Warning: Iteration {k} losses not calculated, skipping")
+                w, l, c, p = calculate_evaluation_metrics(logits_list, xb_list, yb_list, num_modalities,
+                                                          all_vocabularies, all_modality_params, all_file_info)
+                for i in range(num_modalities):
+                    tot_ok[i] += w[i]
+                    tot_bad[i] += l[i]
+                    tot_cert[i] += c[i]
+                    tot_proc[i] += p[i]
+        out[state] = (loss_sum.item() / n_losses) if n_losses else float("nan")
+        disp = "Train Set" if state == "train" else "Val Set"
+        print(f"\nDIRECTIONAL METRICS - {disp} (Correct/Total)")
+        for i in range(num_modalities):
+            name = all_modality_params[i][9] if all_modality_params[i][9] else f"Modality {i+1}"
+            if tot_proc[i] > 0:
+                total = tot_ok[i] + tot_bad[i]
+                if total > 0:
+                    rate = round((tot_ok[i] / total) * 100, 1)
+                    print(f"  - {name:<30}{tot_ok[i]}/{total} ({rate}%)")
+                else:
+                    print(f"  - {name}: No directional predictions")
+            else:
+                print(f"  - {name}: No data processed (non-numeric)")
+        cfg = _get_config()
+        output_file_name = cfg.get("output_file_name", "")
+        project_file_path = cfg.get("project_file_path", "")
+        if output_file_name != "":
+            path = project_file_path + "output/" + output_file_name
+            os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+            with open(path, "a", encoding="utf-8") as f:
+                for i in range(num_modalities):
+                    name = all_modality_params[i][9] if all_modality_params[i][9] else f"Modality {i+1}"
+                    if tot_proc[i] > 0:
+                        total = tot_ok[i] + tot_bad[i]
+                        if total > 0:
+                            rate = round((tot_ok[i] / total) * 100, 1)
+                            f.write(f"   DIRECTIONAL PREDICTION {disp} - {name}: Correct={tot_ok[i]:,} | "
+                                    f"Incorrect={tot_bad[i]:,} | Accuracy={rate}%\n")
+                        else:
+                            f.write(f"   DIRECTIONAL PREDICTION {disp} - {name}: Correct={tot_ok[i]:,} | "
+                                    f"Incorrect={tot_bad[i]:,} | Accuracy=N/A\n")
+                    else:
+                        f.write(f"   DIRECTIONAL PREDICTION {disp} - {name}: Correct=0 | Incorrect=0 | Accuracy=N/A\n")
+                if state == "train":
+                    f.write("\n")
+        if state == "train":
+            print()
+    m.train()
+    return out
+
+
+# module globals injected by main.py (reference training_utils.py:523-534)
+all_full_datasets = None
+all_train_sets = None
+all_val_sets = None
+all_vocabularies = None
+all_modality_params = None
+all_file_info = None
+file_lengths = None
+num_modalities = None
+is_percents = False
+m = None
