@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--probe", default="ffn0", help="engine launch label timed live for the roofline line")
+    ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM pipeline variant (mmt_gemm_set_variant)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -120,6 +121,8 @@ def main():
     import training_utils as TU
     from model import MultimodalTransformer
 
+    if args.gemm_variant >= 0:
+        ML.lib().mmt_gemm_set_variant(args.gemm_variant)
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["B"] = args.batch

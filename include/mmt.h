@@ -122,6 +122,9 @@ int mmt_batch_gather(void* stream, int32_t nmod, const int32_t* const* data, con
                      int32_t T, int64_t* const* x, int64_t* const* y);
 
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
+/* GEMM pipeline variant (tuning knob, process-wide): 0 = K-step 64 x 2 LDS stages (default),
+ * 1 = 32 x 2, 2 = 32 x 3, 3 = 32 x 4, 4 = 64 x 3 */
+int mmt_gemm_set_variant(int variant);
 int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t splits, int32_t M, int32_t N,
                 int32_t K, const void* A, int32_t lda, const void* B, int32_t ldb, const float* bias,
                 const void* aux, int32_t ldaux, const float* resid, int32_t ldres, float* o32, int32_t ldc,

@@ -1,0 +1,92 @@
+"""GEMM microbenchmark over the C1 shapes of the training step, per pipeline variant.
+
+    python tools/gemm_bench.py [--variants 0,1,2,3,4] [--reps 20]
+
+Times mmt_op_gemm (the engine's kernel) with HIP events on the current stream; prints TFLOP/s.
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "trade-aid-multimodal-transformer_amd"))
+
+import torch  # noqa: E402
+
+import mmt_lib as ML  # noqa: E402
+
+R = 65536  # 4 modalities x B 64 x T 256
+SHAPES = [
+    # name, a_kc, b_kc, epi, M, N, K, splits
+    ("ffn0_fwd", 1, 1, "bias_relu_bf16", R, 1024, 256, 1),
+    ("ffn2_fwd", 1, 1, "bias_resid_f32", R, 256, 1024, 1),
+    ("qkv1_fwd", 1, 1, "bias_tanh_bf16", R, 384, 256, 1),
+    ("proj2_fwd", 1, 1, "bias_resid_f32", R, 256, 128, 1),
+    ("ffn2_dx", 1, 0, "drelu_bf16", R, 1024, 256, 1),
+    ("ffn2_dx_noaux", 1, 0, "store_bf16", R, 1024, 256, 1),
+    ("ffn0_dx", 1, 0, "store_f32", R, 256, 1024, 1),
+    ("ffn_dw_s32", 0, 0, "atomic_f32", 1024, 256, R, 32),
+    ("ffn_dw_s16", 0, 0, "atomic_f32", 1024, 256, R, 16),
+    ("qkv1_dw_s32", 0, 0, "atomic_f32", 384, 256, R, 32),
+]
+
+
+def r8(x):
+    return (x + 7) // 8 * 8
+
+
+def run(variant, reps):
+    L = ML.lib()
+    assert L.mmt_gemm_set_variant(variant | (variant << 4)) == 0
+    out = {}
+    for name, akc, bkc, epi, M, N, K, splits in SHAPES:
+        if akc:
+            A = torch.randn(M, r8(K), device="cuda").to(torch.bfloat16)
+            lda = r8(K)
+        else:
+            A = torch.randn(K, r8(M), device="cuda").to(torch.bfloat16)
+            lda = r8(M)
+        if bkc:
+            B = torch.randn(N, r8(K), device="cuda").to(torch.bfloat16)
+            ldb = r8(K)
+        else:
+            B = torch.randn(K, r8(N), device="cuda").to(torch.bfloat16)
+            ldb = r8(N)
+        bias = torch.randn(N, device="cuda")
+        aux = torch.randn(M, r8(N), device="cuda").to(torch.bfloat16)
+        resid = torch.randn(M, N, device="cuda")
+        o32 = torch.zeros(M, N, device="cuda")
+        o16 = torch.zeros(M, r8(N), dtype=torch.bfloat16, device="cuda")
+        s = ML.stream_ptr()
+
+        def call():
+            rc = L.mmt_op_gemm(s, akc, bkc, ML.EPI[epi], splits, M, N, K, ML.ptr(A), lda, ML.ptr(B), ldb, ML.ptr(bias),
+                               ML.ptr(aux), r8(N), ML.ptr(resid), N, ML.ptr(o32), N, ML.ptr(o16), r8(N), 1.0)
+            assert rc == 0
+
+        for _ in range(3):
+            call()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / reps * 1e3
+        tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+        out[name] = (us, tf)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1,2,3,4")
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    for v in [int(x) for x in args.variants.split(",")]:
+        res = run(v, args.reps)
+        print(f"variant {v}: " + "  ".join(f"{k} {us:7.1f}us {tf:6.1f}TF" for k, (us, tf) in res.items()), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -4,23 +4,26 @@
 // softmax, @ v. Cross-attention runs one independent causal softmax per KV modality ("stream")
 // and SUMS the per-stream outputs (no joint softmax).
 //
-// Structure: one wave (64-thread workgroup) owns one 32-row tile of one (batch, head). All
-// products are v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
-//   forward  S^T = K Q^T (keys on accumulator rows, queries on lanes) -> online softmax per lane
-//            O^T += V^T P^T with P^T taken straight from the accumulator registers as the
-//            B operand (no LDS round trip) and V^T read by ds_read_b64_tr_b16 from a V tile.
-//   dQ       S^T, dP^T recomputed per key tile; dQ^T += K^T dS^T (K^T via transposed LDS reads)
-//   dK, dV   S = Q K^T, dP = dO V^T (queries on rows); dV += P^T dO, dK += dS^T Q with P / dS
-//            as the A operand straight from registers, dO / Q by transposed LDS reads.
-// Head sizes 8..64 (padded to 16 on the reduction side and 32 on the output side).
+// Structure: a 256-thread workgroup (4 waves) owns a 128-row block of one (batch, head); each
+// wave owns one 32-row tile. The operand tiles the waves share (K/V in the forward and dQ pass,
+// Q/dO/LSE/D in the dK/dV pass) are staged once per workgroup into double-buffered LDS, the next
+// tile's global loads in flight while the current tile computes; one barrier per tile.
+// All products are v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
+//   forward  S^T = K Q^T (keys on accumulator rows, queries on lanes) -> online softmax per lane;
+//            O^T += V^T P^T with P^T straight from the accumulator registers as the B operand and
+//            V^T by ds_read_b64_tr_b16 from the V tile.
+//   dQ       S^T, dP^T recomputed per key tile; dQ^T += K^T dS^T (K^T by transposed LDS reads).
+//   dK, dV   S = Q K^T, dP = dO V^T (queries on rows); dV += P^T dO, dK += dS^T Q with P and dS
+//            taken from registers as the A operand and dO / Q by transposed LDS reads.
+// Head sizes 8..64: padded to 16 on the reduction side and to 32 on the output side.
 #include "mmt_common.h"
 #include "mmt_kernels.h"
 
+namespace {
+
 __device__ __forceinline__ bf16x8 zero8() {
-  bf16x8 z;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) z[i] = (__bf16)0.0f;
-  return z;
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  return __builtin_bit_cast(bf16x8, z);
 }
 
 __device__ __forceinline__ bf16x8 ld8(const bf16_t* p, bool ok) {
@@ -28,32 +31,32 @@ __device__ __forceinline__ bf16x8 ld8(const bf16_t* p, bool ok) {
   return *reinterpret_cast<const bf16x8*>(p);
 }
 
-// stage a [32 rows][W] tile (rows r0.., columns 0..HS-1 of the head, zero padded) into LDS
-template <int HS, int W>
-__device__ __forceinline__ void stage_tile(bf16_t* lds, const bf16_t* base, int64_t rowbase, int r0, int T, int ld,
-                                          int lane) {
-  constexpr int CPR = W / 8;  // 16-byte chunks per row
-#pragma unroll
-  for (int c = lane; c < 32 * CPR; c += 64) {
-    const int row = c / CPR, col = (c % CPR) * 8;
-    const bool ok = (r0 + row < T) && (col < HS);
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (ok) v = *reinterpret_cast<const u32x4*>(base + (rowbase + r0 + row) * ld + col);
-    *reinterpret_cast<u32x4*>(lds + row * W + col) = v;
-  }
+template <int HS>
+struct Geo {
+  static constexpr int NKS = (HS + 15) / 16;           // k-steps over the head dim
+  static constexpr int ND = (HS + 31) / 32;            // 32-wide output tiles over the head dim
+  static constexpr int W = ND * 32;                    // padded head width in LDS tiles
+  static constexpr int RW = W + 8;                     // row-read tile stride (16-B pad: no b128 conflicts)
+  static constexpr int TW = (W == 64) ? 96 : W;        // transposed-read tile stride (conflict-free)
+  static constexpr int CH = HS / 8;                    // 16-byte chunks per row
+};
+
+// one 16-B chunk (8 bf16) of a 32-row tile: row r0+row, columns col..col+7 of the head (zero padded)
+__device__ __forceinline__ u32x4 tile_chunk(const bf16_t* base, int64_t rowbase, int r0, int row, int col, int T,
+                                            int ld) {
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (r0 + row < T) v = *reinterpret_cast<const u32x4*>(base + (rowbase + r0 + row) * ld + col);
+  return v;
 }
 
-// A-operand fragment of X^T where X is a [32 rows][W] LDS tile: lane gets column
+// A-operand fragment of X^T where X is a [32 rows][stride] LDS tile: lane gets column
 // d = dt*32 + (lane&31) and rows {16s+4h+0..3, 16s+8+4h+0..3} (the accumulator-as-operand k order)
-template <int W>
-__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* lds, int dt, int s, int lane) {
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* lds, int stride, int dt, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int q = i >> 2, p = i & 3;
   const int col = dt * 32 + 16 * (g & 1) + 4 * p;
   const int kb = 16 * s + 4 * (g >> 1) + q;
-  const s16x4 lo = lds_tr16(lds + kb * W + col);
-  const s16x4 hi = lds_tr16(lds + (kb + 8) * W + col);
-  return join4(lo, hi);
+  return join4(lds_tr16(lds + kb * stride + col), lds_tr16(lds + (kb + 8) * stride + col));
 }
 
 // accumulator registers 8s..8s+7 -> bf16 operand fragment
@@ -64,97 +67,134 @@ __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
   return r;
 }
 
+__device__ __forceinline__ void zero16(f32x16& a) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e) a[e] = 0.f;
+}
+
+}  // namespace
+
 // =============================================================================================
-// forward
+// forward: grid (ceil(T/128), B*H, G); wave w owns query tile 4*blockIdx.x + w
 // =============================================================================================
 template <int HS>
-__global__ __launch_bounds__(64) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
-  constexpr int NKS = (HS + 15) / 16;
-  constexpr int ND = (HS + 31) / 32;
-  constexpr int W = ND * 32;
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
+  using G = Geo<HS>;
   const AttnProblem& P = batch.p[blockIdx.z];
-  const int qt = blockIdx.x;
-  const int bh = blockIdx.y;
-  const int b = bh / H, head = bh % H;
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-  const int q0 = qt * 32;
+  const int bh = blockIdx.y, b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int nt = (T + 31) / 32;
+  const int qt = blockIdx.x * 4 + w;
+  const int last_kt = min(blockIdx.x * 4 + 3, nt - 1);
+  const int q0 = qt * 32, tq = q0 + r;
   const int64_t rowbase = (int64_t)b * T;
-  const int tq = q0 + r;
-  __shared__ __attribute__((aligned(16))) bf16_t vt[32 * W];
+  __shared__ __attribute__((aligned(16))) bf16_t ks[2][32 * G::RW];
+  __shared__ __attribute__((aligned(16))) bf16_t vs[2][32 * G::TW];
 
-  bf16x8 qf[NKS];
+  bf16x8 qf[G::NKS];
 #pragma unroll
-  for (int s = 0; s < NKS; ++s) {
+  for (int s = 0; s < G::NKS; ++s) {
     const int d0 = 16 * s + 8 * h;
     qf[s] = ld8(P.q + (rowbase + tq) * P.q_ld + head * HS + d0, tq < T && d0 < HS);
   }
-  f32x16 otot[ND];
+  // zero the pad columns of both buffers once (never written by staging)
+  for (int q = tid; q < 2 * 32 * G::RW; q += 256) { const int c = q % G::RW; if (c >= HS) (&ks[0][0])[q] = 0; }
+  for (int q = tid; q < 2 * 32 * G::TW; q += 256) { const int c = q % G::TW; if (c >= HS) (&vs[0][0])[q] = 0; }
+
+  f32x16 otot[G::ND];
 #pragma unroll
-  for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) otot[dt][e] = 0.f;
+  for (int dt = 0; dt < G::ND; ++dt) zero16(otot[dt]);
 
   for (int j = 0; j < P.nstreams; ++j) {
     const bf16_t* kp = P.k[j] + head * P.kv_hstride;
     const bf16_t* vp = P.v[j] + head * P.kv_hstride;
     float m = -INFINITY, l = 0.f;
-    f32x16 oacc[ND];
+    f32x16 oacc[G::ND];
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+    for (int dt = 0; dt < G::ND; ++dt) zero16(oacc[dt]);
+    // staging: chunk c < 32*CH -> K, else V
+    u32x4 stg[2];
+    auto issue = [&](int kt) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) oacc[dt][e] = 0.f;
-
-    for (int kt = 0; kt <= qt; ++kt) {
-      const int k0 = kt * 32;
-      f32x16 sacc;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) sacc[e] = 0.f;
-#pragma unroll
-      for (int s = 0; s < NKS; ++s) {
-        const int d0 = 16 * s + 8 * h;
-        const bf16x8 kf = ld8(kp + (rowbase + k0 + r) * P.kv_ld + d0, k0 + r < T && d0 < HS);
-        sacc = mfma32(kf, qf[s], sacc);
+      for (int u = 0; u < 2; ++u) {
+        const int c = tid + 256 * u;
+        if (c < 64 * G::CH) {
+          const bool isv = c >= 32 * G::CH;
+          const int cc = isv ? c - 32 * G::CH : c;
+          stg[u] = tile_chunk(isv ? vp : kp, rowbase, kt * 32, cc / G::CH, (cc % G::CH) * 8, T, P.kv_ld);
+        }
       }
+    };
+    auto commit = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = tid + 256 * u;
+        if (c < 64 * G::CH) {
+          const bool isv = c >= 32 * G::CH;
+          const int cc = isv ? c - 32 * G::CH : c;
+          const int row = cc / G::CH, col = (cc % G::CH) * 8;
+          if (isv) *reinterpret_cast<u32x4*>(&vs[buf][row * G::TW + col]) = stg[u];
+          else *reinterpret_cast<u32x4*>(&ks[buf][row * G::RW + col]) = stg[u];
+        }
+      }
+    };
+    __syncthreads();  // previous stream's readers are done with both buffers
+    issue(0);
+    commit(0);
+    __syncthreads();
+    for (int kt = 0; kt <= last_kt; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 <= last_kt;
+      if (more) issue(kt + 1);
+      if (kt <= qt) {
+        const int k0 = kt * 32;
+        f32x16 sacc;
+        zero16(sacc);
+#pragma unroll
+        for (int s = 0; s < G::NKS; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&ks[cur][r * G::RW + 16 * s + 8 * h]);
+          sacc = mfma32(kf, qf[s], sacc);
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const float sv = (key <= tq && key < T) ? sacc[e] * scale : -INFINITY;
+          sacc[e] = sv;
+          tmax = fmaxf(tmax, sv);
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float mnew = fmaxf(m, tmax);
+        const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
+        const float alpha = __expf(m - msafe);
+        float rs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float pv = __expf(sacc[e] - msafe);
+          sacc[e] = pv;
+          rs += pv;
+        }
+        rs += __shfl_xor(rs, 32, 64);
+        l = l * alpha + rs;
+        m = mnew;
+#pragma unroll
+        for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pf = acc_frag(sacc, s);
+#pragma unroll
+          for (int dt = 0; dt < G::ND; ++dt) oacc[dt] = mfma32(tr_frag(vs[cur], G::TW, dt, s, lane), pf, oacc[dt]);
+        }
+      }
+      if (more) commit(cur ^ 1);
       __syncthreads();
-      stage_tile<HS, W>(vt, vp, rowbase, k0, T, P.kv_ld, lane);
-      // online softmax over keys (rows of S^T) for query tq (lane column)
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const float sv = (key <= tq && key < T) ? sacc[e] * scale : -INFINITY;
-        sacc[e] = sv;
-        tmax = fmaxf(tmax, sv);
-      }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(m, tmax);
-      const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = __expf(m - msafe);
-      float rs = 0.f;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float pv = __expf(sacc[e] - msafe);
-        sacc[e] = pv;
-        rs += pv;
-      }
-      rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
-      m = mnew;
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc_frag(sacc, s);
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) oacc[dt] = mfma32(tr_frag<W>(vt, dt, s, lane), pf, oacc[dt]);
-      }
     }
     const float inv = (l > 0.f) ? 1.f / l : 0.f;
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+    for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         oacc[dt][e] *= inv;
@@ -164,7 +204,7 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnBatch batch, int T, in
       if (h == 0) P.lse[j][(int64_t)bh * T + tq] = m + __logf(l);
       if (P.nstreams > 1 && P.oj[j]) {
 #pragma unroll
-        for (int dt = 0; dt < ND; ++dt)
+        for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int d0 = dt * 32 + 8 * g + 4 * h;
@@ -177,7 +217,7 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnBatch batch, int T, in
   }
   if (tq < T) {
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+    for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d0 = dt * 32 + 8 * g + 4 * h;
@@ -189,44 +229,45 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnBatch batch, int T, in
 }
 
 // =============================================================================================
-// backward: dQ (also writes D_j = rowsum(dO * O_j) for the dK/dV kernel)
+// backward dQ (also writes D_j = rowsum(dO * O_j) for the dK/dV pass); grid as forward
 // =============================================================================================
 template <int HS>
-__global__ __launch_bounds__(64) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H, float scale) {
-  constexpr int NKS = (HS + 15) / 16;
-  constexpr int ND = (HS + 31) / 32;
-  constexpr int W = ND * 32;
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H, float scale) {
+  using G = Geo<HS>;
   const AttnProblem& P = batch.p[blockIdx.z];
-  const int qt = blockIdx.x;
-  const int bh = blockIdx.y;
-  const int b = bh / H, head = bh % H;
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-  const int q0 = qt * 32;
-  const int64_t rowbase = (int64_t)b * T;
-  const int tq = q0 + r;
+  const int bh = blockIdx.y, b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int nt = (T + 31) / 32;
+  const int qt = blockIdx.x * 4 + w;
+  const int last_kt = min(blockIdx.x * 4 + 3, nt - 1);
+  const int q0 = qt * 32, tq = q0 + r;
   const bool qok = tq < T;
-  __shared__ __attribute__((aligned(16))) bf16_t kt_lds[32 * W];
+  const int64_t rowbase = (int64_t)b * T;
+  __shared__ __attribute__((aligned(16))) bf16_t ks[2][32 * G::RW];  // K tile: row reads + tr reads
+  __shared__ __attribute__((aligned(16))) bf16_t vs[2][32 * G::RW];  // V tile: row reads
 
-  bf16x8 qf[NKS], dof[NKS];
+  bf16x8 qf[G::NKS], dof[G::NKS];
 #pragma unroll
-  for (int s = 0; s < NKS; ++s) {
+  for (int s = 0; s < G::NKS; ++s) {
     const int d0 = 16 * s + 8 * h;
     const bool ok = qok && d0 < HS;
     qf[s] = ld8(P.q + (rowbase + tq) * P.q_ld + head * HS + d0, ok);
     dof[s] = ld8(P.dout + (rowbase + tq) * P.dout_ld + head * HS + d0, ok);
   }
-  f32x16 dq[ND];
+  for (int q = tid; q < 2 * 32 * G::RW; q += 256) {
+    const int c = q % G::RW;
+    if (c >= HS) { (&ks[0][0])[q] = 0; (&vs[0][0])[q] = 0; }
+  }
+  f32x16 dq[G::ND];
 #pragma unroll
-  for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) dq[dt][e] = 0.f;
+  for (int dt = 0; dt < G::ND; ++dt) zero16(dq[dt]);
 
   for (int j = 0; j < P.nstreams; ++j) {
-    // D_j for this lane's query
     const bf16_t* oj = (P.nstreams > 1) ? P.oj[j] : P.o;
     float dsum = 0.f;
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) {
+    for (int s = 0; s < G::NKS; ++s) {
       const int d0 = 16 * s + 8 * h;
       const bf16x8 ov = ld8(oj + (rowbase + tq) * P.o_ld + head * HS + d0, qok && d0 < HS);
 #pragma unroll
@@ -237,41 +278,71 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_kernel(AttnBatch batch, int T,
     const float lse = qok ? P.lse[j][(int64_t)bh * T + tq] : 0.f;
     const bf16_t* kp = P.k[j] + head * P.kv_hstride;
     const bf16_t* vp = P.v[j] + head * P.kv_hstride;
-    for (int kt = 0; kt <= qt; ++kt) {
-      const int k0 = kt * 32;
-      f32x16 sacc, dpacc;
+    u32x4 stg[2];
+    auto issue = [&](int kt) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) { sacc[e] = 0.f; dpacc[e] = 0.f; }
-#pragma unroll
-      for (int s = 0; s < NKS; ++s) {
-        const int d0 = 16 * s + 8 * h;
-        const bool ok = k0 + r < T && d0 < HS;
-        const bf16x8 kf = ld8(kp + (rowbase + k0 + r) * P.kv_ld + d0, ok);
-        const bf16x8 vf = ld8(vp + (rowbase + k0 + r) * P.kv_ld + d0, ok);
-        sacc = mfma32(kf, qf[s], sacc);
-        dpacc = mfma32(vf, dof[s], dpacc);
+      for (int u = 0; u < 2; ++u) {
+        const int c = tid + 256 * u;
+        if (c < 64 * G::CH) {
+          const bool isv = c >= 32 * G::CH;
+          const int cc = isv ? c - 32 * G::CH : c;
+          stg[u] = tile_chunk(isv ? vp : kp, rowbase, kt * 32, cc / G::CH, (cc % G::CH) * 8, T, P.kv_ld);
+        }
       }
+    };
+    auto commit = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = tid + 256 * u;
+        if (c < 64 * G::CH) {
+          const bool isv = c >= 32 * G::CH;
+          const int cc = isv ? c - 32 * G::CH : c;
+          const int row = cc / G::CH, col = (cc % G::CH) * 8;
+          *reinterpret_cast<u32x4*>(isv ? &vs[buf][row * G::RW + col] : &ks[buf][row * G::RW + col]) = stg[u];
+        }
+      }
+    };
+    __syncthreads();
+    issue(0);
+    commit(0);
+    __syncthreads();
+    for (int kt = 0; kt <= last_kt; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 <= last_kt;
+      if (more) issue(kt + 1);
+      if (kt <= qt) {
+        const int k0 = kt * 32;
+        f32x16 sacc, dpacc;
+        zero16(sacc);
+        zero16(dpacc);
+#pragma unroll
+        for (int s = 0; s < G::NKS; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&ks[cur][r * G::RW + 16 * s + 8 * h]);
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(&vs[cur][r * G::RW + 16 * s + 8 * h]);
+          sacc = mfma32(kf, qf[s], sacc);
+          dpacc = mfma32(vf, dof[s], dpacc);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const bool ok = qok && key <= tq && key < T;
+          const float pv = ok ? __expf(sacc[e] * scale - lse) : 0.f;
+          sacc[e] = pv * (dpacc[e] - dsum);  // dS^T
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 df = acc_frag(sacc, s);
+#pragma unroll
+          for (int dt = 0; dt < G::ND; ++dt) dq[dt] = mfma32(tr_frag(ks[cur], G::RW, dt, s, lane), df, dq[dt]);
+        }
+      }
+      if (more) commit(cur ^ 1);
       __syncthreads();
-      stage_tile<HS, W>(kt_lds, kp, rowbase, k0, T, P.kv_ld, lane);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const bool ok = qok && key <= tq && key < T;
-        const float pv = ok ? __expf(sacc[e] * scale - lse) : 0.f;
-        sacc[e] = pv * (dpacc[e] - dsum);  // dS^T
-      }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 df = acc_frag(sacc, s);
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) dq[dt] = mfma32(tr_frag<W>(kt_lds, dt, s, lane), df, dq[dt]);
-      }
     }
   }
   if (qok) {
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+    for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d0 = dt * 32 + 8 * g + 4 * h;
@@ -284,92 +355,135 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_kernel(AttnBatch batch, int T,
 }
 
 // =============================================================================================
-// backward: dK, dV for one key tile of one (stream, batch, head)
+// backward dK, dV: grid (ceil(T/128), B*H*nstreams, G); wave w owns key tile 4*blockIdx.x + w
 // =============================================================================================
 template <int HS>
-__global__ __launch_bounds__(64) void attn_bwd_dkdv_kernel(AttnBatch batch, int T, int H, float scale) {
-  constexpr int NKS = (HS + 15) / 16;
-  constexpr int ND = (HS + 31) / 32;
-  constexpr int W = ND * 32;
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBatch batch, int T, int H, float scale) {
+  using G = Geo<HS>;
   const AttnProblem& P = batch.p[blockIdx.z];
-  const int kt = blockIdx.x;
   const int nbh = gridDim.y / P.nstreams;
   if ((int)blockIdx.y >= nbh * P.nstreams) return;
   const int j = blockIdx.y / nbh;
   const int bh = blockIdx.y % nbh;
   const int b = bh / H, head = bh % H;
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-  const int k0 = kt * 32;
-  const int64_t rowbase = (int64_t)b * T;
-  const int tk = k0 + r;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int nt = (T + 31) / 32;
+  const int kt = blockIdx.x * 4 + w;
+  const int first_qt = blockIdx.x * 4;
+  const int k0 = kt * 32, tk = k0 + r;
   const bool kok = tk < T;
-  const int nqt = (T + 31) / 32;
-  __shared__ __attribute__((aligned(16))) bf16_t q_lds[32 * W];
-  __shared__ __attribute__((aligned(16))) bf16_t do_lds[32 * W];
+  const int64_t rowbase = (int64_t)b * T;
+  __shared__ __attribute__((aligned(16))) bf16_t qs[2][32 * G::RW];   // Q tile: row + tr reads
+  __shared__ __attribute__((aligned(16))) bf16_t dos[2][32 * G::RW];  // dO tile: row + tr reads
+  __shared__ __attribute__((aligned(16))) float lsd[2][2][32];        // LSE, D of the tile's rows
 
   const bf16_t* kp = P.k[j] + head * P.kv_hstride;
   const bf16_t* vp = P.v[j] + head * P.kv_hstride;
-  bf16x8 kf[NKS], vf[NKS];
+  bf16x8 kf[G::NKS], vf[G::NKS];
 #pragma unroll
-  for (int s = 0; s < NKS; ++s) {
+  for (int s = 0; s < G::NKS; ++s) {
     const int d0 = 16 * s + 8 * h;
     const bool ok = kok && d0 < HS;
     kf[s] = ld8(kp + (rowbase + tk) * P.kv_ld + d0, ok);
     vf[s] = ld8(vp + (rowbase + tk) * P.kv_ld + d0, ok);
   }
-  f32x16 dk[ND], dv[ND];
+  for (int q = tid; q < 2 * 32 * G::RW; q += 256) {
+    const int c = q % G::RW;
+    if (c >= HS) { (&qs[0][0])[q] = 0; (&dos[0][0])[q] = 0; }
+  }
+  f32x16 dk[G::ND], dv[G::ND];
 #pragma unroll
-  for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) { dk[dt][e] = 0.f; dv[dt][e] = 0.f; }
+  for (int dt = 0; dt < G::ND; ++dt) { zero16(dk[dt]); zero16(dv[dt]); }
 
   const float* lsep = P.lse[j] + (int64_t)bh * T;
   const float* dvp = P.dvec[j] + (int64_t)bh * T;
-  for (int qt = kt; qt < nqt; ++qt) {
-    const int q0 = qt * 32;
-    f32x16 sacc, dpacc;
+  const bf16_t* qp = P.q + head * HS;
+  const bf16_t* dop = P.dout + head * HS;
+  u32x4 stg[2];
+  float sl = 0.f;
+  auto issue = [&](int qt) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) { sacc[e] = 0.f; dpacc[e] = 0.f; }
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      const int d0 = 16 * s + 8 * h;
-      const bool ok = q0 + r < T && d0 < HS;
-      const bf16x8 qa = ld8(P.q + (rowbase + q0 + r) * P.q_ld + head * HS + d0, ok);
-      const bf16x8 da = ld8(P.dout + (rowbase + q0 + r) * P.dout_ld + head * HS + d0, ok);
-      sacc = mfma32(qa, kf[s], sacc);    // S[q][key]
-      dpacc = mfma32(da, vf[s], dpacc);  // dP[q][key]
-    }
-    __syncthreads();
-    stage_tile<HS, W>(q_lds, P.q + head * HS, rowbase, q0, T, P.q_ld, lane);
-    stage_tile<HS, W>(do_lds, P.dout + head * HS, rowbase, q0, T, P.dout_ld, lane);
-    f32x16 pm;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int tq = q0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      const bool ok = kok && tq < T && tk <= tq;
-      const float lse = tq < T ? lsep[tq] : 0.f;
-      const float dd = tq < T ? dvp[tq] : 0.f;
-      const float pv = ok ? __expf(sacc[e] * scale - lse) : 0.f;
-      pm[e] = pv;
-      sacc[e] = pv * (dpacc[e] - dd);  // dS[q][key]
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 pf = acc_frag(pm, s);
-      const bf16x8 df = acc_frag(sacc, s);
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt) {
-        dv[dt] = mfma32(pf, tr_frag<W>(do_lds, dt, s, lane), dv[dt]);
-        dk[dt] = mfma32(df, tr_frag<W>(q_lds, dt, s, lane), dk[dt]);
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u;
+      if (c < 64 * G::CH) {
+        const bool isd = c >= 32 * G::CH;
+        const int cc = isd ? c - 32 * G::CH : c;
+        stg[u] = isd ? tile_chunk(dop, rowbase, qt * 32, cc / G::CH, (cc % G::CH) * 8, T, P.dout_ld)
+                     : tile_chunk(qp, rowbase, qt * 32, cc / G::CH, (cc % G::CH) * 8, T, P.q_ld);
       }
     }
+    if (tid < 64) {
+      const int t = qt * 32 + (tid & 31);
+      sl = t < T ? ((tid < 32) ? lsep[t] : dvp[t]) : 0.f;
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * u;
+      if (c < 64 * G::CH) {
+        const bool isd = c >= 32 * G::CH;
+        const int cc = isd ? c - 32 * G::CH : c;
+        const int row = cc / G::CH, col = (cc % G::CH) * 8;
+        *reinterpret_cast<u32x4*>(isd ? &dos[buf][row * G::RW + col] : &qs[buf][row * G::RW + col]) = stg[u];
+      }
+    }
+    if (tid < 64) lsd[buf][tid >> 5][tid & 31] = sl;
+  };
+  issue(first_qt);
+  commit(0);
+  __syncthreads();
+  for (int qt = first_qt; qt < nt; ++qt) {
+    const int cur = (qt - first_qt) & 1;
+    const bool more = qt + 1 < nt;
+    if (more) issue(qt + 1);
+    if (qt >= kt) {
+      const int q0 = qt * 32;
+      f32x16 sacc, dpacc;
+      zero16(sacc);
+      zero16(dpacc);
+#pragma unroll
+      for (int s = 0; s < G::NKS; ++s) {
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(&qs[cur][r * G::RW + 16 * s + 8 * h]);
+        const bf16x8 da = *reinterpret_cast<const bf16x8*>(&dos[cur][r * G::RW + 16 * s + 8 * h]);
+        sacc = mfma32(qa, kf[s], sacc);    // S[q][key]
+        dpacc = mfma32(da, vf[s], dpacc);  // dP[q][key]
+      }
+      f32x16 pm;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(&lsd[cur][0][8 * g + 4 * h]);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&lsd[cur][1][8 * g + 4 * h]);
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int e = 4 * g + e4;
+          const int tq = q0 + 8 * g + 4 * h + e4;
+          const bool ok = kok && tq < T && tk <= tq;
+          const float pv = ok ? __expf(sacc[e] * scale - l4[e4]) : 0.f;
+          pm[e] = pv;
+          sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc_frag(pm, s);
+        const bf16x8 df = acc_frag(sacc, s);
+#pragma unroll
+        for (int dt = 0; dt < G::ND; ++dt) {
+          dv[dt] = mfma32(pf, tr_frag(dos[cur], G::RW, dt, s, lane), dv[dt]);
+          dk[dt] = mfma32(df, tr_frag(qs[cur], G::RW, dt, s, lane), dk[dt]);
+        }
+      }
+    }
+    if (more) commit(cur ^ 1);
+    __syncthreads();
   }
   // dK/dV tiles: rows = key ((e&3)+8(e>>2)+4h), cols = d (lane)
   bf16_t* dkp = P.dk[j] + head * P.dkv_hstride;
   bf16_t* dvo = P.dv[j] + head * P.dkv_hstride;
 #pragma unroll
-  for (int dt = 0; dt < ND; ++dt) {
+  for (int dt = 0; dt < G::ND; ++dt) {
     const int d = dt * 32 + r;
     if (d >= HS) continue;
 #pragma unroll
@@ -385,14 +499,13 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_kernel(AttnBatch batch, int 
 
 template <int HS>
 static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
-  const int nt = (T + 31) / 32;
+  const int nb = (T + 127) / 128;
   if (!bwd) {
-    hipLaunchKernelGGL(attn_fwd_kernel<HS>, dim3(nt, B * H, bt.count), dim3(64), 0, s, bt, T, H, scale);
+    hipLaunchKernelGGL(attn_fwd_kernel<HS>, dim3(nb, B * H, bt.count), dim3(256), 0, s, bt, T, H, scale);
   } else {
-    int maxs = 1;
-    for (int g = 0; g < bt.count; ++g) maxs = bt.p[g].nstreams > maxs ? bt.p[g].nstreams : maxs;
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<HS>, dim3(nt, B * H, bt.count), dim3(64), 0, s, bt, T, H, scale);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HS>, dim3(nt, B * H * maxs, bt.count), dim3(64), 0, s, bt, T, H, scale);
+    const int ns = bt.p[0].nstreams;
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<HS>, dim3(nb, B * H, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HS>, dim3(nb, B * H * ns, bt.count), dim3(256), 0, s, bt, T, H, scale);
   }
 }
 

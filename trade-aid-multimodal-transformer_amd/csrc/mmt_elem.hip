@@ -165,22 +165,57 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbBatch batch, int R, i
   reinterpret_cast<f32x4*>(P.x + (int64_t)r * C)[c4] = a + p;
 }
 
-__global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBatch batch, int R, int T, int C) {
+// token-table gradient: a block owns 256 rows of one modality. Small tables (V*C <= 16K floats)
+// are accumulated in LDS first and flushed with one atomic per touched element per block (the
+// per-token contention of a 5- or 13-entry vocabulary would otherwise serialise thousands of adds
+// on the same addresses); large tables take direct global atomics (few rows per token).
+#define EMB_LDS_FLOATS 16384
+__global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int R, int C) {
   const EmbProblem& P = batch.p[blockIdx.z];
   const int C4 = C >> 2;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)R * C4) return;
-  const int r = (int)(i / C4), c4 = (int)(i % C4);
-  const int t = r % T;
-  int64_t id = P.idx[r];
-  id = id < 0 ? 0 : (id >= P.V ? P.V - 1 : id);
-  const f32x4 d = reinterpret_cast<const f32x4*>(P.dx + (int64_t)r * C)[c4];
-  float* dt = P.dtok + id * C + c4 * 4;
-  float* dp = P.dpos + (int64_t)t * C + c4 * 4;
+  const int r0 = blockIdx.x * 256;
+  const int rows = min(256, R - r0);
+  if (rows <= 0) return;
+  __shared__ float acc[EMB_LDS_FLOATS];
+  const bool priv = (int64_t)P.V * C <= EMB_LDS_FLOATS;
+  if (priv) {
+    for (int q = threadIdx.x; q < P.V * C; q += 256) acc[q] = 0.f;
+    __syncthreads();
+  }
+  for (int q = threadIdx.x; q < rows * C4; q += 256) {
+    const int rr = r0 + q / C4, c4 = q % C4;
+    int64_t id = P.idx[rr];
+    id = id < 0 ? 0 : (id >= P.V ? P.V - 1 : id);
+    const f32x4 d = reinterpret_cast<const f32x4*>(P.dx + (int64_t)rr * C)[c4];
+    if (priv) {
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    atomicAdd(dt + e, d[e]);
-    atomicAdd(dp + e, d[e]);
+      for (int e = 0; e < 4; ++e) atomicAdd(&acc[id * C + c4 * 4 + e], d[e]);
+    } else {
+      float* dt = P.dtok + id * C + c4 * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(dt + e, d[e]);
+    }
+  }
+  if (priv) {
+    __syncthreads();
+    for (int q = threadIdx.x; q < P.V * C; q += 256)
+      if (acc[q] != 0.f) atomicAdd(P.dtok + q, acc[q]);
+  }
+}
+
+// positional-table gradient, shared by all modalities: dpos[t] = sum_m sum_b dx_m[b*T + t]
+// one block per t; deterministic (no atomics): the grad buffer is pre-zeroed, dpos is added once
+__global__ __launch_bounds__(256) void embed_pos_bwd_kernel(EmbBatch batch, int B, int T, int C) {
+  const int t = blockIdx.x;
+  const int C4 = C >> 2;
+  for (int c4 = threadIdx.x; c4 < C4; c4 += 256) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < batch.count; ++m) {
+      const EmbProblem& P = batch.p[m];
+      for (int b = 0; b < B; ++b) s += reinterpret_cast<const f32x4*>(P.dx + ((int64_t)b * T + t) * C)[c4];
+    }
+    f32x4* dp = reinterpret_cast<f32x4*>(batch.p[0].dpos + (int64_t)t * C) + c4;
+    *dp = *dp + s;
   }
 }
 
@@ -194,9 +229,12 @@ hipError_t mmt_launch_embed_fwd(const EmbBatch& b, int B, int T, int C, hipStrea
 
 hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStream_t s) {
   if (C % 4 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
-  const int64_t n = (int64_t)B * T * (C / 4);
-  dim3 grid((unsigned)((n + 255) / 256), 1, b.count);
-  hipLaunchKernelGGL(embed_bwd_kernel, grid, dim3(256), 0, s, b, B * T, T, C);
+  const int R = B * T;
+  hipLaunchKernelGGL(embed_tok_bwd_kernel, dim3((R + 255) / 256, 1, b.count), dim3(256), 0, s, b, R, C);
+  // all problems of one batch must share the positional table (one model): dpos of p[0]
+  for (int g = 1; g < b.count; ++g)
+    if (b.p[g].dpos != b.p[0].dpos) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(embed_pos_bwd_kernel, dim3(T), dim3(256), 0, s, b, B, T, C);
   return hipGetLastError();
 }
 
@@ -289,111 +327,6 @@ hipError_t mmt_launch_colsum(const ColsumBatch& b, int R, hipStream_t s) {
   dim3 grid((maxn + 255) / 256, (R + 255) / 256, b.count);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, b, R);
   return hipGetLastError();
-}
-
-// ============================================================================================
-// Per-head Q/K/V stage 2 (model.py:36-50): Linear(hs/2, hs, bias=False) per (kind, head)
-//   out[r, blk*hs + o] = sum_i W2[blk][o][i] * h1[r, blk*hh + i],  hh = hs/2
-// block = one blk x 256 rows; W2[blk] staged in LDS (fp32)
-// ============================================================================================
-template <int HS>
-__global__ __launch_bounds__(256) void qkv2_fwd_kernel(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
-  constexpr int HH = HS / 2;
-  const Qkv2Problem& P = batch.p[blockIdx.z];
-  const int blk = blockIdx.y;
-  __shared__ float w[HS * HH];
-  for (int i = threadIdx.x; i < HS * HH; i += 256) w[i] = P.w2[(int64_t)blk * HS * HH + i];
-  __syncthreads();
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= R) return;
-  float in[HH];
-  const bf16_t* src = P.h1 + (int64_t)r * ld_h1 + blk * HH;
-#pragma unroll
-  for (int i = 0; i < HH; ++i) in[i] = bf2f(src[i]);
-  bf16_t* dst = P.out + (int64_t)r * ld_out + blk * HS;
-#pragma unroll
-  for (int o = 0; o < HS; o += 2) {
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int i = 0; i < HH; ++i) { a += w[o * HH + i] * in[i]; b += w[(o + 1) * HH + i] * in[i]; }
-    *reinterpret_cast<uint32_t*>(dst + o) = pack2bf(a, b);
-  }
-}
-
-// backward: dh1 = (W2^T dout) * (1 - h1^2)  and  dW2 += dout^T h1 (per 256-row chunk, atomics)
-template <int HS>
-__global__ __launch_bounds__(256) void qkv2_bwd_kernel(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
-  constexpr int HH = HS / 2;
-  const Qkv2Problem& P = batch.p[blockIdx.z];
-  const int blk = blockIdx.y;
-  const int r0 = blockIdx.x * 256;
-  __shared__ float w[HS * HH];
-  __shared__ bf16_t sd[256][HS];
-  __shared__ bf16_t sh[256][HH];
-  for (int i = threadIdx.x; i < HS * HH; i += 256) w[i] = P.w2[(int64_t)blk * HS * HH + i];
-  {
-    const int r = r0 + threadIdx.x;
-    const bool ok = r < R;
-    const bf16_t* d = P.dout + (int64_t)r * ld_out + blk * HS;
-    const bf16_t* h = P.h1 + (int64_t)r * ld_h1 + blk * HH;
-#pragma unroll
-    for (int o = 0; o < HS; ++o) sd[threadIdx.x][o] = ok ? d[o] : (bf16_t)0;
-#pragma unroll
-    for (int i = 0; i < HH; ++i) sh[threadIdx.x][i] = ok ? h[i] : (bf16_t)0;
-  }
-  __syncthreads();
-  // data grad, thread per row
-  {
-    const int r = r0 + threadIdx.x;
-    if (r < R) {
-      bf16_t* dst = P.dh1 + (int64_t)r * ld_h1 + blk * HH;
-#pragma unroll
-      for (int i = 0; i < HH; ++i) {
-        float a = 0.f;
-#pragma unroll
-        for (int o = 0; o < HS; ++o) a += w[o * HH + i] * bf2f(sd[threadIdx.x][o]);
-        const float t = bf2f(sh[threadIdx.x][i]);
-        dst[i] = f2bf(a * (1.f - t * t));
-      }
-    }
-  }
-  // weight grad partials: outputs (o, i) distributed over threads
-  const int rows = min(256, R - r0);
-  for (int q = threadIdx.x; q < HS * HH; q += 256) {
-    const int o = q / HH, i = q % HH;
-    float a = 0.f;
-    for (int rr = 0; rr < rows; ++rr) a += bf2f(sd[rr][o]) * bf2f(sh[rr][i]);
-    atomicAdd(P.dw2 + (int64_t)blk * HS * HH + q, a);
-  }
-}
-
-template <int HS>
-static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_out, bool bwd, hipStream_t s) {
-  dim3 grid((R + 255) / 256, nblk, b.count);
-  if (bwd) hipLaunchKernelGGL(qkv2_bwd_kernel<HS>, grid, dim3(256), 0, s, b, R, ld_h1, ld_out);
-  else hipLaunchKernelGGL(qkv2_fwd_kernel<HS>, grid, dim3(256), 0, s, b, R, ld_h1, ld_out);
-}
-
-static hipError_t qkv2_dispatch(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, bool bwd,
-                                hipStream_t s) {
-  if (b.count == 0) return hipSuccess;
-  switch (hs) {
-    case 2: qkv2_launch<2>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
-    case 4: qkv2_launch<4>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
-    case 8: qkv2_launch<8>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
-    case 16: qkv2_launch<16>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
-    case 32: qkv2_launch<32>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
-    case 64: qkv2_launch<64>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
-hipError_t mmt_launch_qkv2_fwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s) {
-  return qkv2_dispatch(b, R, nblk, hs, ld_h1, ld_out, false, s);
-}
-hipError_t mmt_launch_qkv2_bwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s) {
-  return qkv2_dispatch(b, R, nblk, hs, ld_h1, ld_out, true, s);
 }
 
 // ============================================================================================

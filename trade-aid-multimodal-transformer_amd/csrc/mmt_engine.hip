@@ -374,8 +374,10 @@ int dw_splits(const GemmBatch& gb, int R) {
   for (int g = 0; g < gb.count; ++g)
     tiles += ((gb.p[g].M + 127) / 128) * ((gb.p[g].N + 127) / 128);
   if (tiles <= 0) return 1;
+  // every split adds one fp32 atomic per output element (the chip-wide atomic rate, ~1.3 TB/s,
+  // not the MFMA rate, bounds a heavily split launch): aim at ~one block per CU, at most 8 splits
   int s = 512 / tiles;
-  const int maxs = std::max(1, R / 512);
+  const int maxs = std::max(1, std::min(8, R / 1024));
   return std::max(1, std::min(s, maxs));
 }
 

@@ -1,14 +1,21 @@
 // bf16 MFMA GEMM for gfx950 with fused epilogues (forward linear, backward data, weight grad).
 //
-// Tile 128x128x32, 256 threads = 4 waves (2x2), each wave a 64x64 sub-tile as 2x2
-// v_mfma_f32_32x32x16_bf16 accumulators. Operand tiles are register-staged (16-B global loads)
-// into double-buffered LDS images, one barrier per K-step:
-//   K-contiguous operand  -> image [128 rows][32 k], 64-B rows, 16-B chunk XOR swizzle
-//                            (chunk ^= (row>>2)&3), fragments by ds_read_b128 (conflict-free)
-//   MN-contiguous operand -> image [32 k][128 (+32 pad)], 320-B rows,
-//                            fragments by ds_read_b64_tr_b16 (hardware transpose, conflict-free)
-// SWAP=true computes C^T tiles (N on accumulator rows, M on lanes) so each lane owns one output
-// row and 4 consecutive columns per register group: 8/16-B vector epilogue stores.
+// Tile 128x128, K-step 64, 256 threads = 4 waves (2x2), each wave a 64x64 sub-tile as 2x2
+// v_mfma_f32_32x32x16_bf16 accumulators (fp32).
+//
+// Operand staging is direct global->LDS (buffer_load_dwordx4 ... lds), no VGPR round trip, into
+// an S-stage LDS ring: the loads of K-step t+S-1 are in flight while step t computes; each step
+// starts with a counted `s_waitcnt vmcnt` (never 0 while later stages are in flight) and one raw
+// s_barrier. Out-of-range chunks (M/N/K edges) get an out-of-bounds buffer offset and land as
+// zeros (the buffer descriptor's range check), so edge tiles need no branches.
+//   K-contiguous operand  -> image [128 rows][64 k], 128-B rows, 16-B chunk XOR swizzle
+//                            chunk ^= (row>>1)&7 (conflict-free ds_read_b128 fragments)
+//   MN-contiguous operand -> image [64 k][128], 256-B rows, chunk ^= (k&3)<<2 (conflict-free
+//                            ds_read_b64_tr_b16 transposed fragments)
+// The swizzle is applied on the per-lane GLOBAL source address (the LDS destination of an
+// LDS-DMA is lane-linear) and again on the fragment read.
+// SWAP=true computes C^T tiles (N on accumulator rows, M on lanes): each lane owns one output row
+// and 4 consecutive columns per register group -> 8/16-B vector epilogue stores.
 // SWAP=false keeps N on lanes: 32 lanes hit 128 contiguous bytes of one row, the shape fp32
 // atomics need (weight-grad split-K accumulate).
 #include "mmt_common.h"
@@ -16,83 +23,70 @@
 
 #define GBM 128
 #define GBN 128
-#define GBK 32
-#define KC_ROWB 64
-#define MN_ROWB 320
-#define IMG_BYTES 10240
 
-template <bool KC>
-__device__ __forceinline__ void stage_load(const bf16_t* __restrict__ base, int ld, int rows_total, int K, int r0,
-                                           int k0, u32x4 (&reg)[2], int tid) {
+// tuning knob (mmt_gemm_set_variant): pipeline variant of the forward / backward-data GEMMs in
+// bits 0-3 and of the weight-grad (split-K, atomic) GEMMs in bits 4-7:
+//   0 = BK 64 x 2 stages, 1 = BK 32 x 2, 2 = BK 32 x 3, 3 = BK 32 x 4, 4 = BK 64 x 3
+static int g_gemm_variant = 0;      // forward / backward-data
+static int g_gemm_variant_dw = 3;   // weight grad: long K loops want a deeper ring
+extern "C" int mmt_gemm_set_variant(int v) {
+  if ((v & 15) > 4 || ((v >> 4) & 15) > 4) return -1;
+  g_gemm_variant = v & 15;
+  g_gemm_variant_dw = (v >> 4) & 15;
+  return 0;
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// swizzle of the 16-B chunk index of a K-contiguous image row (BK/8 chunks per row):
+//   BK 64 (128-B rows): chunk ^ ((row>>1)&7) ; BK 32 (64-B rows): chunk ^ ((row>>2)&3)
+template <int BK>
+__device__ __forceinline__ int kc_swz(int chunk, int row) {
+  return BK == 64 ? (chunk ^ ((row >> 1) & 7)) : (chunk ^ ((row >> 2) & 3));
+}
+
+// issue this wave's LDS-DMA pieces (1 KiB each) of one operand tile for K-step k0.
+// the tile (128 x BK bf16) has BK/4 pieces, BK/16 per wave; lane L writes LDS bytes [i*1024 + 16L, +16).
+template <int BK, bool KC>
+__device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rsrc, char* img, int ld, int rows_total, int K,
+                                           int r0, int k0, int wave, int lane) {
+  constexpr int PPW = BK / 16;  // pieces per wave
+  constexpr int CPR = BK / 8;   // chunks per K-contiguous row
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i;
-    int row, kk;
-    if (KC) { row = c >> 2; kk = (c & 3) * 8; } else { kk = c >> 4; row = (c & 15) * 8; }
-    const int grow = r0 + row, gk = k0 + kk;
-    u32x4 v = {0u, 0u, 0u, 0u};
+  for (int u = 0; u < PPW; ++u) {
+    const int i = wave * PPW + u;
+    int voff;
     if (KC) {
-      if (grow < rows_total) {
-        const bf16_t* src = base + (int64_t)grow * ld + gk;
-        if (gk + 8 <= K) {
-          v = *reinterpret_cast<const u32x4*>(src);
-        } else if (gk < K) {
-          uint16_t e[8];
-#pragma unroll
-          for (int t = 0; t < 8; ++t) e[t] = (gk + t < K) ? src[t] : (uint16_t)0;
-          v = {e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
-               e[6] | ((uint32_t)e[7] << 16)};
-        }
-      }
+      const int row = (64 / CPR) * i + lane / CPR;
+      const int chunk = kc_swz<BK>(lane % CPR, row);
+      const int grow = r0 + row, gk = k0 + chunk * 8;
+      voff = (grow < rows_total && gk < K) ? (grow * ld + gk) * 2 : 0x7fffffff;
     } else {
-      if (gk < K) {
-        const bf16_t* src = base + (int64_t)gk * ld + grow;
-        if (grow + 8 <= rows_total) {
-          v = *reinterpret_cast<const u32x4*>(src);
-        } else if (grow < rows_total) {
-          uint16_t e[8];
-#pragma unroll
-          for (int t = 0; t < 8; ++t) e[t] = (grow + t < rows_total) ? src[t] : (uint16_t)0;
-          v = {e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
-               e[6] | ((uint32_t)e[7] << 16)};
-        }
-      }
+      const int kr = 4 * i + (lane >> 4);
+      const int chunk = (lane & 15) ^ ((kr & 3) << 2);
+      const int gk = k0 + kr, gcol = r0 + chunk * 8;
+      voff = (gk < K && gcol < rows_total) ? (gk * ld + gcol) * 2 : 0x7fffffff;
     }
-    reg[i] = v;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(img + i * 1024), 16, voff, 0, 0, 0);
   }
 }
 
-template <bool KC>
-__device__ __forceinline__ void stage_store(char* img, const u32x4 (&reg)[2], int tid) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tid + 256 * i;
-    int off;
-    if (KC) {
-      const int row = c >> 2, ch = c & 3;
-      off = row * KC_ROWB + ((ch ^ ((row >> 2) & 3)) << 4);
-    } else {
-      const int kk = c >> 4, mc = c & 15;
-      off = kk * MN_ROWB + mc * 16;
-    }
-    *reinterpret_cast<u32x4*>(img + off) = reg[i];
-  }
-}
-
-// fragment for "lane row = sb + (lane&31), k = 16*s + 8*(lane>>5) + j"
-template <bool KC>
+// fragment for "lane row = sb + (lane&31), k = 16*s + 8*(lane>>5) + j" from a staged image
+template <int BK, bool KC>
 __device__ __forceinline__ bf16x8 frag(const char* img, int sb, int s, int lane) {
   if (KC) {
     const int row = sb + (lane & 31);
-    const int ch = 2 * s + (lane >> 5);
-    return *reinterpret_cast<const bf16x8*>(img + row * KC_ROWB + ((ch ^ ((row >> 2) & 3)) << 4));
+    const int ch = kc_swz<BK>(2 * s + (lane >> 5), row);
+    return *reinterpret_cast<const bf16x8*>(img + row * (BK * 2) + ch * 16);
   } else {
     const int g = lane >> 4, i = lane & 15;
     const int q = i >> 2, p = i & 3;
     const int col = sb + 16 * (g & 1) + 4 * p;
-    const int kr = 16 * s + 8 * (g >> 1) + q;
-    s16x4 lo = lds_tr16(img + kr * MN_ROWB + col * 2);
-    s16x4 hi = lds_tr16(img + (kr + 4) * MN_ROWB + col * 2);
+    const int kr = 16 * s + 8 * (g >> 1) + q;  // kr & 3 == q ; (kr + 4) & 3 == q
+    const int ch = (col >> 3) ^ (q << 2);
+    const int within = (col & 7) * 2;
+    const s16x4 lo = lds_tr16(img + kr * (GBM * 2) + ch * 16 + within);
+    const s16x4 hi = lds_tr16(img + (kr + 4) * (GBM * 2) + ch * 16 + within);
     return join4(lo, hi);
   }
 }
@@ -145,7 +139,6 @@ __device__ __forceinline__ void epi_vec4(const GemmProblem& P, float alpha, int 
       *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
     return;
   }
-  // bf16 outputs
   *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
 }
 
@@ -172,30 +165,64 @@ __device__ __forceinline__ void epi_scalar(const GemmProblem& P, float alpha, in
   P.o16[(int64_t)m * P.ldo16 + n] = f2bf(r);
 }
 
-template <bool A_KC, bool B_KC, bool SWAP, int EPI>
+// bf16 outputs feed later GEMMs as K-contiguous operands: their pad columns [N, ldo16) are kept
+// zero so a K-step that straddles N reads zeros there.
+template <int EPI>
+__device__ __forceinline__ void epi_pad(const GemmProblem& P, int m, int n) {
+  constexpr bool bf16_out = EPI == EPI_STORE_BF16 || EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 ||
+                            EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
+  if (bf16_out || (EPI == EPI_BIAS_RESID_F32 && P.o16)) {
+    if (n < P.ldo16) P.o16[(int64_t)m * P.ldo16 + n] = 0;
+  }
+}
+
+__device__ __forceinline__ void wait_vm(int n) {
+  // counted wait on this wave's outstanding LDS-DMA pieces (immediate operand: one case each)
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+  }
+}
+
+template <int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
+  constexpr int IMG_BYTES = GBM * BK * 2;  // per operand per stage (both layouts)
+  constexpr int STAGE_BYTES = 2 * IMG_BYTES;
+  constexpr int PIECES = BK / 8;           // LDS-DMA pieces per wave per stage (A + B)
   const GemmProblem& P = batch.p[blockIdx.z];
   const int M = P.M, N = P.N, K = P.K;
   const int tiles_n = (N + GBN - 1) / GBN;
   const int tiles_m = (M + GBM - 1) / GBM;
-  const int tile = blockIdx.x;
-  if (tile >= tiles_m * tiles_n) return;
+  const int ntiles = tiles_m * tiles_n;
+  // XCD-aware remap (bijective): blocks b and b+8 share an XCD; give each XCD a contiguous run
+  // of tiles so neighbouring tiles (same A row panel) share that XCD's L2
+  int tile = blockIdx.x;
+  {
+    const int nwg = gridDim.x;
+    const int x = tile % 8, q = nwg / 8, rr = nwg % 8;
+    tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + tile / 8;
+  }
+  if (tile >= ntiles) return;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int nsplit = gridDim.y;
-  const int ksteps = (K + GBK - 1) / GBK;
+  const int ksteps = (K + BK - 1) / BK;
   const int kper = (ksteps + nsplit - 1) / nsplit;
   const int ks0 = blockIdx.y * kper;
   const int ks1 = min(ksteps, ks0 + kper);
   if (EPI == EPI_ATOMIC_F32 && ks0 >= ks1) return;  // nothing to add
 
-  __shared__ __attribute__((aligned(16))) char lds[4 * IMG_BYTES];
-#define IMG_A(b) (lds + (b) * IMG_BYTES)
-#define IMG_B(b) (lds + (2 + (b)) * IMG_BYTES)
+  // one LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads):
+  // the stage ring during the K loop, the fp32 output tile (128 x 132) in the epilogue
+  constexpr int RING = ST * STAGE_BYTES, CTILE = GBM * (GBN + 4) * 4;
+  __shared__ __attribute__((aligned(1024))) char lds[RING > CTILE ? RING : CTILE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
   f32x16 acc[2][2];
@@ -207,26 +234,36 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
   if (ks0 < ks1) {
-    u32x4 ra[2], rb[2];
-    stage_load<A_KC>(P.A, P.lda, M, K, m0, ks0 * GBK, ra, tid);
-    stage_load<B_KC>(P.B, P.ldb, N, K, n0, ks0 * GBK, rb, tid);
-    stage_store<A_KC>(IMG_A(0), ra, tid);
-    stage_store<B_KC>(IMG_B(0), rb, tid);
-    __syncthreads();
-    for (int ks = ks0; ks < ks1; ++ks) {
-      const int cur = (ks - ks0) & 1;
-      const bool more = ks + 1 < ks1;
-      if (more) {
-        stage_load<A_KC>(P.A, P.lda, M, K, m0, (ks + 1) * GBK, ra, tid);
-        stage_load<B_KC>(P.B, P.ldb, N, K, n0, (ks + 1) * GBK, rb, tid);
-      }
+    // buffer descriptors over each operand's whole extent (range-checked: OOB pieces read 0)
+    const int a_rows = A_KC ? M : K, b_rows = B_KC ? N : K;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)P.A, (short)0, (int)min((int64_t)a_rows * P.lda * 2, (int64_t)0x7ffffff0), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)P.B, (short)0, (int)min((int64_t)b_rows * P.ldb * 2, (int64_t)0x7ffffff0), 0x00020000);
+    const int nk = ks1 - ks0;
+    auto issue = [&](int t) {  // K-step ks0 + t into stage t % ST
+      char* st = lds + (t % ST) * STAGE_BYTES;
+      issue_tile<BK, A_KC>(ra, st, P.lda, M, K, m0, (ks0 + t) * BK, wave, lane);
+      issue_tile<BK, B_KC>(rb, st + IMG_BYTES, P.ldb, N, K, n0, (ks0 + t) * BK, wave, lane);
+    };
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+    for (int t = 0; t < ST - 1; ++t)
+      if (t < nk) issue(t);
+    for (int t = 0; t < nk; ++t) {
+      // stage t landed for this wave: allow the younger stages' pieces to stay in flight
+      wait_vm(PIECES * min(ST - 2, nk - 1 - t));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's pieces of stage t landed; stage t-1 reads done
+      if (t + ST - 1 < nk) issue(t + ST - 1);
+      const char* imgA = lds + (t % ST) * STAGE_BYTES;
+      const char* imgB = imgA + IMG_BYTES;
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
         bf16x8 fa[2], fb[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fa[j] = frag<A_KC>(IMG_A(cur), wm * 64 + 32 * j, s, lane);
+        for (int j = 0; j < 2; ++j) fa[j] = frag<BK, A_KC>(imgA, wm * 64 + 32 * j, s, lane);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) fb[i] = frag<B_KC>(IMG_B(cur), wn * 64 + 32 * i, s, lane);
+        for (int i = 0; i < 2; ++i) fb[i] = frag<BK, B_KC>(imgB, wn * 64 + 32 * i, s, lane);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -235,11 +272,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
             else acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
           }
       }
-      if (more) {
-        stage_store<A_KC>(IMG_A(cur ^ 1), ra, tid);
-        stage_store<B_KC>(IMG_B(cur ^ 1), rb, tid);
-      }
-      __syncthreads();
     }
   }
 
@@ -250,26 +282,100 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
   // groups aligned; bias pointers are 64-B aligned by the parameter layout.
   const bool vec_ok = ((P.ldc | P.ldres | P.ldo16 | P.ldaux) & 3) == 0;
   if (SWAP) {
+    // Stage the fp32 tile through LDS, then run the epilogue row-major: each wave touches two
+    // whole 128-column row segments per instruction (coalesced bias / aux / resid reads and
+    // output writes) instead of 16 B in each of 32 rows.
     // acc[i][j]: rows = n (sub-tile i), cols = m (sub-tile j)
+    constexpr int CT = GBN + 4;  // fp32 row stride of the staged tile (16-B aligned, de-conflicted)
+    float* ct = reinterpret_cast<float*>(lds);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's last fragment reads of the stage ring are done
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int m = m0 + wm * 64 + 32 * j + r;
-        if (m >= M) continue;
+        const int ml = wm * 64 + 32 * j + r;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int n = n0 + wn * 64 + 32 * i + 8 * g + 4 * h;
-          const float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-          if (n + 4 <= N && vec_ok && EPI != EPI_ATOMIC_F32) {
-            epi_vec4<EPI>(P, alpha, m, n, v);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (n + e < N) epi_scalar<EPI>(P, alpha, m, n + e, v[e]);
-          }
+          const int nl = wn * 64 + 32 * i + 8 * g + 4 * h;
+          *reinterpret_cast<f32x4*>(ct + ml * CT + nl) =
+              f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
         }
       }
+    __syncthreads();
+    const int c4 = tid & 31;  // 4-column group of this thread
+    const int n = n0 + 4 * c4;
+    constexpr bool HAS_AUX = EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
+    constexpr bool HAS_RES = EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32;
+    constexpr int IT = GBM / 8;
+    if (n + 4 <= N && vec_ok) {
+      // fast path: issue every operand load of this thread's 16 rows first (memory-level
+      // parallelism), then combine and store; full 4-column groups only
+      u32x2 auxv[IT];
+      f32x4 resv[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int m = m0 + it * 8 + (tid >> 5);
+        if (m < M) {
+          if (HAS_AUX) auxv[it] = *reinterpret_cast<const u32x2*>(P.aux + (int64_t)m * P.ldaux + n);
+          if (EPI == EPI_BIAS_RESID_F32) resv[it] = *reinterpret_cast<const f32x4*>(P.resid + (int64_t)m * P.ldres + n);
+          if (EPI == EPI_ACC_F32) resv[it] = *reinterpret_cast<const f32x4*>(P.o32 + (int64_t)m * P.ldc + n);
+        }
+      }
+      f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
+      if ((EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
+           EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16) && P.bias)
+        bias4 = *reinterpret_cast<const f32x4*>(P.bias + n);
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int ml = it * 8 + (tid >> 5);
+        const int m = m0 + ml;
+        if (m >= M) continue;
+        const f32x4 v4 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 4 * c4);
+        float r[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] = alpha * v4[e] + bias4[e];
+        if (EPI == EPI_BIAS_TANH_BF16) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) r[e] = tanhf(r[e]);
+        }
+        if (EPI == EPI_BIAS_RELU_BF16) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) r[e] = fmaxf(r[e], 0.0f);
+        }
+        if (HAS_AUX) {
+          const u32x2 a = auxv[it];
+          const float t[4] = {bf2f(a[0] & 0xffff), bf2f(a[0] >> 16), bf2f(a[1] & 0xffff), bf2f(a[1] >> 16)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            r[e] = (EPI == EPI_DTANH_BF16) ? r[e] * (1.0f - t[e] * t[e]) : (t[e] > 0.0f ? r[e] : 0.0f);
+        }
+        if (HAS_RES) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) r[e] += resv[it][e];
+        }
+        if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32 || EPI == EPI_ACC_F32) {
+          *reinterpret_cast<f32x4*>(P.o32 + (int64_t)m * P.ldc + n) = f32x4{r[0], r[1], r[2], r[3]};
+          if (EPI == EPI_BIAS_RESID_F32 && P.o16)
+            *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
+        } else {
+          *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
+        }
+      }
+    } else if (n < N + 4) {
+      // edge columns (and unaligned leading dimensions): scalar epilogue + zero pad columns
+      for (int it = 0; it < IT; ++it) {
+        const int ml = it * 8 + (tid >> 5);
+        const int m = m0 + ml;
+        if (m >= M) continue;
+        const f32x4 v4 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 4 * c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (n + e < N) epi_scalar<EPI>(P, alpha, m, n + e, v4[e]);
+          else epi_pad<EPI>(P, m, n + e);
+        }
+      }
+    }
   } else {
     // acc[i][j]: rows = m (sub-tile i), cols = n (sub-tile j)
 #pragma unroll
@@ -287,6 +393,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
   }
 }
 
+template <int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
+static void launch_v(const GemmBatch& b, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_kernel<BK, ST, A_KC, B_KC, SWAP, EPI>), grid, dim3(256), 0, s, b);
+}
+
 template <bool A_KC, bool B_KC, bool SWAP, int EPI>
 static hipError_t launch_t(const GemmBatch& b, int splits, hipStream_t s) {
   int maxtiles = 0;
@@ -297,12 +408,23 @@ static hipError_t launch_t(const GemmBatch& b, int splits, hipStream_t s) {
   }
   if (maxtiles == 0 || b.count == 0) return hipSuccess;
   dim3 grid(maxtiles, splits, b.count);
-  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, SWAP, EPI>), grid, dim3(256), 0, s, b);
+  switch (EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw : g_gemm_variant) {
+    case 1: launch_v<32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    case 2: launch_v<32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    case 3: launch_v<32, 4, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    case 4: launch_v<64, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    default: launch_v<64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+  }
   return hipGetLastError();
 }
 
 hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, int splits, hipStream_t s) {
   if (splits < 1) splits = 1;
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& P = b.p[g];
+    // 16-byte LDS-DMA pieces need 8-element-aligned leading dimensions and 16-byte aligned bases
+    if ((P.lda & 7) || (P.ldb & 7) || (((uintptr_t)P.A | (uintptr_t)P.B) & 15)) return hipErrorInvalidValue;
+  }
   if (a_kc && b_kc) {
     switch (epi) {
       case EPI_STORE_BF16: return launch_t<true, true, true, EPI_STORE_BF16>(b, 1, s);

@@ -1,0 +1,228 @@
+// Per-head Q/K/V stage 2 on MFMA (reference model.py:36-50: each of key/query/value of each head
+// ends in Linear(hs/2, hs, bias=False) after a tanh): 3*H independent [hs/2 -> hs] maps per row.
+//
+// forward   out^T[o][r] = sum_i W2[o][i] h1[r][i]          one 32x32x16 MFMA per (32 rows, blk)
+// backward  dh1^T[i][r] = (sum_o W2[o][i] dout[r][o]) * (1 - h1[r][i]^2)
+//           dW2[o][i]  += sum_r dout[r][o] h1[r][i]        K = rows, operands by transposed LDS reads
+// blk = kind*H + head; h1 / dh1 rows hold nblk*hs/2 columns, out / dout rows nblk*hs columns.
+#include "mmt_common.h"
+#include "mmt_kernels.h"
+
+template <int N>
+__device__ __forceinline__ void ld4_guarded(const bf16_t* p, int valid, uint32_t& w0, uint32_t& w1) {
+  // 4 bf16 at p (8-byte aligned); elements >= valid read as zero
+  if (valid >= 4) {
+    const u32x2 v = *reinterpret_cast<const u32x2*>(p);
+    w0 = v[0]; w1 = v[1];
+  } else {
+    uint16_t e[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) e[t] = t < valid ? p[t] : (uint16_t)0;
+    w0 = e[0] | ((uint32_t)e[1] << 16);
+    w1 = e[2] | ((uint32_t)e[3] << 16);
+  }
+}
+
+__device__ __forceinline__ bf16x8 pack8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const u32x4 v = {a, b, c, d};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int HS>
+__global__ __launch_bounds__(256) void qkv2_fwd_mfma(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
+  constexpr int HH = HS / 2;
+  constexpr int NOT = (HS + 31) / 32;  // output (o) tiles
+  constexpr int KS = (HH + 15) / 16;   // k-steps over i
+  const Qkv2Problem& P = batch.p[blockIdx.z];
+  const int blk = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int row = blockIdx.x * 128 + w * 32 + r;
+  const float* w2 = P.w2 + (int64_t)blk * HS * HH;
+  // B operand: h1[row][i = 16s + 8h + j]
+  bf16x8 hb[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int i0 = 16 * s + 8 * h;
+    uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+    if (row < R) {
+      const bf16_t* src = P.h1 + (int64_t)row * ld_h1 + blk * HH + i0;
+      if (i0 < HH) ld4_guarded<4>(src, HH - i0, a0, a1);
+      if (i0 + 4 < HH) ld4_guarded<4>(src + 4, HH - i0 - 4, b0, b1);
+    }
+    hb[s] = pack8(a0, a1, b0, b1);
+  }
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) {
+    const int o = ot * 32 + r;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 wa;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 16 * s + 8 * h + j;
+        wa[j] = (__bf16)((o < HS && i < HH) ? w2[o * HH + i] : 0.f);
+      }
+      acc = mfma32(wa, hb[s], acc);  // D[o][row]
+    }
+    // lane owns row (r) and o = ot*32 + (e&3) + 8(e>>2) + 4h
+    const int orow = blockIdx.x * 128 + w * 32 + r;
+    if (orow < R) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int o0 = ot * 32 + 8 * g + 4 * h;
+        if (o0 < HS)
+          *reinterpret_cast<u32x2*>(P.out + (int64_t)orow * ld_out + blk * HS + o0) =
+              u32x2{pack2bf(acc[4 * g], acc[4 * g + 1]), pack2bf(acc[4 * g + 2], acc[4 * g + 3])};
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// tr fragment of an LDS image [rows][ld] (ld elements per row): lane gets column
+// cb + (lane&31) and rows kb + 16s + 8(lane>>5) + 0..7 (B/A operand with k along rows)
+__device__ __forceinline__ bf16x8 tr_rows(const bf16_t* img, int ld, int kb, int cb, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int q = i >> 2, p = i & 3;
+  const int col = cb + 16 * (g & 1) + 4 * p;
+  const int kr = kb + 8 * (g >> 1) + q;
+  return join4(lds_tr16(img + kr * ld + col), lds_tr16(img + (kr + 4) * ld + col));
+}
+
+template <int HS>
+__global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
+  constexpr int HH = HS / 2;
+  constexpr int NOT = (HS + 31) / 32;
+  constexpr int SDW = (HS < 32 ? 32 : HS) + 16;  // sd row: HS cols (>= 32 for tr reads) + pad
+  constexpr int SHW = 32 + 16;                    // sh row: 32 cols (HH valid) + pad
+  constexpr int KSD = (HS + 15) / 16;             // k-steps over o for dh1
+  const Qkv2Problem& P = batch.p[blockIdx.z];
+  const int blk = blockIdx.y;
+  const int r0 = blockIdx.x * 256;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  __shared__ __attribute__((aligned(16))) bf16_t sd[256 * SDW];
+  __shared__ __attribute__((aligned(16))) bf16_t sh[256 * SHW];
+  __shared__ __attribute__((aligned(16))) bf16_t w2t[32 * SDW];
+  const float* w2 = P.w2 + (int64_t)blk * HS * HH;
+  // W2^T (bf16) : w2t[i][o]
+  for (int q = tid; q < 32 * SDW; q += 256) {
+    const int i = q / SDW, o = q % SDW;
+    w2t[q] = f2bf((i < HH && o < HS) ? w2[o * HH + i] : 0.f);
+  }
+  // dout chunk and h1 chunk, row per thread, zero padded
+  {
+    const int rr = r0 + tid;
+    const bool ok = rr < R;
+    const bf16_t* d = P.dout + (int64_t)rr * ld_out + blk * HS;
+    bf16_t* dd = sd + tid * SDW;
+#pragma unroll
+    for (int c = 0; c < SDW; c += 4) {
+      uint32_t a = 0, b = 0;
+      if (ok && c < HS) ld4_guarded<4>(d + c, HS - c, a, b);
+      *reinterpret_cast<u32x2*>(dd + c) = u32x2{a, b};
+    }
+    const bf16_t* hp = P.h1 + (int64_t)rr * ld_h1 + blk * HH;
+    bf16_t* hd = sh + tid * SHW;
+#pragma unroll
+    for (int c = 0; c < SHW; c += 4) {
+      uint32_t a = 0, b = 0;
+      if (ok && c < HH) ld4_guarded<4>(hp + c, HH - c, a, b);
+      *reinterpret_cast<u32x2*>(hd + c) = u32x2{a, b};
+    }
+  }
+  __syncthreads();
+  // ---- dh1 for this wave's 64 rows (2 sub-tiles of 32) ----
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const int lr = w * 64 + st * 32;  // local row base
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(w2t + r * SDW + 16 * s + 8 * h);  // W2^T[i=r][o]
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(sd + (lr + r) * SDW + 16 * s + 8 * h);  // dout[row][o]
+      acc = mfma32(a, b, acc);  // D[i][row]
+    }
+    const int grow = r0 + lr + r;
+    if (grow < R) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // D rows i = 8g + 4h + 0..3 cover i < 32 >= HH
+        const int i0 = 8 * g + 4 * h;
+        if (i0 < HH) {
+          const bf16_t* hv = sh + (lr + r) * SHW + i0;
+          float t[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { const float x = bf2f(hv[e]); t[e] = acc[4 * g + e] * (1.f - x * x); }
+          *reinterpret_cast<u32x2*>(P.dh1 + (int64_t)grow * ld_h1 + blk * HH + i0) =
+              u32x2{pack2bf(t[0], t[1]), pack2bf(t[2], t[3])};
+        }
+      }
+    }
+  }
+  // ---- dW2 partial over this wave's 64 rows: D[o][i] = sum_r dout[r][o] h1[r][i] ----
+  f32x16 dw[NOT];
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dw[ot][e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kb = w * 64 + 16 * s;
+      const bf16x8 a = tr_rows(sd, SDW, kb, ot * 32, lane);  // A[o][r]
+      const bf16x8 b = tr_rows(sh, SHW, kb, 0, lane);        // B[r][i]
+      dw[ot] = mfma32(a, b, dw[ot]);
+    }
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(sd);  // reuse: [4 waves][NOT*32 o][32 i] floats
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int o = ot * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      red[(w * NOT * 32 + o) * 32 + r] = dw[ot][e];
+    }
+  __syncthreads();
+  for (int q = tid; q < HS * HH; q += 256) {
+    const int o = q / HH, i = q % HH;
+    float s = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) s += red[(ww * NOT * 32 + o) * 32 + i];
+    atomicAdd(P.dw2 + (int64_t)blk * HS * HH + q, s);
+  }
+}
+
+template <int HS>
+static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_out, bool bwd, hipStream_t s) {
+  if (bwd) hipLaunchKernelGGL(qkv2_bwd_mfma<HS>, dim3((R + 255) / 256, nblk, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
+  else hipLaunchKernelGGL(qkv2_fwd_mfma<HS>, dim3((R + 127) / 128, nblk, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
+}
+
+static hipError_t qkv2_dispatch(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, bool bwd,
+                                hipStream_t s) {
+  if (b.count == 0 || R == 0) return hipSuccess;
+  switch (hs) {
+    case 8: qkv2_launch<8>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 16: qkv2_launch<16>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 24: qkv2_launch<24>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 32: qkv2_launch<32>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 48: qkv2_launch<48>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    case 64: qkv2_launch<64>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t mmt_launch_qkv2_fwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s) {
+  return qkv2_dispatch(b, R, nblk, hs, ld_h1, ld_out, false, s);
+}
+hipError_t mmt_launch_qkv2_bwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s) {
+  return qkv2_dispatch(b, R, nblk, hs, ld_h1, ld_out, true, s);
+}

@@ -69,6 +69,7 @@ _SIGS = {
     "mmt_batch_indices": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     "mmt_batch_gather": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), c_vp, c_i32, c_i32, ctypes.POINTER(c_vp),
                                  ctypes.POINTER(c_vp)]),
+    "mmt_gemm_set_variant": (c_i32, [ctypes.c_int]),
     "mmt_op_gemm": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp,
                             c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32]),
     "mmt_op_layernorm_fwd": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
