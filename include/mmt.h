@@ -80,6 +80,12 @@ int64_t mmt_workspace_bytes(mmt_ctx* ctx, int32_t batch);
 int mmt_forward(mmt_ctx* ctx, void* stream, int32_t batch, const int64_t* const* idx, const int64_t* const* tgt,
                 const float* params, float* const* logits, float* losses, void* workspace, int32_t training);
 
+/* dropout (model.py:57/69, 87/91, 107/116, 134/151, 171; nn.Dropout(p) in training mode only):
+ * masks are a counter hash of (seed, layer, modality, site, row, column) regenerated in the
+ * backward, so nothing is stored. Sets the seed of the NEXT training forward (and its backward);
+ * without a call the engine derives one from mmt_config.seed and a per-context counter. */
+int mmt_set_dropout_seed(mmt_ctx* ctx, uint64_t seed);
+
 /* backward of sum_i loss_grads[i] * loss_i through the last mmt_forward (same workspace/params).
  * grads: fp32 flat buffer (mmt_param_count elements) — OVERWRITTEN (zeroed then accumulated). */
 int mmt_backward(mmt_ctx* ctx, void* stream, const float* loss_grads, const float* params, float* grads,

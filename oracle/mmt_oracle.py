@@ -32,6 +32,7 @@ import math
 import numbers
 import random
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -137,14 +138,73 @@ def _ln(x, w, b):
     return F.layer_norm(x, (x.shape[-1],), w, b, 1e-5)
 
 
-def _drop(x, p, training, gen):
+# --------------------------------------------------------------------------------------
+# dropout masks: the build's counter hash (csrc/mmt_common.h mmt_hash, engine drop keys)
+# restated bit-for-bit, so a dropout forward/backward of the HIP path can be checked
+# element-exactly in its masks. (The reference draws nn.Dropout masks from torch's RNG; the
+# build documents this as its one RNG-stream divergence: same Bernoulli(1-p) / (1-p) law.)
+# --------------------------------------------------------------------------------------
+_U32 = np.uint32
+STREAM_SALT = 0x5BD1E995
+SITE_SA_PROB, SITE_SA_PROJ, SITE_FFN, SITE_CA_PROB, SITE_CA_PROJ = range(5)
+MAX_MOD = 8
+
+
+def mask_hash(a, b, c):
+    """mmt_hash over uint32 arrays (wrapping 32-bit arithmetic)."""
+    with np.errstate(over="ignore"):
+        a = np.asarray(a, dtype=_U32)
+        b = np.asarray(b, dtype=_U32)
+        c = np.asarray(c, dtype=_U32)
+        h = (a * _U32(0x9E3779B1)) ^ ((b + _U32(0x7F4A7C15)) * _U32(0x85EBCA77)) ^ ((c + _U32(0x165667B1)) * _U32(0xC2B2AE3D))
+        h = h ^ (h >> _U32(16))
+        h = h * _U32(0x7FEB352D)
+        h = h ^ (h >> _U32(15))
+        h = h * _U32(0x846CA68B)
+        h = h ^ (h >> _U32(16))
+    return h.astype(_U32)
+
+
+class HashDropout:
+    """Dropout masks of one training forward: seed (uint64) and probability p."""
+
+    def __init__(self, seed, p):
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.p = float(p)
+        self.thr = int(min(4294967295.0, max(1.0, math.floor(self.p * 4294967296.0))))
+        self.scale = float(np.float32(1.0 / (1.0 - self.p)))
+
+    def key(self, l, i, site):
+        return int(mask_hash(self.seed & 0xFFFFFFFF, self.seed >> 32, (l * MAX_MOD + i) * 8 + site))
+
+    def _mask(self, key, rows, cols):
+        keep = mask_hash(key, rows, cols) >= _U32(self.thr)
+        return torch.from_numpy(keep.astype(np.float32) * np.float32(self.scale))
+
+    def rowcol(self, l, i, site, B, T, C):
+        """[B, T, C] branch output: row b*T + t, column c."""
+        rows = (np.arange(B)[:, None, None] * T + np.arange(T)[None, :, None]).astype(np.int64)
+        return self._mask(self.key(l, i, site), rows, np.arange(C)[None, None, :])
+
+    def probs(self, l, i, site, j, h, H, B, T):
+        """[B, T, T] probabilities of head h, stream j: row (b*H + h)*T + t, column s."""
+        kj = int(mask_hash(self.key(l, i, site), j, STREAM_SALT))
+        rows = ((np.arange(B)[:, None, None] * H + h) * T + np.arange(T)[None, :, None]).astype(np.int64)
+        return self._mask(kj, rows, np.arange(T)[None, None, :])
+
+
+def _drop(x, p, training, mask_fn=None):
+    """nn.Dropout: torch's RNG by default, or an explicit (hash) mask (mask_fn() -> scaled mask)."""
     if not training or p == 0.0:
         return x
+    if mask_fn is not None:
+        return x * mask_fn()
     return F.dropout(x, p, True)
 
 
-def _head(sd, pre, x, p, training):
-    """model.py:60-73. k/q/v = Linear(C,hs/2)+b -> tanh -> Linear(hs/2,hs, no bias)."""
+def _head(sd, pre, x, p, training, dm=None):
+    """model.py:60-73. k/q/v = Linear(C,hs/2)+b -> tanh -> Linear(hs/2,hs, no bias).
+    dm: optional () -> mask for the probabilities (HashDropout)."""
     T = x.shape[1]
     def mlp(kind):
         h = torch.tanh(_lin(x, sd[f"{pre}{kind}.0.weight"], sd[f"{pre}{kind}.0.bias"]))
@@ -155,7 +215,7 @@ def _head(sd, pre, x, p, training):
     tril = torch.tril(torch.ones(T, T))
     aff = aff.masked_fill(tril == 0, float("-inf"))
     aff = F.softmax(aff, dim=-1)
-    aff = _drop(aff, p, training, None)
+    aff = _drop(aff, p, training, dm)
     v = mlp("value")
     return aff @ v
 
@@ -166,16 +226,20 @@ def _proj(sd, pre, x):
     return _lin(h, sd[f"{pre}proj.2.weight"], sd[f"{pre}proj.2.bias"])
 
 
-def _mha(sd, pre, x, cfg, training):
+def _mha(sd, pre, x, cfg, training, hd=None, l=0, i=0):
     """model.py:89-92."""
-    out = torch.cat([_head(sd, f"{pre}heads.{h}.", x, cfg.dropout, training) for h in range(cfg.H)], dim=-1)
-    return _drop(_proj(sd, pre, out), cfg.dropout, training, None)
+    B, T, C = x.shape
+    def pm(h):
+        return (lambda: hd.probs(l, i, SITE_SA_PROB, 0, h, cfg.H, B, T)) if hd else None
+    out = torch.cat([_head(sd, f"{pre}heads.{h}.", x, cfg.dropout, training, pm(h)) for h in range(cfg.H)], dim=-1)
+    return _drop(_proj(sd, pre, out), cfg.dropout, training,
+                 (lambda: hd.rowcol(l, i, SITE_SA_PROJ, B, T, C)) if hd else None)
 
 
-def _cross(sd, pre, qx, kv_list, cfg, training):
+def _cross(sd, pre, qx, kv_list, cfg, training, hd=None, l=0, i=0):
     """model.py:109-159: per head, per KV modality separate causal softmax, outputs summed."""
     hs = cfg.hs
-    T = qx.shape[1]
+    B, T, C = qx.shape
     tril = torch.tril(torch.ones(T, T))
     heads = []
     for h in range(cfg.H):
@@ -188,27 +252,33 @@ def _cross(sd, pre, qx, kv_list, cfg, training):
             aff = q @ k.transpose(-2, -1) * k.shape[-1] ** -0.5
             aff = aff.masked_fill(tril == 0, float("-inf"))
             aff = F.softmax(aff, dim=-1)
-            aff = _drop(aff, cfg.dropout, training, None)
+            aff = _drop(aff, cfg.dropout, training,
+                        (lambda: hd.probs(l, i, SITE_CA_PROB, j, h, cfg.H, B, T)) if hd else None)
             outs.append(aff @ v)
         heads.append(sum(outs))
     out = torch.cat(heads, dim=-1)
-    return _drop(_proj(sd, pre, out), cfg.dropout, training, None)
+    return _drop(_proj(sd, pre, out), cfg.dropout, training,
+                 (lambda: hd.rowcol(l, i, SITE_CA_PROJ, B, T, C)) if hd else None)
 
 
-def _ffn(sd, pre, x, cfg, training):
+def _ffn(sd, pre, x, cfg, training, hd=None, l=0, i=0):
     """model.py:167-175."""
+    B, T, C = x.shape
     h = torch.relu(_lin(x, sd[f"{pre}net.0.weight"], sd[f"{pre}net.0.bias"]))
-    return _drop(_lin(h, sd[f"{pre}net.2.weight"], sd[f"{pre}net.2.bias"]), cfg.dropout, training, None)
+    return _drop(_lin(h, sd[f"{pre}net.2.weight"], sd[f"{pre}net.2.bias"]), cfg.dropout, training,
+                 (lambda: hd.rowcol(l, i, SITE_FFN, B, T, C)) if hd else None)
 
 
-def _block(sd, l, xs, cfg, training):
+def _block(sd, l, xs, cfg, training, hd=None):
     """model.py:214-244."""
     p = f"blocks.{l}."
     att = []
     for i in range(cfg.M):
         x = xs[i]
-        x = x + _mha(sd, f"{p}sa_layers.{i}.", _ln(x, sd[f"{p}ln1_layers.{i}.weight"], sd[f"{p}ln1_layers.{i}.bias"]), cfg, training)
-        x = x + _ffn(sd, f"{p}ffwd_layers.{i}.", _ln(x, sd[f"{p}ln2_layers.{i}.weight"], sd[f"{p}ln2_layers.{i}.bias"]), cfg, training)
+        x = x + _mha(sd, f"{p}sa_layers.{i}.", _ln(x, sd[f"{p}ln1_layers.{i}.weight"], sd[f"{p}ln1_layers.{i}.bias"]), cfg,
+                     training, hd, l, i)
+        x = x + _ffn(sd, f"{p}ffwd_layers.{i}.", _ln(x, sd[f"{p}ln2_layers.{i}.weight"], sd[f"{p}ln2_layers.{i}.bias"]), cfg,
+                     training, hd, l, i)
         att.append(x)
     out = []
     for i in range(cfg.M):
@@ -217,13 +287,14 @@ def _block(sd, l, xs, cfg, training):
         if cfg.cross[i] and others:
             kv = [att[j] for j in others]
             xn = _ln(x, sd[f"{p}ln_cross_layers.{i}.weight"], sd[f"{p}ln_cross_layers.{i}.bias"])
-            x = x + _cross(sd, f"{p}cross_attention_layers.{i}.", xn, kv, cfg, training)
+            x = x + _cross(sd, f"{p}cross_attention_layers.{i}.", xn, kv, cfg, training, hd, l, i)
         out.append(x)
     return out
 
 
-def forward(sd, cfg, idx_list, targets_list=None, training=False):
-    """model.py:380-402. Returns (logits_list, losses_list | None)."""
+def forward(sd, cfg, idx_list, targets_list=None, training=False, hash_dropout=None):
+    """model.py:380-402. Returns (logits_list, losses_list | None).
+    hash_dropout: optional HashDropout giving the masks (training mode) instead of torch's RNG."""
     xs = []
     for i in range(cfg.M):
         B, T = idx_list[i].shape
@@ -231,7 +302,7 @@ def forward(sd, cfg, idx_list, targets_list=None, training=False):
         pos = sd["pre_block.position_embedding_table.weight"][torch.arange(T)]
         xs.append(tok + pos.expand_as(tok))
     for l in range(cfg.L):
-        xs = _block(sd, l, xs, cfg, training)
+        xs = _block(sd, l, xs, cfg, training, hash_dropout)
     logits = []
     for i in range(cfg.M):
         x = _ln(xs[i], sd[f"post_block.fin_norm_layers.{i}.weight"], sd[f"post_block.fin_norm_layers.{i}.bias"])
@@ -246,11 +317,13 @@ def forward(sd, cfg, idx_list, targets_list=None, training=False):
     return logits, losses
 
 
-def forward_backward(sd, cfg, idx_list, tgt_list):
+def forward_backward(sd, cfg, idx_list, tgt_list, hash_dropout=None):
     """One train-step forward + backward of sum(losses) (main.py:642-649). Returns logits,
-    losses and grads (None where the reference leaves .grad None)."""
+    losses and grads (None where the reference leaves .grad None). With hash_dropout the
+    step runs in training mode with those dropout masks."""
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
-    logits, losses = forward(leaves, cfg, idx_list, tgt_list, training=False)
+    logits, losses = forward(leaves, cfg, idx_list, tgt_list, training=hash_dropout is not None,
+                             hash_dropout=hash_dropout)
     total = sum(losses)
     total.backward()
     grads = {k: (v.grad.detach().clone() if v.grad is not None else None) for k, v in leaves.items()}

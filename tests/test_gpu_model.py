@@ -23,9 +23,9 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-def build(meta, sd):
+def build(meta, sd, dropout=0.0):
     config_utils._config_cache = {"n_embd": meta["n_embd"], "n_head": meta["n_head"], "n_layer": meta["n_layer"],
-                                  "block_size": meta["block_size"], "dropout": 0.0, "device": "cuda",
+                                  "block_size": meta["block_size"], "dropout": dropout, "device": "cuda",
                                   "batch_size": meta["B"], "eval_iters": 1}
     import model as mmt_model
     params = []
@@ -80,6 +80,44 @@ def test_forward_backward_matches_reference(name):
         # (tiny tensors whose gradient is a near-cancelling sum, e.g. a V=2 head's [2,1] weight)
         err = (g.float().cpu() - ref).norm().item()
         assert err <= 0.1 * ref.norm().item() or err <= 2e-3 * gnorm, (k, rel(g, ref), err, gnorm)
+
+
+@pytest.mark.parametrize("name,p", [("f_demo", 0.3), ("f_small", 0.1), ("f_hs32", 0.2)])
+def test_dropout_step_matches_oracle_masks(name, p):
+    """Training-mode step with dropout p: the HIP path against the CPU oracle run with the SAME
+    hash masks (oracle.HashDropout restates the kernels' counter hash bit-for-bit), at the bf16
+    tolerances above. Parity of the mask law itself: tests/test_oracle.py (keep rate 1-p)."""
+    import mmt_oracle as O
+    z, meta, cfg, sd, idx, tgt = model_fixture(name)
+    m = build(meta, sd, dropout=p)
+    m.train()
+    torch.manual_seed(7)
+    logits, losses = m([t.cuda() for t in idx], [t.cuda() for t in tgt])
+    sum(losses).backward()
+    torch.cuda.synchronize()
+    cfg.dropout = p
+    hd = O.HashDropout(m.last_dropout_seed, p)
+    r_logits, r_losses, r_grads = O.forward_backward(sd, cfg, idx, tgt, hash_dropout=hd)
+    got = torch.stack([l.detach().cpu() for l in losses])
+    ref = torch.stack(r_losses)
+    assert torch.allclose(got, ref, rtol=5e-3, atol=5e-3), (got, ref)
+    # the masks really act: the dropped loss differs from the eval-mode (golden) loss
+    assert (got - torch.from_numpy(z["losses"])).abs().max().item() > 1e-3
+    for i in range(cfg.M):
+        assert rel(logits[i], r_logits[i]) < 2e-2, i
+    names = [n for n, _ in m.named_reference_tensors()]
+    allg, allr = [], []
+    for k, g in zip(names, _grad_views(m)):
+        if r_grads.get(k) is not None and g.numel():
+            allg.append(g.flatten().cpu())
+            allr.append(r_grads[k].flatten())
+    assert rel(torch.cat(allg), torch.cat(allr)) < 3e-2
+    # eval mode: no dropout, the golden (reference) logits again
+    m.eval()
+    with torch.no_grad():
+        lg, _ = m([t.cuda() for t in idx], [t.cuda() for t in tgt])
+    for i in range(cfg.M):
+        assert rel(lg[i], torch.from_numpy(z[f"logits.{i}"])) < 2e-2, i
 
 
 def _grad_views(m):

@@ -96,3 +96,27 @@ def test_jitter_matches_reference():
     data = [int(x) for x in z["before"]]
     O.jitter_inplace(data, True, 12)
     np.testing.assert_array_equal(np.array(data), z["after"])
+
+
+def test_hash_dropout_mask_law():
+    """The build's dropout masks (counter hash): keep rate 1 - p, kept values scaled 1/(1-p),
+    distinct masks per site / stream / head, p = 0 leaves activations untouched."""
+    import mmt_oracle as O
+    hd = O.HashDropout(123456789012345, 0.1)
+    m = hd.rowcol(0, 0, O.SITE_FFN, 8, 64, 256)
+    keep = (m > 0).float().mean().item()
+    assert abs(keep - 0.9) < 0.005, keep
+    assert torch.allclose(m[m > 0], torch.full_like(m[m > 0], 1 / 0.9))
+    m2 = hd.rowcol(0, 0, O.SITE_SA_PROJ, 8, 64, 256)
+    m3 = hd.rowcol(1, 0, O.SITE_FFN, 8, 64, 256)
+    assert not torch.equal(m, m2) and not torch.equal(m, m3)
+    p0 = hd.probs(0, 1, O.SITE_CA_PROB, 0, 0, 4, 2, 32)
+    p1 = hd.probs(0, 1, O.SITE_CA_PROB, 1, 0, 4, 2, 32)
+    ph = hd.probs(0, 1, O.SITE_CA_PROB, 0, 1, 4, 2, 32)
+    assert not torch.equal(p0, p1) and not torch.equal(p0, ph)
+    x = torch.randn(3, 4)
+    assert torch.equal(O._drop(x, 0.0, True, lambda: None), x)
+    # the hash is a fixed function: pinned values guard the device/host/oracle restatements
+    assert int(O.mask_hash(1, 2, 3)) == 1107639200
+    assert int(O.mask_hash(0xFFFFFFFF, 0, 7)) == 352430166
+    assert O.mask_hash([1, 2], 3, 4).dtype == np.uint32

@@ -16,6 +16,9 @@
 //   dK, dV   S = Q K^T, dP = dO V^T (queries on rows); dV += P^T dO, dK += dS^T Q with P and dS
 //            taken from registers as the A operand and dO / Q by transposed LDS reads.
 // Head sizes 8..64: padded to 16 on the reduction side and to 32 on the output side.
+// Dropout (model.py:69, 151: applied to the normalised probabilities): a counter-hash mask
+// regenerated identically in all three kernels; O = (P.Z) V with Z = mask / (1 - p), so
+// dV = (P.Z)^T dO, dS = P.(Z.dP - D) with D = rowsum(dO.O) unchanged.
 #include "mmt_common.h"
 #include "mmt_kernels.h"
 
@@ -106,9 +109,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, i
 #pragma unroll
   for (int dt = 0; dt < G::ND; ++dt) zero16(otot[dt]);
 
+  const uint32_t drow = (uint32_t)(bh * T + tq);  // dropout hash row of this lane's query
   for (int j = 0; j < P.nstreams; ++j) {
     const bf16_t* kp = P.k[j] + head * P.kv_hstride;
     const bf16_t* vp = P.v[j] + head * P.kv_hstride;
+    const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
     float m = -INFINITY, l = 0.f;
     f32x16 oacc[G::ND];
 #pragma unroll
@@ -178,6 +183,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, i
         rs += __shfl_xor(rs, 32, 64);
         l = l * alpha + rs;
         m = mnew;
+        if (P.drop_thr) {  // dropout on the probabilities (the normaliser l keeps every term)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const uint32_t key = (uint32_t)(k0 + (e & 3) + 8 * (e >> 2) + 4 * h);
+            sacc[e] = (mmt_hash(dkey, drow, key) >= P.drop_thr) ? sacc[e] * P.drop_scale : 0.f;
+          }
+        }
 #pragma unroll
         for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
@@ -276,6 +288,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T
     dsum += __shfl_xor(dsum, 32, 64);
     if (qok && h == 0) P.dvec[j][(int64_t)bh * T + tq] = dsum;
     const float lse = qok ? P.lse[j][(int64_t)bh * T + tq] : 0.f;
+    const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+    const uint32_t drow = (uint32_t)(bh * T + tq);
     const bf16_t* kp = P.k[j] + head * P.kv_hstride;
     const bf16_t* vp = P.v[j] + head * P.kv_hstride;
     u32x4 stg[2];
@@ -327,7 +341,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T
           const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
           const bool ok = qok && key <= tq && key < T;
           const float pv = ok ? __expf(sacc[e] * scale - lse) : 0.f;
-          sacc[e] = pv * (dpacc[e] - dsum);  // dS^T
+          float dp = dpacc[e];
+          if (P.drop_thr) dp = (mmt_hash(dkey, drow, (uint32_t)key) >= P.drop_thr) ? dp * P.drop_scale : 0.f;
+          sacc[e] = pv * (dp - dsum);  // dS^T
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -396,6 +412,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBatch batch, int
 #pragma unroll
   for (int dt = 0; dt < G::ND; ++dt) { zero16(dk[dt]); zero16(dv[dt]); }
 
+  const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
   const float* lsep = P.lse[j] + (int64_t)bh * T;
   const float* dvp = P.dvec[j] + (int64_t)bh * T;
   const bf16_t* qp = P.q + head * HS;
@@ -461,8 +478,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBatch batch, int
           const int tq = q0 + 8 * g + 4 * h + e4;
           const bool ok = kok && tq < T && tk <= tq;
           const float pv = ok ? __expf(sacc[e] * scale - l4[e4]) : 0.f;
-          pm[e] = pv;
-          sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
+          if (P.drop_thr) {
+            const bool keep = mmt_hash(dkey, (uint32_t)(bh * T + tq), (uint32_t)tk) >= P.drop_thr;
+            pm[e] = keep ? pv * P.drop_scale : 0.f;
+            sacc[e] = pv * ((keep ? dpacc[e] * P.drop_scale : 0.f) - d4[e4]);
+          } else {
+            pm[e] = pv;
+            sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
+          }
         }
       }
 #pragma unroll

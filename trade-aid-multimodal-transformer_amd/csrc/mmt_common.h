@@ -61,8 +61,10 @@ __device__ __forceinline__ bf16x8 join4(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// counter-based hash RNG (dropout masks); identical in forward and backward
-__device__ __forceinline__ uint32_t mmt_hash(uint32_t a, uint32_t b, uint32_t c) {
+// counter-based hash RNG (dropout masks); identical in forward and backward, and restated
+// bit-for-bit by the host (mmt_engine.hip: drop keys) and by oracle/mmt_oracle.py (mask_hash)
+#define MMT_STREAM_SALT 0x5BD1E995u
+__host__ __device__ __forceinline__ uint32_t mmt_hash(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
   h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
   return h;

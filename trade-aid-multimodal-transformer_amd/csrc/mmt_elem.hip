@@ -52,60 +52,93 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnBatch batch, int R, int C
   if (lane == 0) { P.mean[row] = mean; P.rstd[row] = rstd; }
 }
 
-template <int NV>
+// backward: dx += rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dgamma/dbeta column sums.
+// One wave per row, RPI rows per iteration with every load issued up front (the kernel is
+// HBM-bound: x, dy, dx in; dx (+ bf16 copy) out). Optional: the bf16 copy carries the dropout
+// mask of the branch that consumes it and its column sums (that branch's bias gradient).
+template <int NV, int RPI>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBatch batch, int R, int C) {
   const LnProblem& P = batch.p[blockIdx.z];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int C4 = C >> 2;
-  f32x4 g[NV], dgam[NV], dbet[NV];
+  const bool drop = P.drop_thr != 0;
+  f32x4 g[NV], dgam[NV], dbet[NV], dsm[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c4 = lane + 64 * i;
     g[i] = (c4 < C4) ? reinterpret_cast<const f32x4*>(P.gamma)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
     dgam[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     dbet[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dsm[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
-    const float mean = P.mean[row], rstd = P.rstd[row];
-    const f32x4* x = reinterpret_cast<const f32x4*>(P.x + (int64_t)row * C);
-    const f32x4* dy = reinterpret_cast<const f32x4*>(P.dy + (int64_t)row * C);
-    f32x4 xh[NV], gd[NV];
-    float s1 = 0.f, s2 = 0.f;
+  const int stride = gridDim.x * 4;
+  for (int row0 = blockIdx.x * 4 + wave; row0 < R; row0 += stride * RPI) {
+    f32x4 xv[RPI][NV], dv[RPI][NV], ov[RPI][NV];
+    float mean[RPI], rstd[RPI];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 < C4) {
-        const f32x4 xv = x[c4], dv = dy[c4];
+    for (int u = 0; u < RPI; ++u) {
+      const int row = row0 + u * stride;
+      const bool ok = row < R;
+      mean[u] = ok ? P.mean[row] : 0.f;
+      rstd[u] = ok ? P.rstd[row] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c4 = lane + 64 * i;
+        const bool in = ok && c4 < C4;
+        const int64_t o = (int64_t)row * C4 + c4;
+        xv[u][i] = in ? reinterpret_cast<const f32x4*>(P.x)[o] : f32x4{0.f, 0.f, 0.f, 0.f};
+        dv[u][i] = in ? reinterpret_cast<const f32x4*>(P.dy)[o] : f32x4{0.f, 0.f, 0.f, 0.f};
+        ov[u][i] = in ? reinterpret_cast<const f32x4*>(P.dx)[o] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RPI; ++u) {
+      const int row = row0 + u * stride;
+      if (row >= R) break;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          xh[i][e] = (xv[e] - mean) * rstd;
-          gd[i][e] = dv[e] * g[i][e];
-          s1 += gd[i][e];
-          s2 += gd[i][e] * xh[i][e];
-          dgam[i][e] += dv[e] * xh[i][e];
-          dbet[i][e] += dv[e];
+          const float xh = (xv[u][i][e] - mean[u]) * rstd[u];
+          const float gd = dv[u][i][e] * g[i][e];
+          xv[u][i][e] = xh;
+          s1 += gd;
+          s2 += gd * xh;
+          dgam[i][e] += dv[u][i][e] * xh;
+          dbet[i][e] += dv[u][i][e];
+        }
+      }
+      s1 = warp_sum(s1) / C;
+      s2 = warp_sum(s2) / C;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c4 = lane + 64 * i;
+        if (c4 < C4) {
+          f32x4 o = ov[u][i];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += rstd[u] * (dv[u][i][e] * g[i][e] - s1 - xv[u][i][e] * s2);
+          const int64_t off = (int64_t)row * C4 + c4;
+          reinterpret_cast<f32x4*>(P.dx)[off] = o;
+          if (P.dx16) {
+            if (drop) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                o[e] = (mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(4 * c4 + e)) >= P.drop_thr) ? o[e] * P.drop_scale
+                                                                                                   : 0.f;
+            }
+            reinterpret_cast<u32x2*>(P.dx16)[off] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dsm[i][e] += o[e];
+          }
         }
       }
     }
-    s1 = warp_sum(s1) / C;
-    s2 = warp_sum(s2) / C;
-    f32x4* dx = reinterpret_cast<f32x4*>(P.dx + (int64_t)row * C);
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 < C4) {
-        f32x4 o = dx[c4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] += rstd * (gd[i][e] - s1 - xh[i][e] * s2);
-        dx[c4] = o;
-        if (P.dx16)
-          reinterpret_cast<u32x2*>(P.dx16 + (int64_t)row * C)[c4] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
-      }
-    }
   }
-  // reduce the 4 waves' partial dgamma/dbeta through LDS, then one atomic per column
-  __shared__ float red[2][4][1024];
+  // reduce the 4 waves' partial column sums through LDS, then one atomic per column
+  __shared__ float red[3][4][1024];
+  const int nred = P.dsum ? 3 : 2;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c4 = lane + 64 * i;
@@ -114,15 +147,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBatch batch, int R, int C
       for (int e = 0; e < 4; ++e) {
         red[0][wave][c4 * 4 + e] = dgam[i][e];
         red[1][wave][c4 * 4 + e] = dbet[i][e];
+        red[2][wave][c4 * 4 + e] = dsm[i][e];
       }
     }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
-    const float a = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    const float b = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
-    atomicAdd(P.dgamma + c, a);
-    atomicAdd(P.dbeta + c, b);
+    for (int k = 0; k < nred; ++k) {
+      const float a = red[k][0][c] + red[k][1][c] + red[k][2][c] + red[k][3][c];
+      atomicAdd((k == 0 ? P.dgamma : k == 1 ? P.dbeta : P.dsum) + c, a);
+    }
   }
 }
 
@@ -138,13 +172,14 @@ hipError_t mmt_launch_ln_fwd(const LnBatch& b, int R, int C, hipStream_t s) {
 
 hipError_t mmt_launch_ln_bwd(const LnBatch& b, int R, int C, hipStream_t s) {
   if (C % 4 != 0 || C > 1024 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
+  // 4 rows per block per pass; the grid is capped so the dgamma/dbeta atomics stay few
   int blocks = (R + 3) / 4;
   if (blocks > 1024) blocks = 1024;
   dim3 grid(blocks, 1, b.count);
   const int nv = (C / 4 + 63) / 64;
-  if (nv <= 1) hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, dim3(256), 0, s, b, R, C);
-  else if (nv <= 2) hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, dim3(256), 0, s, b, R, C);
-  else hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, dim3(256), 0, s, b, R, C);
+  if (nv <= 1) hipLaunchKernelGGL((ln_bwd_kernel<1, 4>), grid, dim3(256), 0, s, b, R, C);
+  else if (nv <= 2) hipLaunchKernelGGL((ln_bwd_kernel<2, 2>), grid, dim3(256), 0, s, b, R, C);
+  else hipLaunchKernelGGL((ln_bwd_kernel<4, 1>), grid, dim3(256), 0, s, b, R, C);
   return hipGetLastError();
 }
 
@@ -367,6 +402,43 @@ __global__ void f2bf_kernel(const float* __restrict__ src, bf16_t* __restrict__ 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     dst[i] = f2bf(src[i]);
 }
+// masked copy (dropout of the consuming branch) with fused column sums, grouped over modalities
+__global__ __launch_bounds__(256) void drop_copy_kernel(DropCopyBatch batch, int R, int C) {
+  const DropCopyProblem& P = batch.p[blockIdx.z];
+  const int C4 = C >> 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float red[4][1024];
+  for (int cb = 0; cb < C4; cb += 64) {
+    const int q = cb + lane;
+    f32x4 sm = {0.f, 0.f, 0.f, 0.f};
+    if (q < C4) {
+      for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
+        f32x4 o = reinterpret_cast<const f32x4*>(P.src)[(int64_t)row * C4 + q];
+        if (P.drop_thr) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            o[e] = (mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(4 * q + e)) >= P.drop_thr) ? o[e] * P.drop_scale : 0.f;
+        }
+        reinterpret_cast<u32x2*>(P.dst)[(int64_t)row * C4 + q] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+        sm += o;
+      }
+      *reinterpret_cast<f32x4*>(&red[wave][4 * q]) = sm;
+    }
+  }
+  if (!P.dsum) return;
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) atomicAdd(P.dsum + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+}
+
+hipError_t mmt_launch_drop_copy(const DropCopyBatch& b, int R, int C, hipStream_t s) {
+  if (C % 4 != 0 || C > 1024) return hipErrorInvalidValue;
+  if (b.count == 0 || R == 0) return hipSuccess;
+  int blocks = (R + 15) / 16;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(drop_copy_kernel, dim3(blocks, 1, b.count), dim3(256), 0, s, b, R, C);
+  return hipGetLastError();
+}
+
 hipError_t mmt_launch_f32_to_bf16(const float* src, bf16_t* dst, int64_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
   int64_t blocks = (n + 255) / 256;

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "mmt.h"
+#include "mmt_common.h"
 #include "mmt_kernels.h"
 
 namespace {
@@ -102,6 +103,11 @@ struct mmt_ctx {
   bool fwd_ready = false;
   bool last_training = false;
   uint64_t step_counter = 0;
+  // dropout: seed of the next training forward (mmt_set_dropout_seed) and of the last one
+  uint64_t next_seed = 0;
+  bool next_seed_set = false;
+  uint64_t fwd_seed = 0;
+  bool fwd_drop = false;
   const int64_t* last_idx[MAXM] = {};  // forward token ids, read by the embedding backward stage
   std::string err;
   std::string probe_label;
@@ -381,6 +387,10 @@ int dw_splits(const GemmBatch& gb, int R) {
   return std::max(1, std::min(s, maxs));
 }
 
+// dropout sites (model.py:69 SA probabilities, :91 SA projection, :151 CA probabilities,
+// :116 CA projection, :171 FFN output); one hash key per (seed, layer, modality, site)
+enum DropSite { DS_SA_PROB = 0, DS_SA_PROJ = 1, DS_FFN = 2, DS_CA_PROB = 3, DS_CA_PROJ = 4 };
+
 struct Runner {
   mmt_ctx* c;
   hipStream_t s;
@@ -389,6 +399,18 @@ struct Runner {
   const bf16_t* wpk;
   int B, R;
   int rc = MMT_OK;
+  bool drop = false;  // dropout active for this forward / its backward
+  uint64_t seed = 0;
+
+  // element kept iff mmt_hash(key, row, col) >= thr ; kept values scaled by 1 / (1 - p)
+  template <class Pm>
+  void set_drop(Pm& p, int l, int i, int site) const {
+    if (!drop) { p.drop_key = 0; p.drop_thr = 0; p.drop_scale = 1.f; return; }
+    const double pr = c->cfg.dropout;
+    p.drop_key = mmt_hash((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)((l * MAXM + i) * 8 + site));
+    p.drop_thr = (uint32_t)std::min(4294967295.0, std::max(1.0, std::floor(pr * 4294967296.0)));
+    p.drop_scale = (float)(1.0 / (1.0 - pr));
+  }
 
   bool ok(hipError_t e, const char* what) {
     if (e != hipSuccess && rc == MMT_OK) rc = fail(c, MMT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -474,6 +496,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       bf16_t* qkv = r.W<bf16_t>(a[i].qkv);
       q.q = qkv + C; q.q_ld = 3 * C; q.k[0] = qkv; q.v[0] = qkv + 2 * C; q.kv_ld = 3 * C; q.kv_hstride = hs;
       q.o = r.W<bf16_t>(a[i].o); q.o_ld = C; q.lse[0] = r.W<float>(a[i].lse); q.nstreams = 1;
+      r.set_drop(q, l, i, DS_SA_PROB);
     }
     r.probe_begin("attn_fwd");
     r.ok(mmt_launch_attn_fwd(ab, B, T, H, hs, scale, r.s), "attn_fwd");
@@ -487,6 +510,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       g.p[i] = gp_fwd(r.W<bf16_t>(a[i].p1), ldp, wpk, x[i].P2, R);
       g.p[i].bias = r.P(x[i].bp2); g.p[i].resid = xin[i]; g.p[i].ldres = C;
       g.p[i].o32 = r.W<float>(a[i].x1); g.p[i].ldc = C;
+      r.set_drop(g.p[i], l, i, DS_SA_PROJ);
     }
     r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "proj2");
     for (int i = 0; i < M; ++i) {
@@ -504,6 +528,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       g.p[i].bias = r.P(x[i].bf2); g.p[i].resid = r.W<float>(a[i].x1); g.p[i].ldres = C;
       g.p[i].o32 = r.W<float>(a[i].x2); g.p[i].ldc = C;
       if (c->any_cross) { g.p[i].o16 = r.W<bf16_t>(a[i].x2h); g.p[i].ldo16 = C; }
+      r.set_drop(g.p[i], l, i, DS_FFN);
     }
     r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "ffn2");
     std::vector<const float*> xout(M);
@@ -545,6 +570,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
           q.k[j] = kv; q.v[j] = kv + hs; q.oj[j] = r.W<bf16_t>(a[i].ocj[j]); q.lse[j] = r.W<float>(a[i].lsej[j]);
         }
         q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(a[i].oc); q.o_ld = C; q.nstreams = M - 1;
+        r.set_drop(q, l, i, DS_CA_PROB);
       }
       r.probe_begin("ca_attn_fwd");
       r.ok(mmt_launch_attn_fwd(cb, B, T, H, hs, scale, r.s), "ca_attn_fwd");
@@ -558,6 +584,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         g2.p[u] = gp_fwd(r.W<bf16_t>(a[i].pc), ldp, wpk, x[i].C2, R);
         g2.p[u].bias = r.P(x[i].bc2); g2.p[u].resid = r.W<float>(a[i].x2); g2.p[u].ldres = C;
         g2.p[u].o32 = r.W<float>(a[i].x3); g2.p[u].ldc = C;
+        r.set_drop(g2.p[u], l, i, DS_CA_PROJ);
         xout[i] = r.W<float>(a[i].x3);
       }
       r.gemm(g0, true, true, EPI_BIAS_TANH_BF16, 1, "ca_proj0");
@@ -601,6 +628,27 @@ void colsum_add(Runner& r, ColsumBatch& cb, int u, const bf16_t* x, int ld, floa
   cb.p[u].x = x; cb.p[u].ld = ld; cb.p[u].out = out; cb.p[u].N = N; cb.p[u].alpha_ptr = aptr; cb.p[u].alpha = alpha;
 }
 
+// The bf16 residual-gradient copy dres16 written by a LayerNorm backward feeds the dropped
+// branch that precedes it (layer lprev): its CA projection (cross modalities of a model with
+// cross-attention), else its FFN. The copy carries that branch's dropout mask and its column
+// sums are that branch's output-bias gradient. Modalities whose copy is rebuilt later (non-cross
+// modalities of a cross model) and lprev < 0 (embeddings) get no copy.
+void set_dres16_consumer(mmt_ctx* c, Runner& r, LnProblem& lp, int i, int lprev, float* grads) {
+  lp.dx16 = nullptr; lp.dsum = nullptr;
+  lp.drop_key = 0; lp.drop_thr = 0; lp.drop_scale = 1.f;
+  if (lprev < 0) return;
+  const LM& x = c->lm[(size_t)lprev * c->M + i];
+  if (c->any_cross) {
+    if (!x.cross) return;
+    r.set_drop(lp, lprev, i, DS_CA_PROJ);
+    lp.dsum = grads + x.bc2;
+  } else {
+    r.set_drop(lp, lprev, i, DS_FFN);
+    lp.dsum = grads + x.bf2;
+  }
+  lp.dx16 = r.W<bf16_t>(c->plan.dres16[i]);
+}
+
 int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads, float* grads) {
   const int M = c->M, C = c->C, H = c->H, hs = c->hs, R = r.R, B = r.B, T = c->T, L = c->L;
   const int ldh1 = r8(3 * H * c->hh), ldp = r8(C / 2);
@@ -626,17 +674,16 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     }
     r.dwgemm(dw, "head2_dw");
     r.ok(mmt_launch_colsum(cs, R, r.s), "head2_db");
+    for (int i = 0; i < M; ++i) dx.p[i].dbias = grads + c->post[i].b0;  // head0 bias grad fused
     r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "head2_dx");
     for (int i = 0; i < M; ++i) {
       const PostM& q = c->post[i];
       const bf16_t* g = r.W<bf16_t>(p.gbig[i]);
       dw.p[i] = gp_dw(g, c->ldvh[i], r.W<bf16_t>(p.lnf16[i]), C, grads, q.H0, R);
-      colsum_add(r, cs, i, g, c->ldvh[i], grads + q.b0, c->V[i] / 2, nullptr, 1.f);
       dx.p[i] = gp_dx(g, c->ldvh[i], wpk, q.H0, R);
       dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
     }
     r.dwgemm(dw, "head0_dw");
-    r.ok(mmt_launch_colsum(cs, R, r.s), "head0_db");
     r.gemm(dx, true, false, EPI_STORE_F32, 1, "head0_dx");
     LnBatch lb{}; lb.count = M;
     std::vector<const float*> xfin(M);
@@ -646,7 +693,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       r.ok(hipMemsetAsync(r.W<float>(p.dres[i]), 0, sizeof(float) * (size_t)R * C, r.s), "memset dres");
       lb.p[i].x = xfin[i]; lb.p[i].gamma = r.P(c->post[i].lnw); lb.p[i].mean = r.W<float>(p.meanf[i]);
       lb.p[i].rstd = r.W<float>(p.rstdf[i]); lb.p[i].dy = r.W<float>(p.dln[i]); lb.p[i].dx = r.W<float>(p.dres[i]);
-      lb.p[i].dx16 = r.W<bf16_t>(p.dres16[i]);
+      set_dres16_consumer(c, r, lb.p[i], i, L - 1, grads);
       lb.p[i].dgamma = grads + c->post[i].lnw; lb.p[i].dbeta = grads + c->post[i].lnb;
     }
     r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "lnf_bwd");
@@ -670,28 +717,25 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     const int nc = (int)cx.size();
     GemmBatch dw{}; dw.count = nc;
     GemmBatch dx{}; dx.count = nc;
-    ColsumBatch cs{}; cs.count = nc;
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
+      // dres16[i] already carries this projection's dropout mask; its bias grad came with it
       const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
       dw.p[u] = gp_dw(g, C, r.W<bf16_t>(a[i].pc), ldp, grads, x[i].C2, R);
-      colsum_add(r, cs, u, g, C, grads + x[i].bc2, C, nullptr, 1.f);
       dx.p[u] = gp_dx(g, C, wpk, x[i].C2, R);
       dx.p[u].aux = r.W<bf16_t>(a[i].pc); dx.p[u].ldaux = ldp; dx.p[u].o16 = r.W<bf16_t>(p.gp[i]); dx.p[u].ldo16 = ldp;
+      dx.p[u].dbias = grads + x[i].bc0;
     }
     r.dwgemm(dw, "ca_proj2_dw");
-    r.ok(mmt_launch_colsum(cs, R, r.s), "ca_proj2_db");
     r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "ca_proj2_dx");
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
       const bf16_t* g = r.W<bf16_t>(p.gp[i]);
       dw.p[u] = gp_dw(g, ldp, r.W<bf16_t>(a[i].oc), C, grads, x[i].C0, R);
-      colsum_add(r, cs, u, g, ldp, grads + x[i].bc0, C / 2, nullptr, 1.f);
       dx.p[u] = gp_dx(g, ldp, wpk, x[i].C0, R);
       dx.p[u].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[u].ldo16 = C;
     }
     r.dwgemm(dw, "ca_proj0_dw");
-    r.ok(mmt_launch_colsum(cs, R, r.s), "ca_proj0_db");
     r.gemm(dx, true, false, EPI_STORE_BF16, 1, "ca_proj0_dx");
     AttnBatch ab{}; ab.count = nc;
     for (int u = 0; u < nc; ++u) {
@@ -708,6 +752,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(a[i].oc); q.o_ld = C; q.nstreams = M - 1;
       q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dq = r.W<bf16_t>(p.gq[i]); q.dq_ld = C;
       q.dkv_ld = 2 * C; q.dkv_hstride = 2 * hs;
+      r.set_drop(q, l, i, DS_CA_PROB);
     }
     r.probe_begin("ca_attn_bwd");
     r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "ca_attn_bwd");
@@ -750,8 +795,13 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       }
       if (kw.count) { r.dwgemm(kw, "ca_kv_dw"); r.gemm(kx, true, false, EPI_ACC_F32, 1, "ca_kv_dx"); }
     }
-    for (int i = 0; i < M; ++i)
-      r.ok(mmt_launch_f32_to_bf16(r.W<float>(p.dres[i]), r.W<bf16_t>(p.dres16[i]), (int64_t)R * C, r.s), "dres16");
+    // bf16 copy for the FFN backward: FFN dropout mask + FFN output-bias gradient
+    DropCopyBatch db{}; db.count = M;
+    for (int i = 0; i < M; ++i) {
+      db.p[i].src = r.W<float>(p.dres[i]); db.p[i].dst = r.W<bf16_t>(p.dres16[i]); db.p[i].dsum = grads + x[i].bf2;
+      r.set_drop(db.p[i], l, i, DS_FFN);
+    }
+    r.ok(mmt_launch_drop_copy(db, R, C, r.s), "dres16");
   }
   if (r.rc != MMT_OK) return r.rc;
   // FFN
@@ -760,51 +810,48 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   ColsumBatch cs{}; cs.count = M;
   LnBatch lb{}; lb.count = M;
   for (int i = 0; i < M; ++i) {
+    // dres16[i] carries the FFN dropout mask; the FFN output-bias grad was summed with it
     const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
     dw.p[i] = gp_dw(g, C, r.W<bf16_t>(a[i].f), 4 * C, grads, x[i].F2, R);
-    colsum_add(r, cs, i, g, C, grads + x[i].bf2, C, nullptr, 1.f);
     dx.p[i] = gp_dx(g, C, wpk, x[i].F2, R);
     dx.p[i].aux = r.W<bf16_t>(a[i].f); dx.p[i].ldaux = 4 * C; dx.p[i].o16 = r.W<bf16_t>(p.gbig[i]); dx.p[i].ldo16 = 4 * C;
+    dx.p[i].dbias = grads + x[i].bf0;
   }
   r.dwgemm(dw, "ffn2_dw");
-  r.ok(mmt_launch_colsum(cs, R, r.s), "ffn2_db");
   r.gemm(dx, true, false, EPI_DRELU_BF16, 1, "ffn2_dx");
   for (int i = 0; i < M; ++i) {
     const bf16_t* g = r.W<bf16_t>(p.gbig[i]);
     dw.p[i] = gp_dw(g, 4 * C, r.W<bf16_t>(a[i].c), C, grads, x[i].F0, R);
-    colsum_add(r, cs, i, g, 4 * C, grads + x[i].bf0, 4 * C, nullptr, 1.f);
     dx.p[i] = gp_dx(g, 4 * C, wpk, x[i].F0, R);
     dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
   }
   r.dwgemm(dw, "ffn0_dw");
-  r.ok(mmt_launch_colsum(cs, R, r.s), "ffn0_db");
   r.gemm(dx, true, false, EPI_STORE_F32, 1, "ffn0_dx");
   for (int i = 0; i < M; ++i) {
     lb.p[i].x = r.W<float>(a[i].x1); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].mean = r.W<float>(a[i].mean2);
     lb.p[i].rstd = r.W<float>(a[i].rstd2); lb.p[i].dy = r.W<float>(p.dln[i]); lb.p[i].dx = r.W<float>(p.dres[i]);
     lb.p[i].dx16 = r.W<bf16_t>(p.dres16[i]); lb.p[i].dgamma = grads + x[i].ln2w; lb.p[i].dbeta = grads + x[i].ln2b;
+    r.set_drop(lb.p[i], l, i, DS_SA_PROJ);  // the copy feeds the SA projection backward
+    lb.p[i].dsum = grads + x[i].bp2;
   }
   r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln2_bwd");
   // SA output projection
   for (int i = 0; i < M; ++i) {
     const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
     dw.p[i] = gp_dw(g, C, r.W<bf16_t>(a[i].p1), ldp, grads, x[i].P2, R);
-    colsum_add(r, cs, i, g, C, grads + x[i].bp2, C, nullptr, 1.f);
     dx.p[i] = gp_dx(g, C, wpk, x[i].P2, R);
     dx.p[i].aux = r.W<bf16_t>(a[i].p1); dx.p[i].ldaux = ldp; dx.p[i].o16 = r.W<bf16_t>(p.gp[i]); dx.p[i].ldo16 = ldp;
+    dx.p[i].dbias = grads + x[i].bp0;
   }
   r.dwgemm(dw, "proj2_dw");
-  r.ok(mmt_launch_colsum(cs, R, r.s), "proj2_db");
   r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "proj2_dx");
   for (int i = 0; i < M; ++i) {
     const bf16_t* g = r.W<bf16_t>(p.gp[i]);
     dw.p[i] = gp_dw(g, ldp, r.W<bf16_t>(a[i].o), C, grads, x[i].P0, R);
-    colsum_add(r, cs, i, g, ldp, grads + x[i].bp0, C / 2, nullptr, 1.f);
     dx.p[i] = gp_dx(g, ldp, wpk, x[i].P0, R);
     dx.p[i].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[i].ldo16 = C;
   }
   r.dwgemm(dw, "proj0_dw");
-  r.ok(mmt_launch_colsum(cs, R, r.s), "proj0_db");
   r.gemm(dx, true, false, EPI_STORE_BF16, 1, "proj0_dx");
   AttnBatch ab{}; ab.count = M;
   for (int i = 0; i < M; ++i) {
@@ -815,6 +862,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     q.o = r.W<bf16_t>(a[i].o); q.o_ld = C; q.lse[0] = r.W<float>(a[i].lse); q.nstreams = 1;
     q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dvec[0] = r.W<float>(p.dvec[i][0]);
     q.dq = gq + C; q.dq_ld = 3 * C; q.dk[0] = gq; q.dv[0] = gq + 2 * C; q.dkv_ld = 3 * C; q.dkv_hstride = hs;
+    r.set_drop(q, l, i, DS_SA_PROB);
   }
   r.probe_begin("attn_bwd");
   r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "attn_bwd");
@@ -838,7 +886,8 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   for (int i = 0; i < M; ++i) {
     lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].mean = r.W<float>(a[i].mean1);
     lb.p[i].rstd = r.W<float>(a[i].rstd1); lb.p[i].dy = r.W<float>(p.dln[i]); lb.p[i].dx = r.W<float>(p.dres[i]);
-    lb.p[i].dx16 = r.W<bf16_t>(p.dres16[i]); lb.p[i].dgamma = grads + x[i].ln1w; lb.p[i].dbeta = grads + x[i].ln1b;
+    lb.p[i].dgamma = grads + x[i].ln1w; lb.p[i].dbeta = grads + x[i].ln1b;
+    set_dres16_consumer(c, r, lb.p[i], i, l - 1, grads);
   }
   r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln1_bwd");
   return r.rc;
@@ -940,12 +989,21 @@ int mmt_forward(mmt_ctx* c, void* stream, int32_t batch, const int64_t* const* i
                 const float* params, float* const* logits, float* losses, void* workspace, int32_t training) {
   if (!c) return MMT_ERR_INVALID;
   if (batch < 1 || !idx || !params || !logits || !workspace) return fail(c, MMT_ERR_INVALID, "mmt_forward: null argument");
-  if (training && c->cfg.dropout > 0.f)
-    return fail(c, MMT_ERR_UNSUPPORTED, "dropout > 0 in training mode is not implemented by this build");
   if (c->plan.B != batch) make_plan(c, batch);
   int rc = ensure_device_tables(c);
   if (rc) return rc;
   Runner r{c, (hipStream_t)stream, workspace, params, nullptr, batch, batch * c->T};
+  // dropout (training mode only, as nn.Dropout): one seed per training forward, reused by its backward
+  r.drop = training && c->cfg.dropout > 0.f;
+  if (r.drop) {
+    if (c->next_seed_set) r.seed = c->next_seed;
+    else r.seed = ((uint64_t)mmt_hash((uint32_t)c->cfg.seed, (uint32_t)(c->cfg.seed >> 32), (uint32_t)c->step_counter) << 32) |
+                  mmt_hash((uint32_t)(c->cfg.seed >> 32), (uint32_t)c->cfg.seed, (uint32_t)(c->step_counter >> 32) ^ 0xA5A5A5A5u);
+    c->next_seed_set = false;
+    ++c->step_counter;
+  }
+  c->fwd_drop = r.drop;
+  c->fwd_seed = r.seed;
   c->fwd_ready = false;
   for (int i = 0; i < c->M; ++i) c->last_idx[i] = idx[i];
   rc = run_forward(c, r, idx, tgt, logits, losses);
@@ -977,6 +1035,8 @@ int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* los
   if (!c->fwd_ready) return fail(c, MMT_ERR_STATE, "mmt_backward: no forward with targets to differentiate");
   if (stage < 0 || stage > c->L + 1) return fail(c, MMT_ERR_INVALID, "bad backward stage");
   Runner r{c, (hipStream_t)stream, workspace, params, nullptr, c->plan.B, c->plan.B * c->T};
+  r.drop = c->fwd_drop;
+  r.seed = c->fwd_seed;
   if (stage == c->L + 1) {
     EmbBatch eb{}; eb.count = c->M;
     for (int i = 0; i < c->M; ++i) {
@@ -1021,6 +1081,15 @@ int mmt_eval_direction(mmt_ctx* c, void* stream, int32_t batch, int32_t T, int32
 
 }  // extern "C"
 
+
+// seed of the dropout masks of the next training forward (and its backward); without a call the
+// engine derives one from mmt_config.seed and a per-context counter
+extern "C" int mmt_set_dropout_seed(mmt_ctx* c, uint64_t seed) {
+  if (!c) return MMT_ERR_INVALID;
+  c->next_seed = seed;
+  c->next_seed_set = true;
+  return MMT_OK;
+}
 
 // live per-kernel timing: HIP events around every launch labelled `label` (e.g. "ffn0", "ffn0_dw",
 // "attn_fwd"), on the caller's stream, so bench.py can price one kernel inside the timed region.

@@ -28,7 +28,7 @@
 // bits 0-3 and of the weight-grad (split-K, atomic) GEMMs in bits 4-7:
 //   0 = BK 64 x 2 stages, 1 = BK 32 x 2, 2 = BK 32 x 3, 3 = BK 32 x 4, 4 = BK 64 x 3
 static int g_gemm_variant = 0;      // forward / backward-data
-static int g_gemm_variant_dw = 3;   // weight grad: long K loops want a deeper ring
+static int g_gemm_variant_dw = 0;   // weight grad (split-K atomic)
 extern "C" int mmt_gemm_set_variant(int v) {
   if ((v & 15) > 4 || ((v >> 4) & 15) > 4) return -1;
   g_gemm_variant = v & 15;
@@ -91,59 +91,9 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int sb, int s, int lane)
   }
 }
 
+// one output element; returns the value stored (the bias-gradient column sum adds it up)
 template <int EPI>
-__device__ __forceinline__ void epi_vec4(const GemmProblem& P, float alpha, int m, int n, const float (&v)[4]) {
-  // n..n+3 all < N (checked by caller), m < M
-  const int64_t o = (int64_t)m * P.ldc + n;
-  float r[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) r[e] = alpha * v[e];
-  if (EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
-      EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16) {
-    if (P.bias) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(P.bias + n);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) r[e] += b[e];
-    }
-  }
-  if (EPI == EPI_BIAS_TANH_BF16) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[e] = tanhf(r[e]);
-  }
-  if (EPI == EPI_BIAS_RELU_BF16) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[e] = fmaxf(r[e], 0.0f);
-  }
-  if (EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16) {
-    const u32x2 a = *reinterpret_cast<const u32x2*>(P.aux + (int64_t)m * P.ldaux + n);
-    const float t[4] = {bf2f(a[0] & 0xffff), bf2f(a[0] >> 16), bf2f(a[1] & 0xffff), bf2f(a[1] >> 16)};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[e] = (EPI == EPI_DTANH_BF16) ? r[e] * (1.0f - t[e] * t[e]) : (t[e] > 0.0f ? r[e] : 0.0f);
-  }
-  if (EPI == EPI_BIAS_RESID_F32) {
-    const f32x4 x = *reinterpret_cast<const f32x4*>(P.resid + (int64_t)m * P.ldres + n);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[e] += x[e];
-  }
-  if (EPI == EPI_ACC_F32) {
-    f32x4* dst = reinterpret_cast<f32x4*>(P.o32 + o);
-    f32x4 x = *dst;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) x[e] += r[e];
-    *dst = x;
-    return;
-  }
-  if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32) {
-    *reinterpret_cast<f32x4*>(P.o32 + o) = f32x4{r[0], r[1], r[2], r[3]};
-    if (EPI == EPI_BIAS_RESID_F32 && P.o16)
-      *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
-    return;
-  }
-  *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
-}
-
-template <int EPI>
-__device__ __forceinline__ void epi_scalar(const GemmProblem& P, float alpha, int m, int n, float v) {
+__device__ __forceinline__ float epi_scalar(const GemmProblem& P, float alpha, int m, int n, float v) {
   float r = alpha * v;
   if (EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
       EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16) {
@@ -153,16 +103,20 @@ __device__ __forceinline__ void epi_scalar(const GemmProblem& P, float alpha, in
   if (EPI == EPI_BIAS_RELU_BF16) r = fmaxf(r, 0.0f);
   if (EPI == EPI_DTANH_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r *= (1.0f - t * t); }
   if (EPI == EPI_DRELU_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r = t > 0.0f ? r : 0.0f; }
-  if (EPI == EPI_BIAS_RESID_F32) r += P.resid[(int64_t)m * P.ldres + n];
+  if (EPI == EPI_BIAS_RESID_F32) {
+    if (P.drop_thr) r = (mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)n) >= P.drop_thr) ? r * P.drop_scale : 0.0f;
+    r += P.resid[(int64_t)m * P.ldres + n];
+  }
   const int64_t o = (int64_t)m * P.ldc + n;
-  if (EPI == EPI_ACC_F32) { P.o32[o] += r; return; }
-  if (EPI == EPI_ATOMIC_F32) { atomicAdd(P.o32 + o, r); return; }
+  if (EPI == EPI_ACC_F32) { P.o32[o] += r; return r; }
+  if (EPI == EPI_ATOMIC_F32) { atomicAdd(P.o32 + o, r); return r; }
   if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32) {
     P.o32[o] = r;
     if (EPI == EPI_BIAS_RESID_F32 && P.o16) P.o16[(int64_t)m * P.ldo16 + n] = f2bf(r);
-    return;
+    return r;
   }
   P.o16[(int64_t)m * P.ldo16 + n] = f2bf(r);
+  return r;
 }
 
 // bf16 outputs feed later GEMMs as K-contiguous operands: their pad columns [N, ldo16) are kept
@@ -308,6 +262,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
     constexpr bool HAS_AUX = EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
     constexpr bool HAS_RES = EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32;
     constexpr int IT = GBM / 8;
+    // fused bias gradient (bf16-output epilogues): column sums of the stored values
+    constexpr bool CAN_DB = EPI == EPI_STORE_BF16 || EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
+    const bool want_db = CAN_DB && P.dbias != nullptr;
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
     if (n + 4 <= N && vec_ok) {
       // fast path: issue every operand load of this thread's 16 rows first (memory-level
       // parallelism), then combine and store; full 4-column groups only
@@ -350,6 +308,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
           for (int e = 0; e < 4; ++e)
             r[e] = (EPI == EPI_DTANH_BF16) ? r[e] * (1.0f - t[e] * t[e]) : (t[e] > 0.0f ? r[e] : 0.0f);
         }
+        if (EPI == EPI_BIAS_RESID_F32 && P.drop_thr) {  // dropout on the branch output, then residual add
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            r[e] = (mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n + e)) >= P.drop_thr) ? r[e] * P.drop_scale : 0.0f;
+        }
         if (HAS_RES) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) r[e] += resv[it][e];
@@ -360,6 +323,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
             *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
         } else {
           *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
+          if (CAN_DB) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cs[e] += r[e];
+          }
         }
       }
     } else if (n < N + 4) {
@@ -371,10 +338,22 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
         const f32x4 v4 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 4 * c4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if (n + e < N) epi_scalar<EPI>(P, alpha, m, n + e, v4[e]);
+          if (n + e < N) cs[e] += epi_scalar<EPI>(P, alpha, m, n + e, v4[e]);
           else epi_pad<EPI>(P, m, n + e);
         }
       }
+    }
+    if (want_db) {
+      // rows of a column live in lanes l, l^32 of every wave: fold those, then the 4 waves via
+      // LDS (the staged tile is dead: every thread has read its own rows), one atomic per column
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], 32, 64);
+      __syncthreads();
+      float* red = ct;  // [4 waves][128 columns]
+      if (lane < 32) *reinterpret_cast<f32x4*>(red + wave * GBN + 4 * c4) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      __syncthreads();
+      if (tid < GBN && n0 + tid < N)
+        atomicAdd(P.dbias + n0 + tid, red[tid] + red[GBN + tid] + red[2 * GBN + tid] + red[3 * GBN + tid]);
     }
   } else {
     // acc[i][j]: rows = m (sub-tile i), cols = n (sub-tile j)

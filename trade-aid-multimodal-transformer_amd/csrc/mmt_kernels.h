@@ -20,7 +20,7 @@ enum MmtEpi {
   EPI_STORE_BF16 = 0,   // o16 = alpha*acc (+bias)
   EPI_BIAS_TANH_BF16,   // o16 = tanh(alpha*acc + bias)
   EPI_BIAS_RELU_BF16,   // o16 = relu(alpha*acc + bias)
-  EPI_BIAS_RESID_F32,   // o32 = resid + alpha*acc + bias ; o16 (optional) = bf16 copy
+  EPI_BIAS_RESID_F32,   // o32 = resid + drop(alpha*acc + bias) ; o16 (optional) = bf16 copy
   EPI_STORE_F32,        // o32 = alpha*acc (+bias)
   EPI_DTANH_BF16,       // o16 = alpha*acc * (1 - aux^2)
   EPI_DRELU_BF16,       // o16 = aux > 0 ? alpha*acc : 0
@@ -41,6 +41,12 @@ struct GemmProblem {
   float alpha;
   int M, N, K;
   int lda, ldb, ldc, ldaux, ldres, ldo16;
+  // dropout of the branch output (EPI_BIAS_RESID_F32 only; drop_thr == 0: off):
+  // element (m, n) kept iff mmt_hash(drop_key, m, n) >= drop_thr, kept values scaled by drop_scale
+  uint32_t drop_key, drop_thr;
+  float drop_scale;
+  // fused bias gradient (bf16-output epilogues, SWAP layouts): dbias[n] += sum_m out[m, n]
+  float* dbias;
 };
 
 struct GemmBatch {
@@ -66,6 +72,11 @@ struct LnProblem {
   bf16_t* dx16;         // optional bf16 copy of the accumulated dx
   float* dgamma;        // atomic accumulate
   float* dbeta;
+  // dropout mask applied to the dx16 copy only (the gradient of the dropped branch that consumes
+  // it): dx16[r, c] = keep(r, c) ? dx * drop_scale : 0 ; drop_thr == 0: plain copy
+  uint32_t drop_key, drop_thr;
+  float drop_scale;
+  float* dsum;          // optional: dsum[c] += sum_r (masked) dx16 value (the consumer's bias gradient)
 };
 struct LnBatch { LnProblem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_ln_fwd(const LnBatch& b, int R, int C, hipStream_t s);
@@ -93,6 +104,11 @@ struct AttnProblem {
   bf16_t* dv[MMT_MAX_STREAMS];
   int dkv_ld, dkv_hstride;
   int nstreams;
+  // dropout on the normalised probabilities (drop_thr == 0: off): element (query t, key s) of
+  // stream j, head slot bh = b*H + h, kept iff mmt_hash(mmt_hash(drop_key, j, MMT_STREAM_SALT),
+  // bh*T + t, s) >= drop_thr; kept probabilities scaled by drop_scale
+  uint32_t drop_key, drop_thr;
+  float drop_scale;
 };
 struct AttnBatch { AttnProblem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
@@ -158,6 +174,16 @@ struct PackSeg { int64_t src_off; int64_t dst_off; int rows; int cols; int dld; 
 hipError_t mmt_launch_pack(const PackSeg* segs_dev, int nseg, int64_t ntasks, const int* task_dev, const float* src,
                            bf16_t* dst, hipStream_t s);
 hipError_t mmt_launch_f32_to_bf16(const float* src, bf16_t* dst, int64_t n, hipStream_t s);
+// dst = bf16(mask * src) over row-major [R, C] (mask as in LnProblem), dsum[c] += column sums
+struct DropCopyProblem {
+  const float* src;
+  bf16_t* dst;
+  float* dsum;  // nullable
+  uint32_t drop_key, drop_thr;
+  float drop_scale;
+};
+struct DropCopyBatch { DropCopyProblem p[MMT_MAX_GROUP]; int count; };
+hipError_t mmt_launch_drop_copy(const DropCopyBatch& b, int R, int C, hipStream_t s);
 
 hipError_t mmt_launch_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                             float eps, float wd, float bc1, float bc2_sqrt, hipStream_t s);

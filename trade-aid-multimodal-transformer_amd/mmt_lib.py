@@ -63,6 +63,7 @@ _SIGS = {
     "mmt_backward_stage": (c_i32, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mmt_adamw_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32]),
     "mmt_eval_direction": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "mmt_set_dropout_seed": (c_i32, [c_vp, ctypes.c_uint64]),
     "mmt_probe_set": (c_i32, [c_vp, c_cp]),
     "mmt_probe_read": (c_i32, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
     "mmt_batch_jitter":(c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64]),

@@ -206,6 +206,11 @@ class MultimodalTransformer(nn.Module):
         losses = torch.empty(self.num_modalities, dtype=torch.float32, device=dev) if tgt is not None else None
         idx_arr = ML.ptr_array(idx)
         tgt_arr = ML.ptr_array(tgt) if tgt is not None else None
+        if training:
+            # dropout masks of this step: a counter hash keyed by a seed drawn from torch's
+            # default generator (so torch.manual_seed makes runs repeatable, as with nn.Dropout)
+            self.last_dropout_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            ML.check(L.mmt_set_dropout_seed(self._ctx, self.last_dropout_seed), self._ctx, "mmt_set_dropout_seed")
         rc = L.mmt_forward(self._ctx, ML.stream_ptr(dev), B, idx_arr, tgt_arr, ML.ptr(flat), ML.ptr_array(logits),
                            ML.ptr(losses), ML.ptr(ws), 1 if training else 0)
         ML.check(rc, self._ctx, "mmt_forward")
