@@ -194,7 +194,10 @@ def _attn_ref(q, ks, vs, scale):
 
 
 @pytest.mark.parametrize("B,T,H,hs,ns", [(2, 64, 2, 32, 1), (3, 37, 4, 16, 1), (2, 4, 4, 8, 1), (2, 100, 2, 64, 1),
-                                         (2, 64, 2, 32, 3), (1, 45, 3, 16, 2), (2, 256, 8, 32, 1), (1, 96, 2, 48, 2)])
+                                         (2, 64, 2, 32, 3), (1, 45, 3, 16, 2), (2, 256, 8, 32, 1), (1, 96, 2, 48, 2),
+                                         # longer than one LDS chunk (256 rows at hs <= 32, 128 above)
+                                         (1, 300, 2, 32, 1), (1, 300, 2, 32, 3), (1, 520, 2, 64, 2),
+                                         (1, 1024, 1, 64, 1), (1, 257, 1, 24, 1)])
 def test_attention_fwd_bwd(B, T, H, hs, ns):
     torch.manual_seed(B * 1000 + T * 10 + hs + ns)
     C = H * hs

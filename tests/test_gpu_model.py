@@ -101,8 +101,11 @@ def test_dropout_step_matches_oracle_masks(name, p):
     got = torch.stack([l.detach().cpu() for l in losses])
     ref = torch.stack(r_losses)
     assert torch.allclose(got, ref, rtol=5e-3, atol=5e-3), (got, ref)
-    # the masks really act: the dropped loss differs from the eval-mode (golden) loss
-    assert (got - torch.from_numpy(z["losses"])).abs().max().item() > 1e-3
+    # the masks really act: the step lands far closer to the hash-masked oracle than to the
+    # dropout-free one (a loss comparison is too weak at init scale on the tiny fixtures)
+    cfg.dropout = 0.0
+    _, _, n_grads = O.forward_backward(sd, cfg, idx, tgt)
+    cfg.dropout = p
     for i in range(cfg.M):
         assert rel(logits[i], r_logits[i]) < 2e-2, i
     names = [n for n, _ in m.named_reference_tensors()]
@@ -112,6 +115,9 @@ def test_dropout_step_matches_oracle_masks(name, p):
             allg.append(g.flatten().cpu())
             allr.append(r_grads[k].flatten())
     assert rel(torch.cat(allg), torch.cat(allr)) < 3e-2
+    alln = torch.cat([n_grads[k].flatten() for k, g in zip(names, _grad_views(m))
+                      if r_grads.get(k) is not None and g.numel()])
+    assert rel(torch.cat(allg), alln) > 3 * max(rel(torch.cat(allg), torch.cat(allr)), 1e-2)
     # eval mode: no dropout, the golden (reference) logits again
     m.eval()
     with torch.no_grad():

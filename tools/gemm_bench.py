@@ -28,7 +28,24 @@ SHAPES = [
     ("ffn_dw_s32", 0, 0, "atomic_f32", 1024, 256, R, 32),
     ("ffn_dw_s16", 0, 0, "atomic_f32", 1024, 256, R, 16),
     ("qkv1_dw_s32", 0, 0, "atomic_f32", 384, 256, R, 32),
+    # per-modality weight grads (K = B*T = 16384), the engine groups 4 of these per launch
+    ("ffn_dw16k_s8", 0, 0, "atomic_f32", 1024, 256, 16384, 8),
+    ("ffn_dw16k_s16", 0, 0, "atomic_f32", 1024, 256, 16384, 16),
+    ("ffn_dw16k_s32", 0, 0, "atomic_f32", 1024, 256, 16384, 32),
+    ("proj_dw16k_s8", 0, 0, "atomic_f32", 128, 256, 16384, 8),
+    ("proj_dw16k_s32", 0, 0, "atomic_f32", 128, 256, 16384, 32),
+    ("proj_dw16k_s64", 0, 0, "atomic_f32", 128, 256, 16384, 64),
+    ("ca_dw16k_s8", 0, 0, "atomic_f32", 256, 256, 16384, 8),
+    ("ca_dw16k_s32", 0, 0, "atomic_f32", 256, 256, 16384, 32),
+    ("ca_dw16k_s64", 0, 0, "atomic_f32", 256, 256, 16384, 64),
+    # main-loop rate without atomics: one block per output tile over the whole K
+    ("ffn_dw16k_s1_store", 0, 0, "store_f32", 1024, 256, 16384, 1),
+    ("ffn_dw16k_s1_atomic", 0, 0, "atomic_f32", 1024, 256, 16384, 1),
+    ("ffn_dw2k_s1_store", 0, 0, "store_f32", 1024, 256, 2048, 1),
+    ("ffn_dw2k_s1_atomic", 0, 0, "atomic_f32", 1024, 256, 2048, 1),
 ]
+if os.environ.get("GEMM_BENCH_ONLY"):
+    SHAPES = [s for s in SHAPES if any(k in s[0] for k in os.environ["GEMM_BENCH_ONLY"].split(","))]
 
 
 def r8(x):

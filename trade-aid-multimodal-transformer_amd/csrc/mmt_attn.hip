@@ -4,10 +4,10 @@
 // softmax, @ v. Cross-attention runs one independent causal softmax per KV modality ("stream")
 // and SUMS the per-stream outputs (no joint softmax).
 //
-// Structure: a 256-thread workgroup (4 waves) owns a 128-row block of one (batch, head); each
-// wave owns one 32-row tile. The operand tiles the waves share (K/V in the forward and dQ pass,
-// Q/dO/LSE/D in the dK/dV pass) are staged once per workgroup into double-buffered LDS, the next
-// tile's global loads in flight while the current tile computes; one barrier per tile.
+// Structure: a 256-thread workgroup (4 waves) owns 8 32-row tiles of one (batch, head) (wave w
+// takes tiles w and 7-w: balanced causal work). The operand the tiles share (K/V in the forward
+// and dQ pass, Q/dO/LSE/D in the dK/dV pass) is staged into LDS in chunks of up to 256 rows; at
+// T <= chunk the whole sequence lands with one barrier (see "Chunked staging" below).
 // All products are v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
 //   forward  S^T = K Q^T (keys on accumulator rows, queries on lanes) -> online softmax per lane;
 //            O^T += V^T P^T with P^T straight from the accumulator registers as the B operand and
@@ -78,165 +78,265 @@ __device__ __forceinline__ void zero16(f32x16& a) {
 }  // namespace
 
 // =============================================================================================
-// forward: grid (ceil(T/128), B*H, G); wave w owns query tile 4*blockIdx.x + w
+// Chunked staging. A workgroup (4 waves) owns 8 consecutive 32-row tiles of one (batch, head);
+// wave w takes tiles w and 7-w, so the causal work of the 4 waves is balanced. The operand the
+// tiles share (K/V in the forward and dQ pass, Q/dO in the dK/dV pass) is staged into LDS in
+// chunks of ROWS rows (32 KiB of bf16 per operand pair): at T <= ROWS the whole sequence lands with
+// one barrier and the waves then run barrier-free; longer sequences reload between chunks (the
+// other resident workgroups of the CU cover that latency; a register prefetch would cost the
+// occupancy it buys). Softmax runs in the log2 domain (scale * log2(e) folded into
+// one multiply, exp2 on v_exp_f32); only tiles on the causal diagonal (and a ragged last query
+// tile) evaluate the mask.
+// =============================================================================================
+template <int HS>
+struct Chunk {
+  static constexpr int ROWS = (HS <= 32) ? 256 : 128;
+  static constexpr int HALF = ROWS * Geo<HS>::CH;  // 16-B pieces of one operand
+  static constexpr int NSTG = 2 * HALF / 256;      // pieces per thread (two operands)
+};
+
+template <int HS>
+struct Stager {
+  u32x4 v[Chunk<HS>::NSTG];
+  // rows [r0, r0 + ROWS) of operands a, b (columns 0..HS-1); rows >= T read as zeros
+  __device__ __forceinline__ void load(const bf16_t* a, int lda, const bf16_t* b, int ldb, int64_t rowbase, int r0,
+                                       int T, int tid) {
+    constexpr int CH = Geo<HS>::CH, HALF = Chunk<HS>::HALF;
+#pragma unroll
+    for (int u = 0; u < Chunk<HS>::NSTG; ++u) {
+      const int c = tid + 256 * u;
+      const bool isb = c >= HALF;
+      const int cc = isb ? c - HALF : c;
+      v[u] = tile_chunk(isb ? b : a, rowbase, r0, cc / CH, (cc % CH) * 8, T, isb ? ldb : lda);
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* la, int sa, bf16_t* lb, int sb, int tid) const {
+    constexpr int CH = Geo<HS>::CH, HALF = Chunk<HS>::HALF;
+#pragma unroll
+    for (int u = 0; u < Chunk<HS>::NSTG; ++u) {
+      const int c = tid + 256 * u;
+      const bool isb = c >= HALF;
+      const int cc = isb ? c - HALF : c;
+      const int row = cc / CH, col = (cc % CH) * 8;
+      *reinterpret_cast<u32x4*>(isb ? lb + row * sb + col : la + row * sa + col) = v[u];
+    }
+  }
+};
+
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// forward: one 32x32 (keys x queries) tile of S^T, online softmax, O^T += V^T P^T
+template <int HS>
+__device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq, bool diag,
+                                         const bf16x8 (&qf)[Geo<HS>::NKS], float& m, float& l,
+                                         f32x16 (&oacc)[Geo<HS>::ND], float c2, const AttnProblem& P, uint32_t dkey,
+                                         uint32_t drow, int lane) {
+  using G = Geo<HS>;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 sacc;
+  zero16(sacc);
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s) {
+    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
+    sacc = mfma32(kf, qf[s], sacc);
+  }
+  float tmax = -INFINITY;
+  if (diag) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const float sv = (key <= tq) ? sacc[e] * c2 : -INFINITY;
+      sacc[e] = sv;
+      tmax = fmaxf(tmax, sv);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      sacc[e] *= c2;
+      tmax = fmaxf(tmax, sacc[e]);
+    }
+  }
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+  const float mnew = fmaxf(m, tmax);  // finite: key 0 of tile 0 is valid for every query
+  const float alpha = ex2(m - mnew);
+  float rs = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const float pv = ex2(sacc[e] - mnew);
+    sacc[e] = pv;
+    rs += pv;
+  }
+  rs += __shfl_xor(rs, 32, 64);
+  l = l * alpha + rs;
+  m = mnew;
+  if (P.drop_thr) {  // dropout on the probabilities (the normaliser l keeps every term)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t key = (uint32_t)(k0 + (e & 3) + 8 * (e >> 2) + 4 * h);
+      sacc[e] = (mmt_hash(dkey, drow, key) >= P.drop_thr) ? sacc[e] * P.drop_scale : 0.f;
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 pf = acc_frag(sacc, s);
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) oacc[dt] = mfma32(tr_frag(vs + kl * G::TW, G::TW, dt, s, lane), pf, oacc[dt]);
+  }
+}
+
+// Block-uniform walk over (tile u, stream j, chunk c): the chunk (j, c) resident in LDS is reused
+// while consecutive steps share it (T <= ROWS with one stream: a single load for the whole block).
+struct ChunkWalk {
+  int ns, nch;
+  __device__ __forceinline__ bool next(int u, int j, int c, int& nj, int& nc) const {
+    nj = j; nc = c + 1;
+    int nu = u;
+    if (nc == nch) { nc = 0; ++nj; if (nj == ns) { nj = 0; ++nu; } }
+    return nu < 2 && (nj != j || nc != c);
+  }
+};
+
+// =============================================================================================
+// forward: grid (ceil(nt/8), B*H, G)
 // =============================================================================================
 template <int HS>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
+  constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
   const int bh = blockIdx.y, b = bh / H, head = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int nt = (T + 31) / 32;
-  const int qt = blockIdx.x * 4 + w;
-  const int last_kt = min(blockIdx.x * 4 + 3, nt - 1);
-  const int q0 = qt * 32, tq = q0 + r;
+  const int qt0 = blockIdx.x * 8;
+  const int qmax = min(qt0 + 7, nt - 1);
+  const ChunkWalk walk{P.nstreams, (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS};
   const int64_t rowbase = (int64_t)b * T;
-  __shared__ __attribute__((aligned(16))) bf16_t ks[2][32 * G::RW];
-  __shared__ __attribute__((aligned(16))) bf16_t vs[2][32 * G::TW];
+  const float c2 = scale * kLog2e;
+  __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];
+  __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::TW];
+  for (int q = tid; q < ROWS * G::RW; q += 256) if (q % G::RW >= HS) ks[q] = 0;
+  for (int q = tid; q < ROWS * G::TW; q += 256) if (q % G::TW >= HS) vs[q] = 0;
+  Stager<HS> st;
+  st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
+  st.store(ks, G::RW, vs, G::TW, tid);
+  __syncthreads();
 
-  bf16x8 qf[G::NKS];
+#pragma unroll 1
+  for (int u = 0; u < 2; ++u) {
+    const int qt = u == 0 ? qt0 + w : qt0 + 7 - w;
+    const bool live = qt < nt;
+    const int tq = qt * 32 + r;
+    const uint32_t drow = (uint32_t)(bh * T + tq);
+    bf16x8 qf[G::NKS];
+    f32x16 otot[G::ND];
+#pragma unroll
+    for (int s = 0; s < G::NKS; ++s) {
+      const int d0 = 16 * s + 8 * h;
+      qf[s] = ld8(P.q + (rowbase + tq) * P.q_ld + head * HS + d0, live && tq < T && d0 < HS);
+    }
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) zero16(otot[dt]);
+    for (int j = 0; j < P.nstreams; ++j) {
+      const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+      float m = -INFINITY, l = 0.f;
+      f32x16 oacc[G::ND];
+#pragma unroll
+      for (int dt = 0; dt < G::ND; ++dt) zero16(oacc[dt]);
+      for (int c = 0; c < walk.nch; ++c) {
+        int nj, nc;
+        const bool reload = walk.next(u, j, c, nj, nc);
+        if (live) {
+          const int kt_lo = c * (ROWS / 32);
+          const int last = min(qt, min(kt_lo + ROWS / 32, nt) - 1);
+          #pragma unroll 1
+          for (int kt = kt_lo; kt <= last; ++kt)
+            fwd_tile<HS>(ks, vs, (kt - kt_lo) * 32, kt * 32, tq, kt == qt, qf, m, l, oacc, c2, P, dkey, drow, lane);
+        }
+        if (reload) {
+          __syncthreads();
+          st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
+                  T, tid);
+          st.store(ks, G::RW, vs, G::TW, tid);
+          __syncthreads();
+        }
+      }
+      const float inv = (l > 0.f) ? 1.f / l : 0.f;
+#pragma unroll
+      for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          oacc[dt][e] *= inv;
+          otot[dt][e] += oacc[dt][e];
+        }
+      if (live && tq < T) {
+        if (h == 0) P.lse[j][(int64_t)bh * T + tq] = (m + __log2f(l)) * kLn2;
+        if (P.nstreams > 1 && P.oj[j]) {
+#pragma unroll
+          for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int d0 = dt * 32 + 8 * g + 4 * h;
+              if (d0 < HS)
+                *reinterpret_cast<u32x2*>(P.oj[j] + (rowbase + tq) * P.o_ld + head * HS + d0) =
+                    u32x2{pack2bf(oacc[dt][4 * g], oacc[dt][4 * g + 1]), pack2bf(oacc[dt][4 * g + 2], oacc[dt][4 * g + 3])};
+            }
+        }
+      }
+    }
+    if (live && tq < T) {
+#pragma unroll
+      for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = dt * 32 + 8 * g + 4 * h;
+          if (d0 < HS)
+            *reinterpret_cast<u32x2*>(P.o + (rowbase + tq) * P.o_ld + head * HS + d0) =
+                u32x2{pack2bf(otot[dt][4 * g], otot[dt][4 * g + 1]), pack2bf(otot[dt][4 * g + 2], otot[dt][4 * g + 3])};
+        }
+    }
+  }
+}
+
+// dQ: one 32x32 tile; S^T, dP^T recomputed, dQ^T += K^T dS^T
+template <int HS>
+__device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq, bool diag,
+                                        const bf16x8 (&qf)[Geo<HS>::NKS], const bf16x8 (&dof)[Geo<HS>::NKS],
+                                        float lse2, float dsum, f32x16 (&dq)[Geo<HS>::ND], float c2,
+                                        const AttnProblem& P, uint32_t dkey, uint32_t drow, int lane) {
+  using G = Geo<HS>;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 sacc, dpacc;
+  zero16(sacc);
+  zero16(dpacc);
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
-    const int d0 = 16 * s + 8 * h;
-    qf[s] = ld8(P.q + (rowbase + tq) * P.q_ld + head * HS + d0, tq < T && d0 < HS);
+    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
+    const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vs + (kl + r) * G::RW + 16 * s + 8 * h);
+    sacc = mfma32(kf, qf[s], sacc);
+    dpacc = mfma32(vf, dof[s], dpacc);
   }
-  // zero the pad columns of both buffers once (never written by staging)
-  for (int q = tid; q < 2 * 32 * G::RW; q += 256) { const int c = q % G::RW; if (c >= HS) (&ks[0][0])[q] = 0; }
-  for (int q = tid; q < 2 * 32 * G::TW; q += 256) { const int c = q % G::TW; if (c >= HS) (&vs[0][0])[q] = 0; }
-
-  f32x16 otot[G::ND];
 #pragma unroll
-  for (int dt = 0; dt < G::ND; ++dt) zero16(otot[dt]);
-
-  const uint32_t drow = (uint32_t)(bh * T + tq);  // dropout hash row of this lane's query
-  for (int j = 0; j < P.nstreams; ++j) {
-    const bf16_t* kp = P.k[j] + head * P.kv_hstride;
-    const bf16_t* vp = P.v[j] + head * P.kv_hstride;
-    const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
-    float m = -INFINITY, l = 0.f;
-    f32x16 oacc[G::ND];
-#pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt) zero16(oacc[dt]);
-    // staging: chunk c < 32*CH -> K, else V
-    u32x4 stg[2];
-    auto issue = [&](int kt) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int c = tid + 256 * u;
-        if (c < 64 * G::CH) {
-          const bool isv = c >= 32 * G::CH;
-          const int cc = isv ? c - 32 * G::CH : c;
-          stg[u] = tile_chunk(isv ? vp : kp, rowbase, kt * 32, cc / G::CH, (cc % G::CH) * 8, T, P.kv_ld);
-        }
-      }
-    };
-    auto commit = [&](int buf) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int c = tid + 256 * u;
-        if (c < 64 * G::CH) {
-          const bool isv = c >= 32 * G::CH;
-          const int cc = isv ? c - 32 * G::CH : c;
-          const int row = cc / G::CH, col = (cc % G::CH) * 8;
-          if (isv) *reinterpret_cast<u32x4*>(&vs[buf][row * G::TW + col]) = stg[u];
-          else *reinterpret_cast<u32x4*>(&ks[buf][row * G::RW + col]) = stg[u];
-        }
-      }
-    };
-    __syncthreads();  // previous stream's readers are done with both buffers
-    issue(0);
-    commit(0);
-    __syncthreads();
-    for (int kt = 0; kt <= last_kt; ++kt) {
-      const int cur = kt & 1;
-      const bool more = kt + 1 <= last_kt;
-      if (more) issue(kt + 1);
-      if (kt <= qt) {
-        const int k0 = kt * 32;
-        f32x16 sacc;
-        zero16(sacc);
-#pragma unroll
-        for (int s = 0; s < G::NKS; ++s) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&ks[cur][r * G::RW + 16 * s + 8 * h]);
-          sacc = mfma32(kf, qf[s], sacc);
-        }
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          const float sv = (key <= tq && key < T) ? sacc[e] * scale : -INFINITY;
-          sacc[e] = sv;
-          tmax = fmaxf(tmax, sv);
-        }
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float mnew = fmaxf(m, tmax);
-        const float msafe = (mnew == -INFINITY) ? 0.f : mnew;
-        const float alpha = __expf(m - msafe);
-        float rs = 0.f;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float pv = __expf(sacc[e] - msafe);
-          sacc[e] = pv;
-          rs += pv;
-        }
-        rs += __shfl_xor(rs, 32, 64);
-        l = l * alpha + rs;
-        m = mnew;
-        if (P.drop_thr) {  // dropout on the probabilities (the normaliser l keeps every term)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const uint32_t key = (uint32_t)(k0 + (e & 3) + 8 * (e >> 2) + 4 * h);
-            sacc[e] = (mmt_hash(dkey, drow, key) >= P.drop_thr) ? sacc[e] * P.drop_scale : 0.f;
-          }
-        }
-#pragma unroll
-        for (int dt = 0; dt < G::ND; ++dt)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8 pf = acc_frag(sacc, s);
-#pragma unroll
-          for (int dt = 0; dt < G::ND; ++dt) oacc[dt] = mfma32(tr_frag(vs[cur], G::TW, dt, s, lane), pf, oacc[dt]);
-        }
-      }
-      if (more) commit(cur ^ 1);
-      __syncthreads();
-    }
-    const float inv = (l > 0.f) ? 1.f / l : 0.f;
-#pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        oacc[dt][e] *= inv;
-        otot[dt][e] += oacc[dt][e];
-      }
-    if (tq < T) {
-      if (h == 0) P.lse[j][(int64_t)bh * T + tq] = m + __logf(l);
-      if (P.nstreams > 1 && P.oj[j]) {
-#pragma unroll
-        for (int dt = 0; dt < G::ND; ++dt)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int d0 = dt * 32 + 8 * g + 4 * h;
-            if (d0 < HS)
-              *reinterpret_cast<u32x2*>(P.oj[j] + (rowbase + tq) * P.o_ld + head * HS + d0) =
-                  u32x2{pack2bf(oacc[dt][4 * g], oacc[dt][4 * g + 1]), pack2bf(oacc[dt][4 * g + 2], oacc[dt][4 * g + 3])};
-          }
-      }
-    }
+  for (int e = 0; e < 16; ++e) {
+    const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    float pv = ex2(sacc[e] * c2 - lse2);
+    if (diag && key > tq) pv = 0.f;
+    float dp = dpacc[e];
+    if (P.drop_thr) dp = (mmt_hash(dkey, drow, (uint32_t)key) >= P.drop_thr) ? dp * P.drop_scale : 0.f;
+    sacc[e] = pv * (dp - dsum);  // dS^T
   }
-  if (tq < T) {
 #pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt)
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 df = acc_frag(sacc, s);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d0 = dt * 32 + 8 * g + 4 * h;
-        if (d0 < HS)
-          *reinterpret_cast<u32x2*>(P.o + (rowbase + tq) * P.o_ld + head * HS + d0) =
-              u32x2{pack2bf(otot[dt][4 * g], otot[dt][4 * g + 1]), pack2bf(otot[dt][4 * g + 2], otot[dt][4 * g + 3])};
-      }
+    for (int dt = 0; dt < G::ND; ++dt) dq[dt] = mfma32(tr_frag(ks + kl * G::RW, G::RW, dt, s, lane), df, dq[dt]);
   }
 }
 
@@ -246,275 +346,253 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, i
 template <int HS>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
+  constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
   const int bh = blockIdx.y, b = bh / H, head = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int nt = (T + 31) / 32;
-  const int qt = blockIdx.x * 4 + w;
-  const int last_kt = min(blockIdx.x * 4 + 3, nt - 1);
-  const int q0 = qt * 32, tq = q0 + r;
-  const bool qok = tq < T;
+  const int qt0 = blockIdx.x * 8;
+  const int qmax = min(qt0 + 7, nt - 1);
+  const ChunkWalk walk{P.nstreams, (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS};
   const int64_t rowbase = (int64_t)b * T;
-  __shared__ __attribute__((aligned(16))) bf16_t ks[2][32 * G::RW];  // K tile: row reads + tr reads
-  __shared__ __attribute__((aligned(16))) bf16_t vs[2][32 * G::RW];  // V tile: row reads
+  const float c2 = scale * kLog2e;
+  __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row + tr reads
+  __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::RW];  // V chunk: row reads
+  for (int q = tid; q < ROWS * G::RW; q += 256)
+    if (q % G::RW >= HS) { ks[q] = 0; vs[q] = 0; }
+  Stager<HS> st;
+  st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
+  st.store(ks, G::RW, vs, G::RW, tid);
+  __syncthreads();
 
-  bf16x8 qf[G::NKS], dof[G::NKS];
-#pragma unroll
-  for (int s = 0; s < G::NKS; ++s) {
-    const int d0 = 16 * s + 8 * h;
-    const bool ok = qok && d0 < HS;
-    qf[s] = ld8(P.q + (rowbase + tq) * P.q_ld + head * HS + d0, ok);
-    dof[s] = ld8(P.dout + (rowbase + tq) * P.dout_ld + head * HS + d0, ok);
-  }
-  for (int q = tid; q < 2 * 32 * G::RW; q += 256) {
-    const int c = q % G::RW;
-    if (c >= HS) { (&ks[0][0])[q] = 0; (&vs[0][0])[q] = 0; }
-  }
-  f32x16 dq[G::ND];
-#pragma unroll
-  for (int dt = 0; dt < G::ND; ++dt) zero16(dq[dt]);
-
-  for (int j = 0; j < P.nstreams; ++j) {
-    const bf16_t* oj = (P.nstreams > 1) ? P.oj[j] : P.o;
-    float dsum = 0.f;
+#pragma unroll 1
+  for (int u = 0; u < 2; ++u) {
+    const int qt = u == 0 ? qt0 + w : qt0 + 7 - w;
+    const bool live = qt < nt;
+    const int tq = qt * 32 + r;
+    const bool qok = live && tq < T;
+    const uint32_t drow = (uint32_t)(bh * T + tq);
+    bf16x8 qf[G::NKS], dof[G::NKS];
+    f32x16 dq[G::ND];
 #pragma unroll
     for (int s = 0; s < G::NKS; ++s) {
       const int d0 = 16 * s + 8 * h;
-      const bf16x8 ov = ld8(oj + (rowbase + tq) * P.o_ld + head * HS + d0, qok && d0 < HS);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dsum += (float)ov[e] * (float)dof[s][e];
+      qf[s] = ld8(P.q + (rowbase + tq) * P.q_ld + head * HS + d0, qok && d0 < HS);
+      dof[s] = ld8(P.dout + (rowbase + tq) * P.dout_ld + head * HS + d0, qok && d0 < HS);
     }
-    dsum += __shfl_xor(dsum, 32, 64);
-    if (qok && h == 0) P.dvec[j][(int64_t)bh * T + tq] = dsum;
-    const float lse = qok ? P.lse[j][(int64_t)bh * T + tq] : 0.f;
-    const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
-    const uint32_t drow = (uint32_t)(bh * T + tq);
-    const bf16_t* kp = P.k[j] + head * P.kv_hstride;
-    const bf16_t* vp = P.v[j] + head * P.kv_hstride;
-    u32x4 stg[2];
-    auto issue = [&](int kt) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int c = tid + 256 * u;
-        if (c < 64 * G::CH) {
-          const bool isv = c >= 32 * G::CH;
-          const int cc = isv ? c - 32 * G::CH : c;
-          stg[u] = tile_chunk(isv ? vp : kp, rowbase, kt * 32, cc / G::CH, (cc % G::CH) * 8, T, P.kv_ld);
+    for (int dt = 0; dt < G::ND; ++dt) zero16(dq[dt]);
+    for (int j = 0; j < P.nstreams; ++j) {
+      const bf16_t* oj = (P.nstreams > 1) ? P.oj[j] : P.o;
+      float dsum = 0.f;
+#pragma unroll
+      for (int s = 0; s < G::NKS; ++s) {
+        const int d0 = 16 * s + 8 * h;
+        const bf16x8 ov = ld8(oj + (rowbase + tq) * P.o_ld + head * HS + d0, qok && d0 < HS);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dsum += (float)ov[e] * (float)dof[s][e];
+      }
+      dsum += __shfl_xor(dsum, 32, 64);
+      if (qok && h == 0) P.dvec[j][(int64_t)bh * T + tq] = dsum;
+      const float lse2 = qok ? P.lse[j][(int64_t)bh * T + tq] * kLog2e : 0.f;
+      const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+      for (int c = 0; c < walk.nch; ++c) {
+        int nj, nc;
+        const bool reload = walk.next(u, j, c, nj, nc);
+        if (live) {
+          const int kt_lo = c * (ROWS / 32);
+          const int last = min(qt, min(kt_lo + ROWS / 32, nt) - 1);
+          #pragma unroll 1
+          for (int kt = kt_lo; kt <= last; ++kt)
+            dq_tile<HS>(ks, vs, (kt - kt_lo) * 32, kt * 32, tq, kt == qt, qf, dof, lse2, dsum, dq, c2, P, dkey, drow,
+                        lane);
+        }
+        if (reload) {
+          __syncthreads();
+          st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
+                  T, tid);
+          st.store(ks, G::RW, vs, G::RW, tid);
+          __syncthreads();
         }
       }
-    };
-    auto commit = [&](int buf) {
+    }
+    if (qok) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int c = tid + 256 * u;
-        if (c < 64 * G::CH) {
-          const bool isv = c >= 32 * G::CH;
-          const int cc = isv ? c - 32 * G::CH : c;
-          const int row = cc / G::CH, col = (cc % G::CH) * 8;
-          *reinterpret_cast<u32x4*>(isv ? &vs[buf][row * G::RW + col] : &ks[buf][row * G::RW + col]) = stg[u];
+      for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = dt * 32 + 8 * g + 4 * h;
+          if (d0 < HS)
+            *reinterpret_cast<u32x2*>(P.dq + (rowbase + tq) * P.dq_ld + head * HS + d0) =
+                u32x2{pack2bf(dq[dt][4 * g] * scale, dq[dt][4 * g + 1] * scale),
+                      pack2bf(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale)};
         }
-      }
-    };
-    __syncthreads();
-    issue(0);
-    commit(0);
-    __syncthreads();
-    for (int kt = 0; kt <= last_kt; ++kt) {
-      const int cur = kt & 1;
-      const bool more = kt + 1 <= last_kt;
-      if (more) issue(kt + 1);
-      if (kt <= qt) {
-        const int k0 = kt * 32;
-        f32x16 sacc, dpacc;
-        zero16(sacc);
-        zero16(dpacc);
-#pragma unroll
-        for (int s = 0; s < G::NKS; ++s) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&ks[cur][r * G::RW + 16 * s + 8 * h]);
-          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(&vs[cur][r * G::RW + 16 * s + 8 * h]);
-          sacc = mfma32(kf, qf[s], sacc);
-          dpacc = mfma32(vf, dof[s], dpacc);
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          const bool ok = qok && key <= tq && key < T;
-          const float pv = ok ? __expf(sacc[e] * scale - lse) : 0.f;
-          float dp = dpacc[e];
-          if (P.drop_thr) dp = (mmt_hash(dkey, drow, (uint32_t)key) >= P.drop_thr) ? dp * P.drop_scale : 0.f;
-          sacc[e] = pv * (dp - dsum);  // dS^T
-        }
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8 df = acc_frag(sacc, s);
-#pragma unroll
-          for (int dt = 0; dt < G::ND; ++dt) dq[dt] = mfma32(tr_frag(ks[cur], G::RW, dt, s, lane), df, dq[dt]);
-        }
-      }
-      if (more) commit(cur ^ 1);
-      __syncthreads();
     }
   }
-  if (qok) {
+}
+
+// dK, dV: one 32x32 (queries x keys) tile; S, dP recomputed, dV += P^T dO, dK += dS^T Q
+template <int HS>
+__device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, const float* lsl, const float* dsl,
+                                          int ql, int q0, int tk, bool masked, int T,
+                                          const bf16x8 (&kf)[Geo<HS>::NKS], const bf16x8 (&vf)[Geo<HS>::NKS],
+                                          f32x16 (&dk)[Geo<HS>::ND], f32x16 (&dv)[Geo<HS>::ND], float c2,
+                                          const AttnProblem& P, uint32_t dkey, int bhT, int lane) {
+  using G = Geo<HS>;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 sacc, dpacc, pm;
+  zero16(sacc);
+  zero16(dpacc);
 #pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt)
+  for (int s = 0; s < G::NKS; ++s) {
+    const bf16x8 qa = *reinterpret_cast<const bf16x8*>(qs + (ql + r) * G::RW + 16 * s + 8 * h);
+    const bf16x8 da = *reinterpret_cast<const bf16x8*>(dos + (ql + r) * G::RW + 16 * s + 8 * h);
+    sacc = mfma32(qa, kf[s], sacc);    // S[q][key]
+    dpacc = mfma32(da, vf[s], dpacc);  // dP[q][key]
+  }
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d0 = dt * 32 + 8 * g + 4 * h;
-        if (d0 < HS)
-          *reinterpret_cast<u32x2*>(P.dq + (rowbase + tq) * P.dq_ld + head * HS + d0) =
-              u32x2{pack2bf(dq[dt][4 * g] * scale, dq[dt][4 * g + 1] * scale),
-                    pack2bf(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale)};
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsl + ql + 8 * g + 4 * h);
+    const f32x4 d4 = *reinterpret_cast<const f32x4*>(dsl + ql + 8 * g + 4 * h);
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      const int e = 4 * g + e4;
+      const int tq = q0 + 8 * g + 4 * h + e4;
+      float pv = ex2(sacc[e] * c2 - l4[e4]);
+      if (masked && !(tk <= tq && tq < T)) pv = 0.f;
+      if (P.drop_thr) {
+        const bool keep = mmt_hash(dkey, (uint32_t)(bhT + tq), (uint32_t)tk) >= P.drop_thr;
+        pm[e] = keep ? pv * P.drop_scale : 0.f;
+        sacc[e] = pv * ((keep ? dpacc[e] * P.drop_scale : 0.f) - d4[e4]);
+      } else {
+        pm[e] = pv;
+        sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
       }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 pf = acc_frag(pm, s);
+    const bf16x8 df = acc_frag(sacc, s);
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) {
+      dv[dt] = mfma32(pf, tr_frag(dos + ql * G::RW, G::RW, dt, s, lane), dv[dt]);
+      dk[dt] = mfma32(df, tr_frag(qs + ql * G::RW, G::RW, dt, s, lane), dk[dt]);
+    }
   }
 }
 
 // =============================================================================================
-// backward dK, dV: grid (ceil(T/128), B*H*nstreams, G); wave w owns key tile 4*blockIdx.x + w
+// backward dK, dV: grid (ceil(nt/8), B*H*nstreams, G); wave w owns key tiles 8*bx + w, 8*bx + 7 - w
 // =============================================================================================
 template <int HS>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
+  constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
   const int nbh = gridDim.y / P.nstreams;
   if ((int)blockIdx.y >= nbh * P.nstreams) return;
   const int j = blockIdx.y / nbh;
   const int bh = blockIdx.y % nbh;
   const int b = bh / H, head = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int nt = (T + 31) / 32;
-  const int kt = blockIdx.x * 4 + w;
-  const int first_qt = blockIdx.x * 4;
-  const int k0 = kt * 32, tk = k0 + r;
-  const bool kok = tk < T;
+  const int kt0 = blockIdx.x * 8;
+  const int q_lo = kt0 * 32;
+  const ChunkWalk walk{1, (T - q_lo + ROWS - 1) / ROWS};
+  const bool ragged = (T & 31) != 0;
   const int64_t rowbase = (int64_t)b * T;
-  __shared__ __attribute__((aligned(16))) bf16_t qs[2][32 * G::RW];   // Q tile: row + tr reads
-  __shared__ __attribute__((aligned(16))) bf16_t dos[2][32 * G::RW];  // dO tile: row + tr reads
-  __shared__ __attribute__((aligned(16))) float lsd[2][2][32];        // LSE, D of the tile's rows
+  const float c2 = scale * kLog2e;
+  __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
+  __shared__ __attribute__((aligned(16))) bf16_t dos[ROWS * G::RW];  // dO chunk: row + tr reads
+  __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // log2-domain LSE, D of the chunk rows
+  for (int q = tid; q < ROWS * G::RW; q += 256)
+    if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
 
   const bf16_t* kp = P.k[j] + head * P.kv_hstride;
   const bf16_t* vp = P.v[j] + head * P.kv_hstride;
-  bf16x8 kf[G::NKS], vf[G::NKS];
-#pragma unroll
-  for (int s = 0; s < G::NKS; ++s) {
-    const int d0 = 16 * s + 8 * h;
-    const bool ok = kok && d0 < HS;
-    kf[s] = ld8(kp + (rowbase + tk) * P.kv_ld + d0, ok);
-    vf[s] = ld8(vp + (rowbase + tk) * P.kv_ld + d0, ok);
-  }
-  for (int q = tid; q < 2 * 32 * G::RW; q += 256) {
-    const int c = q % G::RW;
-    if (c >= HS) { (&qs[0][0])[q] = 0; (&dos[0][0])[q] = 0; }
-  }
-  f32x16 dk[G::ND], dv[G::ND];
-#pragma unroll
-  for (int dt = 0; dt < G::ND; ++dt) { zero16(dk[dt]); zero16(dv[dt]); }
-
   const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
   const float* lsep = P.lse[j] + (int64_t)bh * T;
   const float* dvp = P.dvec[j] + (int64_t)bh * T;
   const bf16_t* qp = P.q + head * HS;
   const bf16_t* dop = P.dout + head * HS;
-  u32x4 stg[2];
-  float sl = 0.f;
-  auto issue = [&](int qt) {
+  constexpr int NSL = 2 * ROWS / 256;
+  Stager<HS> st;
+  float sl[NSL];
+  auto load = [&](int r0) {
+    st.load(qp, P.q_ld, dop, P.dout_ld, rowbase, r0, T, tid);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
-      if (c < 64 * G::CH) {
-        const bool isd = c >= 32 * G::CH;
-        const int cc = isd ? c - 32 * G::CH : c;
-        stg[u] = isd ? tile_chunk(dop, rowbase, qt * 32, cc / G::CH, (cc % G::CH) * 8, T, P.dout_ld)
-                     : tile_chunk(qp, rowbase, qt * 32, cc / G::CH, (cc % G::CH) * 8, T, P.q_ld);
-      }
-    }
-    if (tid < 64) {
-      const int t = qt * 32 + (tid & 31);
-      sl = t < T ? ((tid < 32) ? lsep[t] : dvp[t]) : 0.f;
+      const int t = r0 + (c % ROWS);
+      sl[u] = t < T ? ((c < ROWS) ? lsep[t] * kLog2e : dvp[t]) : 0.f;
     }
   };
-  auto commit = [&](int buf) {
+  auto store = [&]() {
+    st.store(qs, G::RW, dos, G::RW, tid);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
-      if (c < 64 * G::CH) {
-        const bool isd = c >= 32 * G::CH;
-        const int cc = isd ? c - 32 * G::CH : c;
-        const int row = cc / G::CH, col = (cc % G::CH) * 8;
-        *reinterpret_cast<u32x4*>(isd ? &dos[buf][row * G::RW + col] : &qs[buf][row * G::RW + col]) = stg[u];
-      }
+      lsd[c / ROWS][c % ROWS] = sl[u];
     }
-    if (tid < 64) lsd[buf][tid >> 5][tid & 31] = sl;
   };
-  issue(first_qt);
-  commit(0);
+  load(q_lo);
+  store();
   __syncthreads();
-  for (int qt = first_qt; qt < nt; ++qt) {
-    const int cur = (qt - first_qt) & 1;
-    const bool more = qt + 1 < nt;
-    if (more) issue(qt + 1);
-    if (qt >= kt) {
-      const int q0 = qt * 32;
-      f32x16 sacc, dpacc;
-      zero16(sacc);
-      zero16(dpacc);
+
+#pragma unroll 1
+  for (int u = 0; u < 2; ++u) {
+    const int kt = u == 0 ? kt0 + w : kt0 + 7 - w;
+    const bool live = kt < nt;
+    const int tk = kt * 32 + r;
+    bf16x8 kf[G::NKS], vf[G::NKS];
+    f32x16 dk[G::ND], dv[G::ND];
 #pragma unroll
-      for (int s = 0; s < G::NKS; ++s) {
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(&qs[cur][r * G::RW + 16 * s + 8 * h]);
-        const bf16x8 da = *reinterpret_cast<const bf16x8*>(&dos[cur][r * G::RW + 16 * s + 8 * h]);
-        sacc = mfma32(qa, kf[s], sacc);    // S[q][key]
-        dpacc = mfma32(da, vf[s], dpacc);  // dP[q][key]
+    for (int s = 0; s < G::NKS; ++s) {
+      const int d0 = 16 * s + 8 * h;
+      const bool ok = live && tk < T && d0 < HS;
+      kf[s] = ld8(kp + (rowbase + tk) * P.kv_ld + d0, ok);
+      vf[s] = ld8(vp + (rowbase + tk) * P.kv_ld + d0, ok);
+    }
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) { zero16(dk[dt]); zero16(dv[dt]); }
+    for (int c = 0; c < walk.nch; ++c) {
+      int nj, nc;
+      const bool reload = walk.next(u, 0, c, nj, nc);
+      const int r0 = q_lo + c * ROWS;
+      if (live) {
+        const int qt_lo = r0 / 32, qt_hi = min(qt_lo + ROWS / 32, nt) - 1;
+        #pragma unroll 1
+        for (int qt = max(kt, qt_lo); qt <= qt_hi; ++qt)
+          dkdv_tile<HS>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tk, qt == kt || (ragged && qt == nt - 1), T,
+                        kf, vf, dk, dv, c2, P, dkey, bh * T, lane);
       }
-      f32x16 pm;
+      if (reload) {
+        __syncthreads();
+        load(q_lo + nc * ROWS);
+        store();
+        __syncthreads();
+      }
+    }
+    // dK/dV tiles: rows = key ((e&3)+8(e>>2)+4h), cols = d (lane)
+    if (live) {
+      bf16_t* dkp = P.dk[j] + head * P.dkv_hstride;
+      bf16_t* dvo = P.dv[j] + head * P.dkv_hstride;
+      const int k0 = kt * 32;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(&lsd[cur][0][8 * g + 4 * h]);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&lsd[cur][1][8 * g + 4 * h]);
+      for (int dt = 0; dt < G::ND; ++dt) {
+        const int d = dt * 32 + r;
+        if (d >= HS) continue;
 #pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          const int e = 4 * g + e4;
-          const int tq = q0 + 8 * g + 4 * h + e4;
-          const bool ok = kok && tq < T && tk <= tq;
-          const float pv = ok ? __expf(sacc[e] * scale - l4[e4]) : 0.f;
-          if (P.drop_thr) {
-            const bool keep = mmt_hash(dkey, (uint32_t)(bh * T + tq), (uint32_t)tk) >= P.drop_thr;
-            pm[e] = keep ? pv * P.drop_scale : 0.f;
-            sacc[e] = pv * ((keep ? dpacc[e] * P.drop_scale : 0.f) - d4[e4]);
-          } else {
-            pm[e] = pv;
-            sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
+        for (int e = 0; e < 16; ++e) {
+          const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (key < T) {
+            dkp[(rowbase + key) * P.dkv_ld + d] = f2bf(dk[dt][e] * scale);
+            dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(dv[dt][e]);
           }
         }
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = acc_frag(pm, s);
-        const bf16x8 df = acc_frag(sacc, s);
-#pragma unroll
-        for (int dt = 0; dt < G::ND; ++dt) {
-          dv[dt] = mfma32(pf, tr_frag(dos[cur], G::RW, dt, s, lane), dv[dt]);
-          dk[dt] = mfma32(df, tr_frag(qs[cur], G::RW, dt, s, lane), dk[dt]);
-        }
-      }
-    }
-    if (more) commit(cur ^ 1);
-    __syncthreads();
-  }
-  // dK/dV tiles: rows = key ((e&3)+8(e>>2)+4h), cols = d (lane)
-  bf16_t* dkp = P.dk[j] + head * P.dkv_hstride;
-  bf16_t* dvo = P.dv[j] + head * P.dkv_hstride;
-#pragma unroll
-  for (int dt = 0; dt < G::ND; ++dt) {
-    const int d = dt * 32 + r;
-    if (d >= HS) continue;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (key < T) {
-        dkp[(rowbase + key) * P.dkv_ld + d] = f2bf(dk[dt][e] * scale);
-        dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(dv[dt][e]);
       }
     }
   }
@@ -522,7 +600,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBatch batch, int
 
 template <int HS>
 static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
-  const int nb = (T + 127) / 128;
+  const int nb = ((T + 31) / 32 + 7) / 8;
   if (!bwd) {
     hipLaunchKernelGGL(attn_fwd_kernel<HS>, dim3(nb, B * H, bt.count), dim3(256), 0, s, bt, T, H, scale);
   } else {

@@ -380,10 +380,12 @@ int dw_splits(const GemmBatch& gb, int R) {
   for (int g = 0; g < gb.count; ++g)
     tiles += ((gb.p[g].M + 127) / 128) * ((gb.p[g].N + 127) / 128);
   if (tiles <= 0) return 1;
-  // every split adds one fp32 atomic per output element (the chip-wide atomic rate, ~1.3 TB/s,
-  // not the MFMA rate, bounds a heavily split launch): aim at ~one block per CU, at most 8 splits
-  int s = 512 / tiles;
-  const int maxs = std::max(1, std::min(8, R / 1024));
+  // every split adds one fp32 atomic per output element and a per-block epilogue, so aim at ~2
+  // blocks per CU and no more: launches of <= 8 output tiles split up to 32 ways (>= 8 K-steps of
+  // 64 rows each), larger ones at most 8 ways. Measured at C1 (rocprof, grouped launches):
+  // 8 tiles 44.5 -> 29.2 us going from 8 to 32 splits, 24 tiles 50.7 -> 64.9 us going from 8 to 22.
+  const int s = (512 + tiles - 1) / tiles;
+  const int maxs = std::max(1, std::min(tiles <= 8 ? 32 : 8, R / 512));
   return std::max(1, std::min(s, maxs));
 }
 

@@ -21,6 +21,8 @@
 #include "mmt_common.h"
 #include "mmt_kernels.h"
 
+#include <type_traits>
+
 #define GBM 128
 #define GBN 128
 
@@ -45,10 +47,37 @@ __device__ __forceinline__ int kc_swz(int chunk, int row) {
   return BK == 64 ? (chunk ^ ((row >> 1) & 7)) : (chunk ^ ((row >> 2) & 3));
 }
 
+// Buffer resource (V#) as four SGPR words: base, range in bytes, raw dword access.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int32_t)((a >> 32) & 0xffffu));  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((int32_t)min(bytes, (int64_t)0x7ffffff0));
+  r[3] = 0x00020000;
+  return r;
+}
+
+// One 16-B-per-lane LDS-DMA: LDS[lds_addr + 16*lane .. +16) = buffer[voff .. +16) (0 if out of
+// range). Issued as inline asm on purpose: the compiler's waitcnt pass cannot tell the ring stage
+// a DMA targets from the stage the fragment reads use and would drain vmcnt(0) before every
+// fragment read (no pipelining at all); the kernel counts its own DMAs (wait_vm) instead.
+__device__ __forceinline__ void dma16(const i32x4& rsrc, uint32_t lds_addr, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(lds_addr), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+
 // issue this wave's LDS-DMA pieces (1 KiB each) of one operand tile for K-step k0.
 // the tile (128 x BK bf16) has BK/4 pieces, BK/16 per wave; lane L writes LDS bytes [i*1024 + 16L, +16).
 template <int BK, bool KC>
-__device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rsrc, char* img, int ld, int rows_total, int K,
+__device__ __forceinline__ void issue_tile(const i32x4& rsrc, char* img, int ld, int rows_total, int K,
                                            int r0, int k0, int wave, int lane) {
   constexpr int PPW = BK / 16;  // pieces per wave
   constexpr int CPR = BK / 8;   // chunks per K-contiguous row
@@ -67,7 +96,7 @@ __device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rsrc, char* im
       const int gk = k0 + kr, gcol = r0 + chunk * 8;
       voff = (gk < K && gcol < rows_total) ? (gk * ld + gcol) * 2 : 0x7fffffff;
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(img + i * 1024), 16, voff, 0, 0, 0);
+    dma16(rsrc, __builtin_amdgcn_readfirstlane(lds_u32(img + i * 1024)), voff);
   }
 }
 
@@ -190,26 +219,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
   if (ks0 < ks1) {
     // buffer descriptors over each operand's whole extent (range-checked: OOB pieces read 0)
     const int a_rows = A_KC ? M : K, b_rows = B_KC ? N : K;
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)P.A, (short)0, (int)min((int64_t)a_rows * P.lda * 2, (int64_t)0x7ffffff0), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)P.B, (short)0, (int)min((int64_t)b_rows * P.ldb * 2, (int64_t)0x7ffffff0), 0x00020000);
+    const i32x4 ra = make_rsrc(P.A, (int64_t)a_rows * P.lda * 2);
+    const i32x4 rb = make_rsrc(P.B, (int64_t)b_rows * P.ldb * 2);
     const int nk = ks1 - ks0;
-    auto issue = [&](int t) {  // K-step ks0 + t into stage t % ST
-      char* st = lds + (t % ST) * STAGE_BYTES;
-      issue_tile<BK, A_KC>(ra, st, P.lda, M, K, m0, (ks0 + t) * BK, wave, lane);
-      issue_tile<BK, B_KC>(rb, st + IMG_BYTES, P.ldb, N, K, n0, (ks0 + t) * BK, wave, lane);
-    };
-#pragma unroll
-    for (int t = 0; t < ST - 1; ++t)
-      if (t < nk) issue(t);
-    for (int t = 0; t < nk; ++t) {
-      // stage t landed for this wave: allow the younger stages' pieces to stay in flight
-      wait_vm(PIECES * min(ST - 2, nk - 1 - t));
+    // one K-step: stage U of the ring holds K-step tt (tt % ST == U), the step prefetches K-step
+    // tt + ST - 1 into stage (U + ST - 1) % ST. U is a compile-time constant (the loop below is
+    // unrolled by ST) so the LDS offsets of the DMA writes and of the fragment reads are static:
+    // with a dynamic stage index hipcc cannot separate them and drains vmcnt(0) before the
+    // fragment reads, serialising every K-step behind its own prefetch.
+    auto step = [&](int tt, auto UC) {
+      constexpr int U = decltype(UC)::value;
+      // stage U landed for this wave: allow the younger stages' pieces to stay in flight
+      wait_vm(PIECES * min(ST - 2, nk - 1 - tt));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's pieces of stage t landed; stage t-1 reads done
-      if (t + ST - 1 < nk) issue(t + ST - 1);
-      const char* imgA = lds + (t % ST) * STAGE_BYTES;
+      __builtin_amdgcn_s_barrier();  // every wave's pieces of stage U landed; the previous stage's reads done
+      if (tt + ST - 1 < nk) {
+        char* st = lds + ((U + ST - 1) % ST) * STAGE_BYTES;
+        const int k0 = (ks0 + tt + ST - 1) * BK;
+        issue_tile<BK, A_KC>(ra, st, P.lda, M, K, m0, k0, wave, lane);
+        issue_tile<BK, B_KC>(rb, st + IMG_BYTES, P.ldb, N, K, n0, k0, wave, lane);
+      }
+      const char* imgA = lds + U * STAGE_BYTES;
       const char* imgB = imgA + IMG_BYTES;
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
@@ -226,7 +256,24 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
             else acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
           }
       }
+    };
+#pragma unroll
+    for (int t = 0; t < ST - 1; ++t)
+      if (t < nk) {
+        char* st = lds + t * STAGE_BYTES;
+        issue_tile<BK, A_KC>(ra, st, P.lda, M, K, m0, (ks0 + t) * BK, wave, lane);
+        issue_tile<BK, B_KC>(rb, st + IMG_BYTES, P.ldb, N, K, n0, (ks0 + t) * BK, wave, lane);
+      }
+    int t = 0;
+    for (; t + ST <= nk; t += ST) {
+      step(t, std::integral_constant<int, 0>{});
+      step(t + 1, std::integral_constant<int, 1>{});
+      if constexpr (ST > 2) step(t + 2, std::integral_constant<int, (ST > 2 ? 2 : 0)>{});
+      if constexpr (ST > 3) step(t + 3, std::integral_constant<int, (ST > 3 ? 3 : 0)>{});
     }
+    if (t < nk) step(t, std::integral_constant<int, 0>{});
+    if (ST > 2 && t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
+    if constexpr (ST > 3) { if (t + 2 < nk) step(t + 2, std::integral_constant<int, (ST > 3 ? 2 : 0)>{}); }
   }
 
   float alpha = P.alpha;
