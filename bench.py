@@ -35,6 +35,8 @@ CONFIGS = {
     "target": dict(M=4, C=512, H=8, L=6, T=512, B=32),
     "c3": dict(M=8, C=512, H=8, L=12, T=1024, B=16),
 }
+PEAK_TFLOPS = 2500.0  # MI355X bf16 dense MFMA (MI355X_MICROARCH.md; no sparsity)
+PEAK_HBM_GBS = 8000.0  # HBM3E
 METRIC = "training tokens/sec/GPU, 4-modality 1M-row synthetic, at 1/2/4/8 MI355X"
 
 
@@ -59,6 +61,31 @@ def dominant_kernel_flops(label, M, C, H, T, B, V):
     if label == "qkv1":
         return M * 2.0 * R * C * (1.5 * C)
     raise ValueError(label)
+
+
+def dominant_kernel_bytes(label, M, C, H, T, B, V):
+    """Algorithmic HBM bytes of one grouped launch of `label`: each operand read once, each
+    output written once (bf16 activations / packed weights, fp32 bias)."""
+    R = B * T
+    if label == "ffn0":
+        return M * (R * C * 2 + 4 * C * C * 2 + 4 * C * 4 + R * 4 * C * 2)
+    if label == "ffn2":
+        return M * (R * 4 * C * 2 + 4 * C * C * 2 + C * 4 + 2 * R * C * 4 + R * C * 2)
+    if label == "qkv1":
+        return M * (R * C * 2 + int(1.5 * C) * C * 2 + int(1.5 * C) * 4 + R * int(1.5 * C) * 2)
+    raise ValueError(label)
+
+
+def pmc_traffic(label):
+    """HBM bytes per launch of `label` from the committed PMC passes (profiles/pmc_traffic.json:
+    rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate runs of this bench, FETCH_SIZE doubled
+    per the gfx950 correction of MI355X_MICROARCH.md); None when not collected for this kernel."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(label, {}).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(cfg, data, seconds):
@@ -102,6 +129,7 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--probe", default="ffn0", help="engine launch label timed live for the roofline line")
     ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM pipeline variant (mmt_gemm_set_variant)")
+    ap.add_argument("--bucket-mb", type=int, default=32, help="DP gradient all-reduce bucket size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -116,6 +144,7 @@ def main():
 
     import config_utils
     import mmt_data
+    import mmt_dist
     import mmt_lib as ML
     import mmt_optim
     import training_utils as TU
@@ -134,7 +163,9 @@ def main():
     torch.manual_seed(1234)
     model = MultimodalTransformer(M, V, data["params"]).to(dev)
     if world > 1:
-        dist.broadcast(model.flat_params.data, src=0)
+        # identical replicas (broadcast from rank 0) + bucketed gradient all-reduce over RCCL,
+        # issued stage by stage during the backward (overlapped with the remaining stages)
+        mmt_dist.enable_data_parallel(model, bucket_bytes=args.bucket_mb << 20)
     opt = mmt_optim.AdamW(model.parameters(), lr=3e-4)
     batcher = TU.DeviceBatcher(data["train"], data["val"], V, [p[2] for p in data["params"]], data["file_lengths"],
                                data["is_percents"], T, B, dev, seed=1000 + rank)
@@ -143,9 +174,7 @@ def main():
         xb, yb = batcher.next("train", 1)
         _, losses = model(xb, yb)
         opt.zero_grad(set_to_none=True)
-        sum(losses).backward()
-        if world > 1:
-            dist.all_reduce(model.flat_params.grad, op=dist.ReduceOp.AVG)
+        sum(losses).backward()  # DP: the gradient comes back already averaged over ranks
         opt.step()
         return losses
 
@@ -183,11 +212,18 @@ def main():
     if probe_n.value > 0:
         per_launch_ms = probe_ms.value / probe_n.value
         fl = dominant_kernel_flops(args.probe, M, C, H, T, B, V)
-        ach = fl / (per_launch_ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": 2500.0, "unit": "TFLOP/s",
-                "frac": round(ach / 2500.0, 4), "traffic": None, "kernel": args.probe,
-                "launches": probe_n.value, "avg_launch_us": round(per_launch_ms * 1e3, 2),
-                "flops_per_launch": fl}
+        by = dominant_kernel_bytes(args.probe, M, C, H, T, B, V)
+        sec = per_launch_ms * 1e-3
+        # the binding roof at this kernel's arithmetic intensity (ridge = 2500 TFLOP/s / 8 TB/s)
+        if fl / by >= PEAK_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9):
+            roof = {"bound": "mfma", "achieved": round(fl / sec / 1e12, 1), "peak": PEAK_TFLOPS, "unit": "TFLOP/s"}
+        else:
+            roof = {"bound": "hbm", "achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
+        roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+        roof.update({"traffic": pmc_traffic(args.probe), "kernel": args.probe, "launches": probe_n.value,
+                     "avg_launch_us": round(per_launch_ms * 1e3, 2), "flops_per_launch": fl,
+                     "algorithmic_bytes_per_launch": by, "tflops": round(fl / sec / 1e12, 1),
+                     "gbs": round(by / sec / 1e9, 1)})
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
@@ -198,7 +234,7 @@ def main():
                    "parallelism": f"dp{world}"},
         "tokens_per_gpu_per_s": round(value / world, 1),
         "step_tflops_per_gpu": round(achieved_step_tflops, 2),
-        "step_mfma_frac": round(achieved_step_tflops / 2500.0, 4),
+        "step_mfma_frac": round(achieved_step_tflops / PEAK_TFLOPS, 4),
         "train_flops_per_row": flops_row,
         "final_loss": round(final_loss, 4),
         "roofline": roof,

@@ -1,0 +1,87 @@
+"""Worker of tests/test_gpu_dp.py (launched by torch.distributed.run, 2 ranks on one GPU, gloo).
+
+Each rank trains on its half of one global batch with mmt_dist's bucketed, stage-overlapped
+gradient averaging; rank 0 also runs the whole global batch through a second, single-process
+replica. DP equivalence: N ranks x local batch b == 1 rank x batch N*b on the same
+samples -> gradients, losses and the params after 2 AdamW steps agree (the only difference is
+the fp32 summation order of the weight-gradient split-K accumulation).
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "trade-aid-multimodal-transformer_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    import config_utils
+    import mmt_dist
+    import mmt_optim
+    from model import MultimodalTransformer
+    C, H, L, T, Bg = 64, 2, 2, 64, 8
+    V = [57, 13, 24, 5]
+    cross = [True, False, True, False]
+    config_utils._config_cache = {"n_embd": C, "n_head": H, "n_layer": L, "block_size": T, "dropout": 0.0,
+                                  "device": "cuda", "batch_size": Bg, "eval_iters": 1}
+    params = [[None] * 8 + [c] + [None] * 3 for c in cross]
+    torch.manual_seed(1234 + 17 * rank)  # different init per rank: the broadcast must fix it
+    m = MultimodalTransformer(len(V), V, params).to("cuda")
+    sync = mmt_dist.enable_data_parallel(m, bucket_bytes=64 << 10)
+    assert len(sync.buckets) >= 3, sync.buckets
+    g = torch.Generator().manual_seed(99)
+    idx = [torch.randint(0, v, (Bg, T), generator=g) for v in V]
+    tgt = [torch.randint(0, v, (Bg, T), generator=g) for v in V]
+    b = Bg // world
+    mine = slice(rank * b, (rank + 1) * b)
+    opt = mmt_optim.AdamW(m.parameters(), lr=1e-3)
+    ref = None
+    if rank == 0:
+        ref = MultimodalTransformer(len(V), V, params).to("cuda")
+        with torch.no_grad():
+            ref.flat_params.copy_(m.flat_params)
+        ropt = mmt_optim.AdamW(ref.parameters(), lr=1e-3)
+    fails = []
+    for it in range(2):
+        _, losses = m([t[mine].cuda() for t in idx], [t[mine].cuda() for t in tgt])
+        opt.zero_grad(set_to_none=True)
+        sum(losses).backward()
+        gdp = m.flat_params.grad.detach().clone()
+        loc = torch.stack([l.detach() for l in losses])
+        dist.all_reduce(loc)  # gloo on a CUDA tensor: mean of the per-rank mean losses
+        loc /= world
+        opt.step()
+        if rank == 0:
+            _, rl = ref([t.cuda() for t in idx], [t.cuda() for t in tgt])
+            ropt.zero_grad(set_to_none=True)
+            sum(rl).backward()
+            gref = ref.flat_params.grad.detach()
+            e = ((gdp - gref).norm() / gref.norm()).item()
+            lerr = (loc - torch.stack([l.detach() for l in rl])).abs().max().item()
+            ropt.step()
+            perr = (m.flat_params.detach() - ref.flat_params.detach()).abs().max().item()
+            print(f"iter {it}: grad rel-L2 {e:.2e}  loss max-abs {lerr:.2e}  param max-abs {perr:.2e}", flush=True)
+            if not (e < 2e-3 and lerr < 2e-3 and perr < 1e-4):
+                fails.append((it, e, lerr, perr))
+    # replicas stay identical across ranks
+    p = m.flat_params.detach().clone()
+    p0 = p.clone()
+    dist.broadcast(p0, src=0)
+    same = torch.equal(p, p0)
+    if not same:
+        fails.append(("replica drift", rank))
+    dist.destroy_process_group()
+    if fails:
+        print("FAIL", fails, flush=True)
+        sys.exit(1)
+    print(f"rank {rank} ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()

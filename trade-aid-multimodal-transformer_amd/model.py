@@ -105,6 +105,7 @@ class MultimodalTransformer(nn.Module):
         self._ws_bytes = {}
         self._gen = 0
         self._last = None
+        self._grad_sync = None  # mmt_dist.GradSync when data parallel
 
     # ------------------------------------------------------------------ layout / state_dict
     def _make_tril_keys(self):
@@ -218,14 +219,37 @@ class MultimodalTransformer(nn.Module):
         self._last = (flat, idx, tgt)
         return logits, losses
 
+    def backward_stage_ranges(self):
+        """[(begin, end)] of the flat gradient finalised by each backward stage, in execution order
+        (post block, layers L-1..0, embeddings); see mmt_backward_stage_range in include/mmt.h."""
+        L = ML.lib()
+        out = []
+        b, e = ML.c_i64(), ML.c_i64()
+        for s in range(L.mmt_backward_stage_count(self._ctx)):
+            ML.check(L.mmt_backward_stage_range(self._ctx, s, ctypes.byref(b), ctypes.byref(e)), self._ctx,
+                     "mmt_backward_stage_range")
+            out.append((b.value, e.value))
+        return out
+
     def _launch_backward(self, g_losses):
         L = ML.lib()
         flat = self._last[0]
         g = g_losses.detach().to(dtype=torch.float32).contiguous()
         grad = torch.empty_like(flat)
-        rc = L.mmt_backward(self._ctx, ML.stream_ptr(flat.device), ML.ptr(g), ML.ptr(flat), ML.ptr(grad),
-                            ML.ptr(self._ws))
-        ML.check(rc, self._ctx, "mmt_backward")
+        sync = self._grad_sync
+        if sync is None:
+            rc = L.mmt_backward(self._ctx, ML.stream_ptr(flat.device), ML.ptr(g), ML.ptr(flat), ML.ptr(grad),
+                                ML.ptr(self._ws))
+            ML.check(rc, self._ctx, "mmt_backward")
+            return grad
+        # data parallel (mmt_dist): stage by stage, each finished bucket all-reduced while the
+        # next stages compute
+        for s in range(L.mmt_backward_stage_count(self._ctx)):
+            rc = L.mmt_backward_stage(self._ctx, ML.stream_ptr(flat.device), s, ML.ptr(g), ML.ptr(flat),
+                                      ML.ptr(grad), ML.ptr(self._ws))
+            ML.check(rc, self._ctx, "mmt_backward_stage")
+            sync.stage_done(s, grad)
+        sync.finish()
         return grad
 
     def forward(self, idx_list, targets_list=None):
