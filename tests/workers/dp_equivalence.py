@@ -48,6 +48,7 @@ def main():
             ref.flat_params.copy_(m.flat_params)
         ropt = mmt_optim.AdamW(ref.parameters(), lr=1e-3)
     fails = []
+    p_init = m.flat_params.detach().clone()
     for it in range(2):
         _, losses = m([t[mine].cuda() for t in idx], [t[mine].cuda() for t in tgt])
         opt.zero_grad(set_to_none=True)
@@ -65,9 +66,12 @@ def main():
             e = ((gdp - gref).norm() / gref.norm()).item()
             lerr = (loc - torch.stack([l.detach() for l in rl])).abs().max().item()
             ropt.step()
-            perr = (m.flat_params.detach() - ref.flat_params.detach()).abs().max().item()
-            print(f"iter {it}: grad rel-L2 {e:.2e}  loss max-abs {lerr:.2e}  param max-abs {perr:.2e}", flush=True)
-            if not (e < 2e-3 and lerr < 2e-3 and perr < 1e-4):
+            # AdamW's early updates are ~lr * sign(g): near-zero gradient elements may flip sign under
+            # a different fp32 summation order, so compare the accumulated UPDATES in L2
+            upd_ref = ref.flat_params.detach() - p_init
+            perr = ((m.flat_params.detach() - p_init - upd_ref).norm() / upd_ref.norm()).item()
+            print(f"iter {it}: grad rel-L2 {e:.2e}  loss max-abs {lerr:.2e}  update rel-L2 {perr:.2e}", flush=True)
+            if not (e < 2e-3 and lerr < 2e-3 and perr < 5e-2):
                 fails.append((it, e, lerr, perr))
     # replicas stay identical across ranks
     p = m.flat_params.detach().clone()

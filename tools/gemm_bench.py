@@ -19,6 +19,9 @@ R = 65536  # 4 modalities x B 64 x T 256
 SHAPES = [
     # name, a_kc, b_kc, epi, M, N, K, splits
     ("ffn0_fwd", 1, 1, "bias_relu_bf16", R, 1024, 256, 1),
+    ("ffn0_store", 1, 1, "store_bf16", R, 1024, 256, 1),
+    ("ffn0_f32", 1, 1, "store_f32", R, 1024, 256, 1),
+    ("qkv1_store", 1, 1, "store_bf16", R, 384, 256, 1),
     ("ffn2_fwd", 1, 1, "bias_resid_f32", R, 256, 1024, 1),
     ("qkv1_fwd", 1, 1, "bias_tanh_bf16", R, 384, 256, 1),
     ("proj2_fwd", 1, 1, "bias_resid_f32", R, 256, 128, 1),
@@ -102,7 +105,8 @@ def main():
     args = ap.parse_args()
     for v in [int(x) for x in args.variants.split(",")]:
         res = run(v, args.reps)
-        print(f"variant {v}: " + "  ".join(f"{k} {us:7.1f}us {tf:6.1f}TF" for k, (us, tf) in res.items()), flush=True)
+        for k, (us, tf) in res.items():
+            print(f"variant {v}: {k:22s} {us:8.1f} us {tf:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -29,6 +29,17 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
+// tanh for fp32 epilogues whose result is stored as bf16: exp-based away from 0, odd Taylor
+// polynomial near 0 (avoids the 1 - e cancellation); |error| < 2e-7, far below bf16 rounding.
+__device__ __forceinline__ float fast_tanh(float x) {
+  const float ax = fabsf(x);
+  const float e = __expf(-2.0f * ax);
+  const float t = __fdividef(1.0f - e, 1.0f + e);
+  const float x2 = x * x;
+  const float p = x * (1.0f + x2 * (-0.333333343f + x2 * (0.133333340f + x2 * -0.0539682540f)));
+  return ax < 0.125f ? p : copysignf(t, x);
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

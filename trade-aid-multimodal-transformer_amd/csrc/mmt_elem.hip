@@ -2,6 +2,8 @@
 // embedding fwd/bwd, fused softmax-cross-entropy, bias-gradient column sums, per-head Q/K/V
 // stage-2 block-diagonal maps, fp32->bf16 weight packing, fused AdamW, directional metric.
 // All grouped over modalities with blockIdx.z (one launch per op per layer).
+#include <stdlib.h>
+
 #include "mmt_common.h"
 #include "mmt_kernels.h"
 
@@ -173,8 +175,15 @@ hipError_t mmt_launch_ln_fwd(const LnBatch& b, int R, int C, hipStream_t s) {
 hipError_t mmt_launch_ln_bwd(const LnBatch& b, int R, int C, hipStream_t s) {
   if (C % 4 != 0 || C > 1024 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
   // 4 rows per block per pass; the grid is capped so the dgamma/dbeta atomics stay few
+  static const int cap = [] {
+    // blocks per problem: every block adds its dgamma/dbeta(/dsum) partials with one atomic per
+    // column, so the cap bounds the same-address atomic chain (C1, 4 problems: 4096 blocks 228 us,
+    // 1024 75 us, 512 52 us, 256 45 us = 5.2 TB/s)
+    const char* e = getenv("MMT_LNB_CAP");
+    return e ? atoi(e) : 256;
+  }();
   int blocks = (R + 3) / 4;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > cap) blocks = cap;
   dim3 grid(blocks, 1, b.count);
   const int nv = (C / 4 + 63) / 64;
   if (nv <= 1) hipLaunchKernelGGL((ln_bwd_kernel<1, 4>), grid, dim3(256), 0, s, b, R, C);
@@ -200,57 +209,107 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbBatch batch, int R, i
   reinterpret_cast<f32x4*>(P.x + (int64_t)r * C)[c4] = a + p;
 }
 
-// token-table gradient: a block owns 256 rows of one modality. Small tables (V*C <= 16K floats)
-// are accumulated in LDS first and flushed with one atomic per touched element per block (the
-// per-token contention of a 5- or 13-entry vocabulary would otherwise serialise thousands of adds
-// on the same addresses); large tables take direct global atomics (few rows per token).
+// token-table gradient, privatised in LDS: a block owns one column slab (SLAB floats, the
+// widest power of two with V * SLAB floats <= 16 K = 64 KiB) of one modality's table and a chunk
+// of rows; it scatter-adds its rows into the LDS slab (ds_add_f32) and flushes the touched
+// entries with one global atomic each. Rows per block scale with V (>= 4 V) so the flush stays
+// small against the rows read; a vocabulary too large for a 4-float slab takes direct atomics.
 #define EMB_LDS_FLOATS 16384
+__host__ __device__ __forceinline__ int emb_slab(int V, int C) {
+  if ((int64_t)V * C <= EMB_LDS_FLOATS) return C;
+  int p = 256;  // largest power-of-two slab dividing C that fits (4 always divides C)
+  while (p > 4 && (C % p != 0 || (int64_t)V * p > EMB_LDS_FLOATS)) p >>= 1;
+  return p;
+}
+__host__ __device__ __forceinline__ int emb_chunk(int V, int R) {
+  int ch = 256;
+  while (ch < 4 * V && ch < R) ch <<= 1;
+  return ch;
+}
 __global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int R, int C) {
   const EmbProblem& P = batch.p[blockIdx.z];
-  const int C4 = C >> 2;
-  const int r0 = blockIdx.x * 256;
-  const int rows = min(256, R - r0);
-  if (rows <= 0) return;
+  const int V = P.V;
+  const int slab = emb_slab(V, C);
+  const int nslab = C / slab;
+  const int chunk = emb_chunk(V, R);
+  const int nchunk = (R + chunk - 1) / chunk;
+  if ((int)blockIdx.x >= nslab * nchunk) return;
+  const int sl = blockIdx.x % nslab, ck = blockIdx.x / nslab;
+  const int c0 = sl * slab;
+  const int r0 = ck * chunk, r1 = min(R, r0 + chunk);
   __shared__ float acc[EMB_LDS_FLOATS];
-  const bool priv = (int64_t)P.V * C <= EMB_LDS_FLOATS;
+  const bool priv = (int64_t)V * slab <= EMB_LDS_FLOATS;
   if (priv) {
-    for (int q = threadIdx.x; q < P.V * C; q += 256) acc[q] = 0.f;
+    for (int q = threadIdx.x; q < V * slab; q += 256) acc[q] = 0.f;
     __syncthreads();
   }
-  for (int q = threadIdx.x; q < rows * C4; q += 256) {
-    const int rr = r0 + q / C4, c4 = q % C4;
-    int64_t id = P.idx[rr];
-    id = id < 0 ? 0 : (id >= P.V ? P.V - 1 : id);
-    const f32x4 d = reinterpret_cast<const f32x4*>(P.dx + (int64_t)rr * C)[c4];
-    if (priv) {
+  const int s4 = slab >> 2;            // f32x4 per row slab
+  const int rows_per_pass = 256 / s4;  // rows covered by the block per pass
+  const int lr = threadIdx.x / s4, c4 = threadIdx.x % s4;
+  constexpr int U = 4;  // passes in flight per thread (idx and dx loads issued together)
+  for (int rb = r0 + lr; lr < rows_per_pass && rb < r1; rb += U * rows_per_pass) {
+    int64_t id[U];
+    f32x4 d[U];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(&acc[id * C + c4 * 4 + e], d[e]);
-    } else {
-      float* dt = P.dtok + id * C + c4 * 4;
+    for (int u = 0; u < U; ++u) {
+      const int rr = rb + u * rows_per_pass;
+      id[u] = rr < r1 ? P.idx[rr] : -1;
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(dt + e, d[e]);
+    for (int u = 0; u < U; ++u) {
+      const int rr = rb + u * rows_per_pass;
+      d[u] = rr < r1 ? reinterpret_cast<const f32x4*>(P.dx + (int64_t)rr * C + c0)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (rb + u * rows_per_pass >= r1) break;
+      const int64_t t = id[u] < 0 ? 0 : (id[u] >= V ? V - 1 : id[u]);
+      if (priv) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(&acc[t * slab + c4 * 4 + e], d[u][e]);
+      } else {
+        float* dt = P.dtok + t * C + c0 + c4 * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(dt + e, d[u][e]);
+      }
     }
   }
   if (priv) {
     __syncthreads();
-    for (int q = threadIdx.x; q < P.V * C; q += 256)
-      if (acc[q] != 0.f) atomicAdd(P.dtok + q, acc[q]);
+    for (int q = threadIdx.x; q < V * slab; q += 256)
+      if (acc[q] != 0.f) atomicAdd(P.dtok + (int64_t)(q / slab) * C + c0 + (q % slab), acc[q]);
   }
 }
 
-// positional-table gradient, shared by all modalities: dpos[t] = sum_m sum_b dx_m[b*T + t]
-// one block per t; deterministic (no atomics): the grad buffer is pre-zeroed, dpos is added once
+// positional-table gradient, shared by all modalities: dpos[t] += sum_m sum_b dx_m[b*T + t].
+// block (t, split): a slice of the M*B rows of position t, 4 rows per wave in flight; one atomic
+// per column per block (EMB_POS_SPLIT per element)
+#define EMB_POS_SPLIT 8
 __global__ __launch_bounds__(256) void embed_pos_bwd_kernel(EmbBatch batch, int B, int T, int C) {
   const int t = blockIdx.x;
   const int C4 = C >> 2;
+  const int nrows = batch.count * B;  // (modality, b) pairs
+  const int per = (nrows + EMB_POS_SPLIT - 1) / EMB_POS_SPLIT;
+  const int q0 = blockIdx.y * per, q1 = min(nrows, q0 + per);
   for (int c4 = threadIdx.x; c4 < C4; c4 += 256) {
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int m = 0; m < batch.count; ++m) {
-      const EmbProblem& P = batch.p[m];
-      for (int b = 0; b < B; ++b) s += reinterpret_cast<const f32x4*>(P.dx + ((int64_t)b * T + t) * C)[c4];
+    int q = q0;
+    for (; q + 4 <= q1; q += 4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int m = (q + u) / B, b = (q + u) % B;
+        v[u] = reinterpret_cast<const f32x4*>(batch.p[m].dx + ((int64_t)b * T + t) * C)[c4];
+      }
+      s += (v[0] + v[1]) + (v[2] + v[3]);
     }
-    f32x4* dp = reinterpret_cast<f32x4*>(batch.p[0].dpos + (int64_t)t * C) + c4;
-    *dp = *dp + s;
+    for (; q < q1; ++q) {
+      const int m = q / B, b = q % B;
+      s += reinterpret_cast<const f32x4*>(batch.p[m].dx + ((int64_t)b * T + t) * C)[c4];
+    }
+    float* dp = batch.p[0].dpos + (int64_t)t * C + 4 * c4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicAdd(dp + e, s[e]);
   }
 }
 
@@ -265,42 +324,71 @@ hipError_t mmt_launch_embed_fwd(const EmbBatch& b, int B, int T, int C, hipStrea
 hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStream_t s) {
   if (C % 4 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
   const int R = B * T;
-  hipLaunchKernelGGL(embed_tok_bwd_kernel, dim3((R + 255) / 256, 1, b.count), dim3(256), 0, s, b, R, C);
+  if (C % 4 || C > 1024) return hipErrorInvalidValue;
+  // grid: the largest (slabs x row chunks) over the problems
+  int maxblocks = 1;
+  for (int g = 0; g < b.count; ++g) {
+    const int nb = (C / emb_slab(b.p[g].V, C)) * ((R + emb_chunk(b.p[g].V, R) - 1) / emb_chunk(b.p[g].V, R));
+    maxblocks = nb > maxblocks ? nb : maxblocks;
+  }
+  hipLaunchKernelGGL(embed_tok_bwd_kernel, dim3(maxblocks, 1, b.count), dim3(256), 0, s, b, R, C);
   // all problems of one batch must share the positional table (one model): dpos of p[0]
   for (int g = 1; g < b.count; ++g)
     if (b.p[g].dpos != b.p[0].dpos) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(embed_pos_bwd_kernel, dim3(T), dim3(256), 0, s, b, B, T, C);
+  hipLaunchKernelGGL(embed_pos_bwd_kernel, dim3(T, EMB_POS_SPLIT), dim3(256), 0, s, b, B, T, C);
   return hipGetLastError();
 }
 
 // ============================================================================================
 // Cross-entropy (F.cross_entropy mean over B*T; model.py:393-400), fused with dlogits:
 //   loss += (logsumexp(x) - x[t]) / R ;  dlogits = softmax(x) - onehot(t)  (bf16, unscaled)
-// one wave per row
+// one wave per row, the row held in registers (KV logits per lane, all loads issued at once);
+// grid-strided rows so each block adds its loss share with ONE atomic (a per-4-row atomic on
+// the single loss address serialised ~16 k atomics per launch)
 // ============================================================================================
+template <int KV>
 __global__ __launch_bounds__(256) void ce_fwd_kernel(CeBatch batch, int R) {
   const CeProblem& P = batch.p[blockIdx.z];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int row = blockIdx.x * 4 + wave;
+  const int V = P.V;
   __shared__ float part[4];
   float contrib = 0.f;
-  if (row < R) {
-    const float* x = P.logits + (int64_t)row * P.V;
-    float m = -INFINITY;
-    for (int v = lane; v < P.V; v += 64) m = fmaxf(m, x[v]);
-    m = warp_max(m);
-    float sum = 0.f;
-    for (int v = lane; v < P.V; v += 64) sum += __expf(x[v] - m);
-    sum = warp_sum(sum);
-    const float lse = m + __logf(sum);
+  for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
+    const float* x = P.logits + (int64_t)row * V;
     const int t = (int)P.tgt[row];
-    contrib = lse - x[t];
     bf16_t* d = P.dlogits + (int64_t)row * P.ld_d;
-    for (int v = lane; v < P.ld_d; v += 64) {
-      float g = 0.f;
-      if (v < P.V) g = __expf(x[v] - lse) - (v == t ? 1.f : 0.f);
-      d[v] = f2bf(g);
+    if (KV > 0) {
+      float v[KV > 0 ? KV : 1];
+#pragma unroll
+      for (int k = 0; k < KV; ++k) {
+        const int i = lane + 64 * k;
+        v[k] = i < V ? x[i] : -INFINITY;
+      }
+      float m = v[0];
+#pragma unroll
+      for (int k = 1; k < KV; ++k) m = fmaxf(m, v[k]);
+      m = warp_max(m);
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < KV; ++k) sum += __expf(v[k] - m);  // exp(-inf) = 0 for the padding
+      const float lse = m + __logf(warp_sum(sum));
+      contrib += lse - x[t];
+#pragma unroll
+      for (int k = 0; k < KV; ++k) {
+        const int i = lane + 64 * k;
+        if (i < P.ld_d) d[i] = f2bf(i < V ? __expf(v[k] - lse) - (i == t ? 1.f : 0.f) : 0.f);
+      }
+    } else {  // V > 1024: three passes over the row
+      float m = -INFINITY;
+      for (int i = lane; i < V; i += 64) m = fmaxf(m, x[i]);
+      m = warp_max(m);
+      float sum = 0.f;
+      for (int i = lane; i < V; i += 64) sum += __expf(x[i] - m);
+      const float lse = m + __logf(warp_sum(sum));
+      contrib += lse - x[t];
+      for (int i = lane; i < P.ld_d; i += 64)
+        d[i] = f2bf(i < V ? __expf(x[i] - lse) - (i == t ? 1.f : 0.f) : 0.f);
     }
   }
   if (lane == 0) part[wave] = contrib;
@@ -310,8 +398,18 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(CeBatch batch, int R) {
 
 hipError_t mmt_launch_ce_fwd(const CeBatch& b, int R, hipStream_t s) {
   if (b.count == 0) return hipSuccess;
-  dim3 grid((R + 3) / 4, 1, b.count);
-  hipLaunchKernelGGL(ce_fwd_kernel, grid, dim3(256), 0, s, b, R);
+  int maxv = 1;
+  for (int g = 0; g < b.count; ++g) maxv = b.p[g].V > maxv ? b.p[g].V : maxv;
+  int blocks = (R + 3) / 4;
+  if (blocks > 512) blocks = 512;
+  dim3 grid(blocks, 1, b.count);
+  const int kv = (maxv + 63) / 64;
+  if (kv <= 1) hipLaunchKernelGGL(ce_fwd_kernel<1>, grid, dim3(256), 0, s, b, R);
+  else if (kv <= 2) hipLaunchKernelGGL(ce_fwd_kernel<2>, grid, dim3(256), 0, s, b, R);
+  else if (kv <= 4) hipLaunchKernelGGL(ce_fwd_kernel<4>, grid, dim3(256), 0, s, b, R);
+  else if (kv <= 8) hipLaunchKernelGGL(ce_fwd_kernel<8>, grid, dim3(256), 0, s, b, R);
+  else if (kv <= 16) hipLaunchKernelGGL(ce_fwd_kernel<16>, grid, dim3(256), 0, s, b, R);
+  else hipLaunchKernelGGL(ce_fwd_kernel<0>, grid, dim3(256), 0, s, b, R);
   return hipGetLastError();
 }
 
@@ -407,20 +505,34 @@ __global__ __launch_bounds__(256) void drop_copy_kernel(DropCopyBatch batch, int
   const DropCopyProblem& P = batch.p[blockIdx.z];
   const int C4 = C >> 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int RPI = 4;  // rows per wave per iteration, loads issued together
   __shared__ float red[4][1024];
+  const int stride = gridDim.x * 4;
   for (int cb = 0; cb < C4; cb += 64) {
     const int q = cb + lane;
     f32x4 sm = {0.f, 0.f, 0.f, 0.f};
     if (q < C4) {
-      for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
-        f32x4 o = reinterpret_cast<const f32x4*>(P.src)[(int64_t)row * C4 + q];
-        if (P.drop_thr) {
+      for (int row0 = blockIdx.x * 4 + wave; row0 < R; row0 += stride * RPI) {
+        f32x4 o[RPI];
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            o[e] = (mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(4 * q + e)) >= P.drop_thr) ? o[e] * P.drop_scale : 0.f;
+        for (int u = 0; u < RPI; ++u) {
+          const int row = row0 + u * stride;
+          o[u] = row < R ? reinterpret_cast<const f32x4*>(P.src)[(int64_t)row * C4 + q] : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        reinterpret_cast<u32x2*>(P.dst)[(int64_t)row * C4 + q] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
-        sm += o;
+#pragma unroll
+        for (int u = 0; u < RPI; ++u) {
+          const int row = row0 + u * stride;
+          if (row >= R) break;
+          if (P.drop_thr) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              o[u][e] = (mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(4 * q + e)) >= P.drop_thr) ? o[u][e] * P.drop_scale
+                                                                                                   : 0.f;
+          }
+          reinterpret_cast<u32x2*>(P.dst)[(int64_t)row * C4 + q] =
+              u32x2{pack2bf(o[u][0], o[u][1]), pack2bf(o[u][2], o[u][3])};
+          sm += o[u];
+        }
       }
       *reinterpret_cast<f32x4*>(&red[wave][4 * q]) = sm;
     }
@@ -433,8 +545,9 @@ __global__ __launch_bounds__(256) void drop_copy_kernel(DropCopyBatch batch, int
 hipError_t mmt_launch_drop_copy(const DropCopyBatch& b, int R, int C, hipStream_t s) {
   if (C % 4 != 0 || C > 1024) return hipErrorInvalidValue;
   if (b.count == 0 || R == 0) return hipSuccess;
+  // one dsum atomic per column per block: cap the blocks (see mmt_launch_ln_bwd)
   int blocks = (R + 15) / 16;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > 256) blocks = 256;
   hipLaunchKernelGGL(drop_copy_kernel, dim3(blocks, 1, b.count), dim3(256), 0, s, b, R, C);
   return hipGetLastError();
 }

@@ -384,7 +384,11 @@ int dw_splits(const GemmBatch& gb, int R) {
   // blocks per CU and no more: launches of <= 8 output tiles split up to 32 ways (>= 8 K-steps of
   // 64 rows each), larger ones at most 8 ways. Measured at C1 (rocprof, grouped launches):
   // 8 tiles 44.5 -> 29.2 us going from 8 to 32 splits, 24 tiles 50.7 -> 64.9 us going from 8 to 22.
-  const int s = (512 + tiles - 1) / tiles;
+  static const int target = [] {
+    const char* e = getenv("MMT_DW_TARGET");  // tuning knob: weight-grad blocks per launch
+    return e ? std::max(1, atoi(e)) : 512;
+  }();
+  const int s = (target + tiles - 1) / tiles;
   const int maxs = std::max(1, std::min(tiles <= 8 ? 32 : 8, R / 512));
   return std::max(1, std::min(s, maxs));
 }

@@ -128,7 +128,7 @@ __device__ __forceinline__ float epi_scalar(const GemmProblem& P, float alpha, i
       EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16) {
     if (P.bias) r += P.bias[n];
   }
-  if (EPI == EPI_BIAS_TANH_BF16) r = tanhf(r);
+  if (EPI == EPI_BIAS_TANH_BF16) r = fast_tanh(r);
   if (EPI == EPI_BIAS_RELU_BF16) r = fmaxf(r, 0.0f);
   if (EPI == EPI_DTANH_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r *= (1.0f - t * t); }
   if (EPI == EPI_DRELU_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r = t > 0.0f ? r : 0.0f; }
@@ -279,13 +279,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
   float alpha = P.alpha;
   if (P.alpha_ptr) alpha *= *P.alpha_ptr;
   const int h = lane >> 5, r = lane & 31;
-  // 16-B (f32) / 8-B (bf16) vector epilogue needs every leading dimension to keep 4-column
-  // groups aligned; bias pointers are 64-B aligned by the parameter layout.
-  const bool vec_ok = ((P.ldc | P.ldres | P.ldo16 | P.ldaux) & 3) == 0;
   if (SWAP) {
-    // Stage the fp32 tile through LDS, then run the epilogue row-major: each wave touches two
-    // whole 128-column row segments per instruction (coalesced bias / aux / resid reads and
-    // output writes) instead of 16 B in each of 32 rows.
+    // Stage the fp32 tile through LDS, then run the epilogue row-major: a thread owns 8
+    // consecutive columns of 8 rows, so every global access is 16 B per lane (bf16 x 8, or
+    // 2 x f32x4) and 16 lanes cover one 128-column row segment. 16-B stores halve the store
+    // instructions of the 8-B form (the epilogue of a short-K tile is store-issue bound).
     // acc[i][j]: rows = n (sub-tile i), cols = m (sub-tile j)
     constexpr int CT = GBN + 4;  // fp32 row stride of the staged tile (16-B aligned, de-conflicted)
     float* ct = reinterpret_cast<float*>(lds);
@@ -304,100 +302,135 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
         }
       }
     __syncthreads();
-    const int c4 = tid & 31;  // 4-column group of this thread
-    const int n = n0 + 4 * c4;
+    const int c8 = tid & 15;     // 8-column group of this thread
+    const int rsub = tid >> 4;   // row within a pass of 16 rows
+    const int n = n0 + 8 * c8;
     constexpr bool HAS_AUX = EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
     constexpr bool HAS_RES = EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32;
-    constexpr int IT = GBM / 8;
+    constexpr bool HAS_BIAS = EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
+                              EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16;
+    constexpr int IT = GBM / 16;
     // fused bias gradient (bf16-output epilogues): column sums of the stored values
     constexpr bool CAN_DB = EPI == EPI_STORE_BF16 || EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
     const bool want_db = CAN_DB && P.dbias != nullptr;
-    float cs[4] = {0.f, 0.f, 0.f, 0.f};
-    if (n + 4 <= N && vec_ok) {
-      // fast path: issue every operand load of this thread's 16 rows first (memory-level
-      // parallelism), then combine and store; full 4-column groups only
-      u32x2 auxv[IT];
-      f32x4 resv[IT];
+    // 16-B vector accesses need bf16 leading dimensions % 8 and fp32 ones % 4 (bias pointers are
+    // 64-B aligned by the parameter layout)
+    const bool vec_ok = ((P.ldo16 | P.ldaux) & 7) == 0 && ((P.ldc | P.ldres) & 3) == 0;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (n + 8 <= N && vec_ok) {
+      // issue every operand load of this thread's rows first (memory-level parallelism)
+      u32x4 auxv[IT];
+      f32x4 resv[IT][2];
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
-        const int m = m0 + it * 8 + (tid >> 5);
+        const int m = m0 + it * 16 + rsub;
         if (m < M) {
-          if (HAS_AUX) auxv[it] = *reinterpret_cast<const u32x2*>(P.aux + (int64_t)m * P.ldaux + n);
-          if (EPI == EPI_BIAS_RESID_F32) resv[it] = *reinterpret_cast<const f32x4*>(P.resid + (int64_t)m * P.ldres + n);
-          if (EPI == EPI_ACC_F32) resv[it] = *reinterpret_cast<const f32x4*>(P.o32 + (int64_t)m * P.ldc + n);
+          if (HAS_AUX) auxv[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
+          const float* rp = EPI == EPI_BIAS_RESID_F32 ? P.resid + (int64_t)m * P.ldres + n
+                                                      : P.o32 + (int64_t)m * P.ldc + n;
+          if (HAS_RES) {
+            resv[it][0] = *reinterpret_cast<const f32x4*>(rp);
+            resv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+          }
         }
       }
-      f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
-      if ((EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
-           EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16) && P.bias)
-        bias4 = *reinterpret_cast<const f32x4*>(P.bias + n);
+      f32x4 bias0 = {0.f, 0.f, 0.f, 0.f}, bias1 = {0.f, 0.f, 0.f, 0.f};
+      if (HAS_BIAS && P.bias) {
+        bias0 = *reinterpret_cast<const f32x4*>(P.bias + n);
+        bias1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
+      }
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
-        const int ml = it * 8 + (tid >> 5);
+        const int ml = it * 16 + rsub;
         const int m = m0 + ml;
         if (m >= M) continue;
-        const f32x4 v4 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 4 * c4);
-        float r[4];
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8 + 4);
+        float r[8];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) r[e] = alpha * v4[e] + bias4[e];
+        for (int e = 0; e < 4; ++e) {
+          r[e] = alpha * v0[e] + bias0[e];
+          r[e + 4] = alpha * v1[e] + bias1[e];
+        }
         if (EPI == EPI_BIAS_TANH_BF16) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) r[e] = tanhf(r[e]);
+          for (int e = 0; e < 8; ++e) r[e] = fast_tanh(r[e]);
         }
         if (EPI == EPI_BIAS_RELU_BF16) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) r[e] = fmaxf(r[e], 0.0f);
+          for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.0f);
         }
         if (HAS_AUX) {
-          const u32x2 a = auxv[it];
-          const float t[4] = {bf2f(a[0] & 0xffff), bf2f(a[0] >> 16), bf2f(a[1] & 0xffff), bf2f(a[1] >> 16)};
+          const u32x4 a = auxv[it];
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            r[e] = (EPI == EPI_DTANH_BF16) ? r[e] * (1.0f - t[e] * t[e]) : (t[e] > 0.0f ? r[e] : 0.0f);
+          for (int q = 0; q < 4; ++q) {
+            const float t0 = bf2f(a[q] & 0xffff), t1 = bf2f(a[q] >> 16);
+            if (EPI == EPI_DTANH_BF16) {
+              r[2 * q] *= (1.0f - t0 * t0);
+              r[2 * q + 1] *= (1.0f - t1 * t1);
+            } else {
+              r[2 * q] = t0 > 0.0f ? r[2 * q] : 0.0f;
+              r[2 * q + 1] = t1 > 0.0f ? r[2 * q + 1] : 0.0f;
+            }
+          }
         }
         if (EPI == EPI_BIAS_RESID_F32 && P.drop_thr) {  // dropout on the branch output, then residual add
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
+          for (int e = 0; e < 8; ++e)
             r[e] = (mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n + e)) >= P.drop_thr) ? r[e] * P.drop_scale : 0.0f;
         }
         if (HAS_RES) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) r[e] += resv[it][e];
+          for (int e = 0; e < 4; ++e) {
+            r[e] += resv[it][0][e];
+            r[e + 4] += resv[it][1][e];
+          }
         }
         if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32 || EPI == EPI_ACC_F32) {
-          *reinterpret_cast<f32x4*>(P.o32 + (int64_t)m * P.ldc + n) = f32x4{r[0], r[1], r[2], r[3]};
+          float* op = P.o32 + (int64_t)m * P.ldc + n;
+          *reinterpret_cast<f32x4*>(op) = f32x4{r[0], r[1], r[2], r[3]};
+          *reinterpret_cast<f32x4*>(op + 4) = f32x4{r[4], r[5], r[6], r[7]};
           if (EPI == EPI_BIAS_RESID_F32 && P.o16)
-            *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
+            *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+                u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
         } else {
-          *reinterpret_cast<u32x2*>(P.o16 + (int64_t)m * P.ldo16 + n) = u32x2{pack2bf(r[0], r[1]), pack2bf(r[2], r[3])};
+          *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+              u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
           if (CAN_DB) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) cs[e] += r[e];
+            for (int e = 0; e < 8; ++e) cs[e] += r[e];
           }
         }
       }
-    } else if (n < N + 4) {
+    } else if (n < N) {
       // edge columns (and unaligned leading dimensions): scalar epilogue + zero pad columns
       for (int it = 0; it < IT; ++it) {
-        const int ml = it * 8 + (tid >> 5);
+        const int ml = it * 16 + rsub;
         const int m = m0 + ml;
         if (m >= M) continue;
-        const f32x4 v4 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 4 * c4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (n + e < N) cs[e] += epi_scalar<EPI>(P, alpha, m, n + e, v4[e]);
+        for (int e = 0; e < 8; ++e) {
+          const float v = ct[ml * CT + 8 * c8 + e];
+          if (n + e < N) cs[e] += epi_scalar<EPI>(P, alpha, m, n + e, v);
           else epi_pad<EPI>(P, m, n + e);
         }
       }
     }
     if (want_db) {
-      // rows of a column live in lanes l, l^32 of every wave: fold those, then the 4 waves via
-      // LDS (the staged tile is dead: every thread has read its own rows), one atomic per column
+      // rows of a column group live in lanes l, l^16, l^32, l^48 of every wave: fold those, then
+      // the 4 waves via LDS (the staged tile is dead: every thread has read its own rows), one
+      // atomic per column
 #pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], 32, 64);
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], 16, 64);
+        cs[e] += __shfl_xor(cs[e], 32, 64);
+      }
       __syncthreads();
       float* red = ct;  // [4 waves][128 columns]
-      if (lane < 32) *reinterpret_cast<f32x4*>(red + wave * GBN + 4 * c4) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      if (lane < 16) {
+        *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+        *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8 + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+      }
       __syncthreads();
       if (tid < GBN && n0 + tid < N)
         atomicAdd(P.dbias + n0 + tid, red[tid] + red[GBN + tid] + red[2 * GBN + tid] + red[3 * GBN + tid]);
