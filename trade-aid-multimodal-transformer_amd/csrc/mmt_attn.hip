@@ -211,11 +211,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, i
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
-  const int bh = blockIdx.y, b = bh / H, head = bh % H;
+  // grid.x = nb * B*H in XCD-aware logical order: the heads of one batch row (halves of the same
+  // Q/K/V cache lines) run on one XCD together
+  const int nb = ((T + 31) / 32 + 7) / 8;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int bh = tile / nb, b = bh / H, head = bh % H;
+  const int bx = tile % nb;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int nt = (T + 31) / 32;
-  const int qt0 = blockIdx.x * 8;
+  const int qt0 = bx * 8;
   const int qmax = min(qt0 + 7, nt - 1);
   const ChunkWalk walk{P.nstreams, (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS};
   const int64_t rowbase = (int64_t)b * T;
@@ -348,11 +353,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
-  const int bh = blockIdx.y, b = bh / H, head = bh % H;
+  // grid.x = nb * B*H in XCD-aware logical order: the heads of one batch row (halves of the same
+  // Q/K/V cache lines) run on one XCD together
+  const int nb = ((T + 31) / 32 + 7) / 8;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int bh = tile / nb, b = bh / H, head = bh % H;
+  const int bx = tile % nb;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int nt = (T + 31) / 32;
-  const int qt0 = blockIdx.x * 8;
+  const int qt0 = bx * 8;
   const int qmax = min(qt0 + 7, nt - 1);
   const ChunkWalk walk{P.nstreams, (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS};
   const int64_t rowbase = (int64_t)b * T;
@@ -491,15 +501,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBatch batch, int
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
-  const int nbh = gridDim.y / P.nstreams;
-  if ((int)blockIdx.y >= nbh * P.nstreams) return;
-  const int j = blockIdx.y / nbh;
-  const int bh = blockIdx.y % nbh;
+  const int nb = ((T + 31) / 32 + 7) / 8;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int yy = tile / nb, bx = tile % nb;
+  const int nbh = gridDim.x / nb / P.nstreams;
+  if (yy >= nbh * P.nstreams) return;
+  const int j = yy / nbh;
+  const int bh = yy % nbh;
   const int b = bh / H, head = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int nt = (T + 31) / 32;
-  const int kt0 = blockIdx.x * 8;
+  const int kt0 = bx * 8;
   const int q_lo = kt0 * 32;
   const ChunkWalk walk{1, (T - q_lo + ROWS - 1) / ROWS};
   const bool ragged = (T & 31) != 0;
@@ -602,11 +615,11 @@ template <int HS>
 static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
   const int nb = ((T + 31) / 32 + 7) / 8;
   if (!bwd) {
-    hipLaunchKernelGGL(attn_fwd_kernel<HS>, dim3(nb, B * H, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    hipLaunchKernelGGL(attn_fwd_kernel<HS>, dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
   } else {
     const int ns = bt.p[0].nstreams;
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<HS>, dim3(nb, B * H, bt.count), dim3(256), 0, s, bt, T, H, scale);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HS>, dim3(nb, B * H * ns, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<HS>, dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HS>, dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
   }
 }
 

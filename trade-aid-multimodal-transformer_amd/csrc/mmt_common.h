@@ -72,6 +72,15 @@ __device__ __forceinline__ bf16x8 join4(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// XCD-aware block order (bijective): hardware block ids b and b+8 share an XCD (and its L2);
+// give each XCD a contiguous run of logical tiles so neighbouring tiles that read the two halves of
+// the same cache lines (adjacent heads / Q-K-V blocks of one row) run on one XCD at nearly the
+// same time. Returns the logical tile of hardware block `bid` out of `nwg`.
+__device__ __forceinline__ int xcd_tile(int bid, int nwg) {
+  const int x = bid % 8, q = nwg / 8, rr = nwg % 8;
+  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + bid / 8;
+}
+
 // counter-based hash RNG (dropout masks); identical in forward and backward, and restated
 // bit-for-bit by the host (mmt_engine.hip: drop keys) and by oracle/mmt_oracle.py (mask_hash)
 #define MMT_STREAM_SALT 0x5BD1E995u

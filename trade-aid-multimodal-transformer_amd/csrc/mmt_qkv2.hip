@@ -35,10 +35,13 @@ __global__ __launch_bounds__(256) void qkv2_fwd_mfma(Qkv2Batch batch, int R, int
   constexpr int NOT = (HS + 31) / 32;  // output (o) tiles
   constexpr int KS = (HH + 15) / 16;   // k-steps over i
   const Qkv2Problem& P = batch.p[blockIdx.z];
-  const int blk = blockIdx.y;
+  // grid.x = row blocks x nblk, blk fastest in logical order (one row's blocks share its lines)
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int nblk = gridDim.x / ((R + 127) / 128);
+  const int blk = tile % nblk, rb = tile / nblk;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int row = blockIdx.x * 128 + w * 32 + r;
+  const int row = rb * 128 + w * 32 + r;
   const float* w2 = P.w2 + (int64_t)blk * HS * HH;
   // B operand: h1[row][i = 16s + 8h + j]
   bf16x8 hb[KS];
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(256) void qkv2_fwd_mfma(Qkv2Batch batch, int R, int
       acc = mfma32(wa, hb[s], acc);  // D[o][row]
     }
     // lane owns row (r) and o = ot*32 + (e&3) + 8(e>>2) + 4h
-    const int orow = blockIdx.x * 128 + w * 32 + r;
+    const int orow = rb * 128 + w * 32 + r;
     if (orow < R) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -102,8 +105,10 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
   constexpr int SHW = 32 + 16;                    // sh row: 32 cols (HH valid) + pad
   constexpr int KSD = (HS + 15) / 16;             // k-steps over o for dh1
   const Qkv2Problem& P = batch.p[blockIdx.z];
-  const int blk = blockIdx.y;
-  const int r0 = blockIdx.x * 256;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int nblk = gridDim.x / ((R + 255) / 256);
+  const int blk = tile % nblk;
+  const int r0 = (tile / nblk) * 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   __shared__ __attribute__((aligned(16))) bf16_t sd[256 * SDW];
@@ -201,8 +206,10 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
 
 template <int HS>
 static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_out, bool bwd, hipStream_t s) {
-  if (bwd) hipLaunchKernelGGL(qkv2_bwd_mfma<HS>, dim3((R + 255) / 256, nblk, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
-  else hipLaunchKernelGGL(qkv2_fwd_mfma<HS>, dim3((R + 127) / 128, nblk, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
+  if (bwd)
+    hipLaunchKernelGGL(qkv2_bwd_mfma<HS>, dim3((R + 255) / 256 * nblk, 1, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
+  else
+    hipLaunchKernelGGL(qkv2_fwd_mfma<HS>, dim3((R + 127) / 128 * nblk, 1, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
 }
 
 static hipError_t qkv2_dispatch(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, bool bwd,
