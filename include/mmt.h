@@ -131,10 +131,16 @@ int mmt_batch_gather(void* stream, int32_t nmod, const int32_t* const* data, con
 /* GEMM pipeline variant (tuning knob, process-wide): 0 = K-step 64 x 2 LDS stages (default),
  * 1 = 32 x 2, 2 = 32 x 3, 3 = 32 x 4, 4 = 64 x 3 */
 int mmt_gemm_set_variant(int variant);
+/* splits: split-K factor of EPI atomic_f32 launches (<= 0: automatic) */
 int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t splits, int32_t M, int32_t N,
                 int32_t K, const void* A, int32_t lda, const void* B, int32_t ldb, const float* bias,
                 const void* aux, int32_t ldaux, const float* resid, int32_t ldres, float* o32, int32_t ldc,
                 void* o16, int32_t ldo16, float alpha);
+/* weight gradient out[M, N] += alpha * A[K, M]^T B[K, N] (A, B bf16, MN-contiguous rows of K):
+ * split-K into fp32 slabs in `slab` (device scratch of slab_bytes; NULL/0: one K pass) + a reduce
+ * pass, the engine's path for every dW of the backward */
+int mmt_op_gemm_wgrad(void* stream, int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, const void* B,
+                      int32_t ldb, float* out, int32_t ldc, float alpha, void* slab, int64_t slab_bytes);
 int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
                          void* y16, float* mean, float* rstd);
 int mmt_op_layernorm_bwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* mean,

@@ -46,6 +46,9 @@ SHAPES = [
     ("ffn_dw16k_s1_atomic", 0, 0, "atomic_f32", 1024, 256, 16384, 1),
     ("ffn_dw2k_s1_store", 0, 0, "store_f32", 1024, 256, 2048, 1),
     ("ffn_dw2k_s1_atomic", 0, 0, "atomic_f32", 1024, 256, 2048, 1),
+    # per-CU main-loop rate: one block per output tile over a long K (16 or 64 blocks)
+    ("rate_1k_16k_s1", 0, 0, "store_f32", 1024, 1024, 16384, 1),
+    ("rate_1k_16k_kc", 1, 1, "store_f32", 1024, 1024, 16384, 1),
 ]
 if os.environ.get("GEMM_BENCH_ONLY"):
     SHAPES = [s for s in SHAPES if any(k in s[0] for k in os.environ["GEMM_BENCH_ONLY"].split(","))]

@@ -67,6 +67,7 @@ struct Plan {
   int B = -1;
   size_t total = 0;
   size_t pack = 0;
+  size_t slab = 0, slab_bytes = 0;  // split-K slabs of the weight-gradient GEMMs
   std::vector<ActLM> act;  // [L*M]
   size_t xemb[MAXM];
   size_t lnf16[MAXM], meanf[MAXM], rstdf[MAXM], hh[MAXM], dlog[MAXM];
@@ -347,6 +348,17 @@ void make_plan(mmt_ctx* c, int B) {
     if (c->any_cross && c->cfg.cross_attention[i])
       for (int j = 0; j < M - 1; ++j) p.dkv[i][j] = A(R * 2 * C * b2);
   }
+  // weight-gradient split-K slabs: room for 16 splits of the largest grouped dW launch
+  {
+    int64_t mx = 0, heads = 0;
+    mx = std::max<int64_t>(mx, (int64_t)M * 4 * C * C);                  // FFN (either matrix)
+    mx = std::max<int64_t>(mx, (int64_t)M * r8(3 * H * c->hh) * C);      // Q/K/V stage 1
+    mx = std::max<int64_t>(mx, (int64_t)MMT_MAX_GROUP * 2 * C * C);      // cross-attention KV
+    for (int i = 0; i < M; ++i) heads += (int64_t)c->V[i] * (c->V[i] / 2 + 4) + (int64_t)(c->V[i] / 2 + 4) * C;
+    mx = std::max<int64_t>(mx, heads);
+    p.slab_bytes = (size_t)mx * 16 * f4;
+    p.slab = A(p.slab_bytes);
+  }
   p.total = cur;
 }
 
@@ -373,24 +385,6 @@ GemmProblem gp_dw(const bf16_t* dY, int ldy, const bf16_t* X, int ldx, float* gr
   g.A = dY; g.lda = ldy; g.B = X; g.ldb = ldx;
   g.M = W.rows; g.N = W.cols; g.K = R; g.o32 = grads + W.off; g.ldc = W.cols; g.alpha = 1.f;
   return g;
-}
-
-int dw_splits(const GemmBatch& gb, int R) {
-  int tiles = 0;
-  for (int g = 0; g < gb.count; ++g)
-    tiles += ((gb.p[g].M + 127) / 128) * ((gb.p[g].N + 127) / 128);
-  if (tiles <= 0) return 1;
-  // every split adds one fp32 atomic per output element and a per-block epilogue, so aim at ~2
-  // blocks per CU and no more: launches of <= 8 output tiles split up to 32 ways (>= 8 K-steps of
-  // 64 rows each), larger ones at most 8 ways. Measured at C1 (rocprof, grouped launches):
-  // 8 tiles 44.5 -> 29.2 us going from 8 to 32 splits, 24 tiles 50.7 -> 64.9 us going from 8 to 22.
-  static const int target = [] {
-    const char* e = getenv("MMT_DW_TARGET");  // tuning knob: weight-grad blocks per launch
-    return e ? std::max(1, atoi(e)) : 512;
-  }();
-  const int s = (target + tiles - 1) / tiles;
-  const int maxs = std::max(1, std::min(tiles <= 8 ? 32 : 8, R / 512));
-  return std::max(1, std::min(s, maxs));
 }
 
 // dropout sites (model.py:69 SA probabilities, :91 SA projection, :151 CA probabilities,
@@ -444,7 +438,7 @@ struct Runner {
   void dwgemm(const GemmBatch& b, const char* what) {
     if (rc != MMT_OK) return;
     probe_begin(what);
-    ok(mmt_launch_gemm(b, false, false, EPI_ATOMIC_F32, dw_splits(b, R), s), what);
+    ok(mmt_launch_gemm_wgrad(b, W<float>(c->plan.slab), (int64_t)c->plan.slab_bytes, s), what);
     probe_end(what);
   }
   template <class T> T* W(size_t off) { return at<T>(ws, off); }

@@ -21,10 +21,25 @@
 #include "mmt_common.h"
 #include "mmt_kernels.h"
 
+#include <stdlib.h>
+
+#include <algorithm>
 #include <type_traits>
 
-#define GBM 128
-#define GBN 128
+// Block tile configurations: WM x WN waves, each wave TM x TN MFMA 32x32 sub-tiles.
+template <int WM_, int WN_, int TM_, int TN_>
+struct TileCfg {
+  static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+};
+// 128 x 128, 4 waves of 64 x 64: short-K shapes (2 blocks per CU overlap one block's prologue
+// and epilogue with the other's main loop)
+using TileS = TileCfg<2, 2, 2, 2>;
+// 256 x 256, 8 waves (2 x 4) of 128 x 64: 32 MFMAs per wave per 64-deep K-step, so the one
+// stage in flight has ~2 k cycles of matrix work per SIMD to land behind (long-K shapes, weight
+// gradients); 128 KiB ring -> 1 block per CU
+using TileL = TileCfg<2, 4, 4, 2>;
 
 // tuning knob (mmt_gemm_set_variant): pipeline variant of the forward / backward-data GEMMs in
 // bits 0-3 and of the weight-grad (split-K, atomic) GEMMs in bits 4-7:
@@ -75,12 +90,15 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 }
 
 // issue this wave's LDS-DMA pieces (1 KiB each) of one operand tile for K-step k0.
-// the tile (128 x BK bf16) has BK/4 pieces, BK/16 per wave; lane L writes LDS bytes [i*1024 + 16L, +16).
-template <int BK, bool KC>
+// the tile (ROWS x BK bf16) has ROWS*BK/512 pieces, split over NW waves; lane L writes LDS bytes
+// [i*1024 + 16L, +16).
+template <int BK, bool KC, int ROWS, int NW>
 __device__ __forceinline__ void issue_tile(const i32x4& rsrc, char* img, int ld, int rows_total, int K,
                                            int r0, int k0, int wave, int lane) {
-  constexpr int PPW = BK / 16;  // pieces per wave
-  constexpr int CPR = BK / 8;   // chunks per K-contiguous row
+  constexpr int PPW = ROWS * BK / 512 / NW;  // pieces per wave
+  constexpr int CPR = BK / 8;                // chunks per K-contiguous row
+  constexpr int CPK = ROWS / 8;              // chunks per k-row of an MN-contiguous image
+  static_assert(PPW >= 1 && CPK >= 16, "tile geometry");
 #pragma unroll
   for (int u = 0; u < PPW; ++u) {
     const int i = wave * PPW + u;
@@ -91,8 +109,8 @@ __device__ __forceinline__ void issue_tile(const i32x4& rsrc, char* img, int ld,
       const int grow = r0 + row, gk = k0 + chunk * 8;
       voff = (grow < rows_total && gk < K) ? (grow * ld + gk) * 2 : 0x7fffffff;
     } else {
-      const int kr = 4 * i + (lane >> 4);
-      const int chunk = (lane & 15) ^ ((kr & 3) << 2);
+      const int kr = (64 / CPK) * i + lane / CPK;
+      const int chunk = (lane % CPK) ^ ((kr & 3) << 2);
       const int gk = k0 + kr, gcol = r0 + chunk * 8;
       voff = (gk < K && gcol < rows_total) ? (gk * ld + gcol) * 2 : 0x7fffffff;
     }
@@ -101,7 +119,7 @@ __device__ __forceinline__ void issue_tile(const i32x4& rsrc, char* img, int ld,
 }
 
 // fragment for "lane row = sb + (lane&31), k = 16*s + 8*(lane>>5) + j" from a staged image
-template <int BK, bool KC>
+template <int BK, bool KC, int ROWS>
 __device__ __forceinline__ bf16x8 frag(const char* img, int sb, int s, int lane) {
   if (KC) {
     const int row = sb + (lane & 31);
@@ -114,15 +132,15 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int sb, int s, int lane)
     const int kr = 16 * s + 8 * (g >> 1) + q;  // kr & 3 == q ; (kr + 4) & 3 == q
     const int ch = (col >> 3) ^ (q << 2);
     const int within = (col & 7) * 2;
-    const s16x4 lo = lds_tr16(img + kr * (GBM * 2) + ch * 16 + within);
-    const s16x4 hi = lds_tr16(img + (kr + 4) * (GBM * 2) + ch * 16 + within);
+    const s16x4 lo = lds_tr16(img + kr * (ROWS * 2) + ch * 16 + within);
+    const s16x4 hi = lds_tr16(img + (kr + 4) * (ROWS * 2) + ch * 16 + within);
     return join4(lo, hi);
   }
 }
 
 // one output element; returns the value stored (the bias-gradient column sum adds it up)
 template <int EPI>
-__device__ __forceinline__ float epi_scalar(const GemmProblem& P, float alpha, int m, int n, float v) {
+__device__ __forceinline__ float epi_scalar(const GemmProblem& P, float* o32, float alpha, int m, int n, float v) {
   float r = alpha * v;
   if (EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
       EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16) {
@@ -137,10 +155,10 @@ __device__ __forceinline__ float epi_scalar(const GemmProblem& P, float alpha, i
     r += P.resid[(int64_t)m * P.ldres + n];
   }
   const int64_t o = (int64_t)m * P.ldc + n;
-  if (EPI == EPI_ACC_F32) { P.o32[o] += r; return r; }
-  if (EPI == EPI_ATOMIC_F32) { atomicAdd(P.o32 + o, r); return r; }
+  if (EPI == EPI_ACC_F32) { o32[o] += r; return r; }
+  if (EPI == EPI_ATOMIC_F32) { atomicAdd(o32 + o, r); return r; }
   if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32) {
-    P.o32[o] = r;
+    o32[o] = r;
     if (EPI == EPI_BIAS_RESID_F32 && P.o16) P.o16[(int64_t)m * P.ldo16 + n] = f2bf(r);
     return r;
   }
@@ -170,11 +188,13 @@ __device__ __forceinline__ void wait_vm(int n) {
   }
 }
 
-template <int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
-  constexpr int IMG_BYTES = GBM * BK * 2;  // per operand per stage (both layouts)
-  constexpr int STAGE_BYTES = 2 * IMG_BYTES;
-  constexpr int PIECES = BK / 8;           // LDS-DMA pieces per wave per stage (A + B)
+template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
+__global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
+  constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
+  constexpr int IMG_A = GBM * BK * 2, IMG_B = GBN * BK * 2;  // per operand per stage (both layouts)
+  constexpr int STAGE_BYTES = IMG_A + IMG_B;
+  constexpr int PIECES = (GBM + GBN) * BK / 512 / NW;        // LDS-DMA pieces per wave per stage (A + B)
+  constexpr int AI = SWAP ? TN : TM, AJ = SWAP ? TM : TN;    // accumulator sub-tile grid
   const GemmProblem& P = batch.p[blockIdx.z];
   const int M = P.M, N = P.N, K = P.K;
   const int tiles_n = (N + GBN - 1) / GBN;
@@ -196,23 +216,24 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
   const int kper = (ksteps + nsplit - 1) / nsplit;
   const int ks0 = blockIdx.y * kper;
   const int ks1 = min(ksteps, ks0 + kper);
-  if (EPI == EPI_ATOMIC_F32 && ks0 >= ks1) return;  // nothing to add
+  if (EPI == EPI_ATOMIC_F32 && ks0 >= ks1) return;  // nothing to add (a slab split still writes its zeros)
 
   // one LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads):
-  // the stage ring during the K loop, the fp32 output tile (128 x 132) in the epilogue
-  constexpr int RING = ST * STAGE_BYTES, CTILE = GBM * (GBN + 4) * 4;
+  // the stage ring during the K loop, the fp32 output tile (EPI_ROWS x (GBN + 4)) in the epilogue
+  constexpr int EPI_ROWS = GBM == 128 ? 128 : 64;
+  constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
   __shared__ __attribute__((aligned(1024))) char lds[RING > CTILE ? RING : CTILE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
 
-  f32x16 acc[2][2];
+  f32x16 acc[AI][AJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < AI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < AJ; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
@@ -236,22 +257,22 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
       if (tt + ST - 1 < nk) {
         char* st = lds + ((U + ST - 1) % ST) * STAGE_BYTES;
         const int k0 = (ks0 + tt + ST - 1) * BK;
-        issue_tile<BK, A_KC>(ra, st, P.lda, M, K, m0, k0, wave, lane);
-        issue_tile<BK, B_KC>(rb, st + IMG_BYTES, P.ldb, N, K, n0, k0, wave, lane);
+        issue_tile<BK, A_KC, GBM, NW>(ra, st, P.lda, M, K, m0, k0, wave, lane);
+        issue_tile<BK, B_KC, GBN, NW>(rb, st + IMG_A, P.ldb, N, K, n0, k0, wave, lane);
       }
       const char* imgA = lds + U * STAGE_BYTES;
-      const char* imgB = imgA + IMG_BYTES;
+      const char* imgB = imgA + IMG_A;
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
-        bf16x8 fa[2], fb[2];
+        bf16x8 fa[TM], fb[TN];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fa[j] = frag<BK, A_KC>(imgA, wm * 64 + 32 * j, s, lane);
+        for (int j = 0; j < TM; ++j) fa[j] = frag<BK, A_KC, GBM>(imgA, wm * TM * 32 + 32 * j, s, lane);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) fb[i] = frag<BK, B_KC>(imgB, wn * 64 + 32 * i, s, lane);
+        for (int i = 0; i < TN; ++i) fb[i] = frag<BK, B_KC, GBN>(imgB, wn * TN * 32 + 32 * i, s, lane);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < AI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < AJ; ++j) {
             if (SWAP) acc[i][j] = mfma32(fb[i], fa[j], acc[i][j]);
             else acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
           }
@@ -261,8 +282,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
     for (int t = 0; t < ST - 1; ++t)
       if (t < nk) {
         char* st = lds + t * STAGE_BYTES;
-        issue_tile<BK, A_KC>(ra, st, P.lda, M, K, m0, (ks0 + t) * BK, wave, lane);
-        issue_tile<BK, B_KC>(rb, st + IMG_BYTES, P.ldb, N, K, n0, (ks0 + t) * BK, wave, lane);
+        issue_tile<BK, A_KC, GBM, NW>(ra, st, P.lda, M, K, m0, (ks0 + t) * BK, wave, lane);
+        issue_tile<BK, B_KC, GBN, NW>(rb, st + IMG_A, P.ldb, N, K, n0, (ks0 + t) * BK, wave, lane);
       }
     int t = 0;
     for (; t + ST <= nk; t += ST) {
@@ -278,38 +299,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
 
   float alpha = P.alpha;
   if (P.alpha_ptr) alpha *= *P.alpha_ptr;
+  // split-K into slabs: split s of the K loop writes its own fp32 slab (reduced by mmt_gemm_slab_reduce)
+  float* o32 = P.o32 + (P.split_stride ? (int64_t)blockIdx.y * P.split_stride : (int64_t)0);
   const int h = lane >> 5, r = lane & 31;
   if (SWAP) {
-    // Stage the fp32 tile through LDS, then run the epilogue row-major: a thread owns 8
-    // consecutive columns of 8 rows, so every global access is 16 B per lane (bf16 x 8, or
-    // 2 x f32x4) and 16 lanes cover one 128-column row segment. 16-B stores halve the store
-    // instructions of the 8-B form (the epilogue of a short-K tile is store-issue bound).
+    // Stage the fp32 tile through LDS (EPI_ROWS rows per pass), then run the epilogue row-major:
+    // a thread owns 8 consecutive columns, so every global access is 16 B per lane (bf16 x 8, or
+    // 2 x f32x4) and GBN/8 lanes cover one row segment. 16-B stores halve the store instructions
+    // of the 8-B form (the epilogue of a short-K tile is store-issue bound).
     // acc[i][j]: rows = n (sub-tile i), cols = m (sub-tile j)
     constexpr int CT = GBN + 4;  // fp32 row stride of the staged tile (16-B aligned, de-conflicted)
+    constexpr int TPR = GBN / 8;          // threads per row
+    constexpr int RPI = NT / TPR;         // rows per iteration
+    constexpr int IT = EPI_ROWS / RPI;    // iterations per pass
     float* ct = reinterpret_cast<float*>(lds);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave's last fragment reads of the stage ring are done
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ml = wm * 64 + 32 * j + r;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int nl = wn * 64 + 32 * i + 8 * g + 4 * h;
-          *reinterpret_cast<f32x4*>(ct + ml * CT + nl) =
-              f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-        }
-      }
-    __syncthreads();
-    const int c8 = tid & 15;     // 8-column group of this thread
-    const int rsub = tid >> 4;   // row within a pass of 16 rows
+    const int c8 = tid % TPR;   // 8-column group of this thread
+    const int rsub = tid / TPR; // row within an iteration
     const int n = n0 + 8 * c8;
     constexpr bool HAS_AUX = EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
     constexpr bool HAS_RES = EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32;
     constexpr bool HAS_BIAS = EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
                               EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16;
-    constexpr int IT = GBM / 16;
     // fused bias gradient (bf16-output epilogues): column sums of the stored values
     constexpr bool CAN_DB = EPI == EPI_STORE_BF16 || EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
     const bool want_db = CAN_DB && P.dbias != nullptr;
@@ -317,204 +327,378 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch) {
     // 64-B aligned by the parameter layout)
     const bool vec_ok = ((P.ldo16 | P.ldaux) & 7) == 0 && ((P.ldc | P.ldres) & 3) == 0;
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (n + 8 <= N && vec_ok) {
-      // issue every operand load of this thread's rows first (memory-level parallelism)
-      u32x4 auxv[IT];
-      f32x4 resv[IT][2];
+    f32x4 bias0 = {0.f, 0.f, 0.f, 0.f}, bias1 = {0.f, 0.f, 0.f, 0.f};
+    if (HAS_BIAS && P.bias && n + 8 <= N) {
+      bias0 = *reinterpret_cast<const f32x4*>(P.bias + n);
+      bias1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 1
+    for (int pass = 0; pass < GBM / EPI_ROWS; ++pass) {
+      __syncthreads();  // stage-ring / previous pass reads done
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int m = m0 + it * 16 + rsub;
-        if (m < M) {
-          if (HAS_AUX) auxv[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
-          const float* rp = EPI == EPI_BIAS_RESID_F32 ? P.resid + (int64_t)m * P.ldres + n
-                                                      : P.o32 + (int64_t)m * P.ldc + n;
-          if (HAS_RES) {
-            resv[it][0] = *reinterpret_cast<const f32x4*>(rp);
-            resv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const int mf = wm * TM * 32 + 32 * j;  // first row of this sub-tile in the block tile
+          if (mf / EPI_ROWS != pass) continue;
+          const int ml = mf - pass * EPI_ROWS + r;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int nl = wn * TN * 32 + 32 * i + 8 * g + 4 * h;
+            *reinterpret_cast<f32x4*>(ct + ml * CT + nl) =
+                f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
           }
         }
-      }
-      f32x4 bias0 = {0.f, 0.f, 0.f, 0.f}, bias1 = {0.f, 0.f, 0.f, 0.f};
-      if (HAS_BIAS && P.bias) {
-        bias0 = *reinterpret_cast<const f32x4*>(P.bias + n);
-        bias1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
-      }
+      __syncthreads();
+      const int mb = m0 + pass * EPI_ROWS;
+      if (n + 8 <= N && vec_ok) {
+        // issue every operand load of this thread's rows first (memory-level parallelism)
+        u32x4 auxv[IT];
+        f32x4 resv[IT][2];
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int ml = it * 16 + rsub;
-        const int m = m0 + ml;
-        if (m >= M) continue;
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8);
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8 + 4);
-        float r[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          r[e] = alpha * v0[e] + bias0[e];
-          r[e + 4] = alpha * v1[e] + bias1[e];
-        }
-        if (EPI == EPI_BIAS_TANH_BF16) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) r[e] = fast_tanh(r[e]);
-        }
-        if (EPI == EPI_BIAS_RELU_BF16) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.0f);
-        }
-        if (HAS_AUX) {
-          const u32x4 a = auxv[it];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float t0 = bf2f(a[q] & 0xffff), t1 = bf2f(a[q] >> 16);
-            if (EPI == EPI_DTANH_BF16) {
-              r[2 * q] *= (1.0f - t0 * t0);
-              r[2 * q + 1] *= (1.0f - t1 * t1);
-            } else {
-              r[2 * q] = t0 > 0.0f ? r[2 * q] : 0.0f;
-              r[2 * q + 1] = t1 > 0.0f ? r[2 * q + 1] : 0.0f;
+        for (int it = 0; it < IT; ++it) {
+          const int m = mb + it * RPI + rsub;
+          if (m < M) {
+            if (HAS_AUX) auxv[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
+            const float* rp = EPI == EPI_BIAS_RESID_F32 ? P.resid + (int64_t)m * P.ldres + n
+                                                        : o32 + (int64_t)m * P.ldc + n;
+            if (HAS_RES) {
+              resv[it][0] = *reinterpret_cast<const f32x4*>(rp);
+              resv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
             }
           }
         }
-        if (EPI == EPI_BIAS_RESID_F32 && P.drop_thr) {  // dropout on the branch output, then residual add
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
-            r[e] = (mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n + e)) >= P.drop_thr) ? r[e] * P.drop_scale : 0.0f;
-        }
-        if (HAS_RES) {
+        for (int it = 0; it < IT; ++it) {
+          const int ml = it * RPI + rsub;
+          const int m = mb + ml;
+          if (m >= M) continue;
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8);
+          const f32x4 v1 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8 + 4);
+          float r[8];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            r[e] += resv[it][0][e];
-            r[e + 4] += resv[it][1][e];
+            r[e] = alpha * v0[e] + bias0[e];
+            r[e + 4] = alpha * v1[e] + bias1[e];
           }
-        }
-        if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32 || EPI == EPI_ACC_F32) {
-          float* op = P.o32 + (int64_t)m * P.ldc + n;
-          *reinterpret_cast<f32x4*>(op) = f32x4{r[0], r[1], r[2], r[3]};
-          *reinterpret_cast<f32x4*>(op + 4) = f32x4{r[4], r[5], r[6], r[7]};
-          if (EPI == EPI_BIAS_RESID_F32 && P.o16)
+          if (EPI == EPI_BIAS_TANH_BF16) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] = fast_tanh(r[e]);
+          }
+          if (EPI == EPI_BIAS_RELU_BF16) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.0f);
+          }
+          if (HAS_AUX) {
+            const u32x4 a = auxv[it];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float t0 = bf2f(a[q] & 0xffff), t1 = bf2f(a[q] >> 16);
+              if (EPI == EPI_DTANH_BF16) {
+                r[2 * q] *= (1.0f - t0 * t0);
+                r[2 * q + 1] *= (1.0f - t1 * t1);
+              } else {
+                r[2 * q] = t0 > 0.0f ? r[2 * q] : 0.0f;
+                r[2 * q + 1] = t1 > 0.0f ? r[2 * q + 1] : 0.0f;
+              }
+            }
+          }
+          if (EPI == EPI_BIAS_RESID_F32 && P.drop_thr) {  // dropout on the branch output, then residual add
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              r[e] = (mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n + e)) >= P.drop_thr) ? r[e] * P.drop_scale : 0.0f;
+          }
+          if (HAS_RES) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              r[e] += resv[it][0][e];
+              r[e + 4] += resv[it][1][e];
+            }
+          }
+          if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32 || EPI == EPI_ACC_F32) {
+            float* op = o32 + (int64_t)m * P.ldc + n;
+            *reinterpret_cast<f32x4*>(op) = f32x4{r[0], r[1], r[2], r[3]};
+            *reinterpret_cast<f32x4*>(op + 4) = f32x4{r[4], r[5], r[6], r[7]};
+            if (EPI == EPI_BIAS_RESID_F32 && P.o16)
+              *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+                  u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+          } else {
             *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
                 u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
-        } else {
-          *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
-              u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
-          if (CAN_DB) {
+            if (CAN_DB) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) cs[e] += r[e];
+              for (int e = 0; e < 8; ++e) cs[e] += r[e];
+            }
           }
         }
-      }
-    } else if (n < N) {
-      // edge columns (and unaligned leading dimensions): scalar epilogue + zero pad columns
-      for (int it = 0; it < IT; ++it) {
-        const int ml = it * 16 + rsub;
-        const int m = m0 + ml;
-        if (m >= M) continue;
+      } else if (n < N) {
+        // edge columns (and unaligned leading dimensions): scalar epilogue + zero pad columns
+        for (int it = 0; it < IT; ++it) {
+          const int ml = it * RPI + rsub;
+          const int m = mb + ml;
+          if (m >= M) continue;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = ct[ml * CT + 8 * c8 + e];
-          if (n + e < N) cs[e] += epi_scalar<EPI>(P, alpha, m, n + e, v);
-          else epi_pad<EPI>(P, m, n + e);
+          for (int e = 0; e < 8; ++e) {
+            const float v = ct[ml * CT + 8 * c8 + e];
+            if (n + e < N) cs[e] += epi_scalar<EPI>(P, o32, alpha, m, n + e, v);
+            else epi_pad<EPI>(P, m, n + e);
+          }
         }
       }
     }
     if (want_db) {
-      // rows of a column group live in lanes l, l^16, l^32, l^48 of every wave: fold those, then
-      // the 4 waves via LDS (the staged tile is dead: every thread has read its own rows), one
-      // atomic per column
+      // rows of a column group live in lanes l, l^TPR, ... of every wave: fold those, then the
+      // waves via LDS (the staged tile is dead: every thread has read its own rows), one atomic
+      // per column
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        cs[e] += __shfl_xor(cs[e], 16, 64);
-        cs[e] += __shfl_xor(cs[e], 32, 64);
-      }
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = TPR; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
       __syncthreads();
-      float* red = ct;  // [4 waves][128 columns]
-      if (lane < 16) {
+      float* red = ct;  // [NW waves][GBN columns]
+      if (lane < TPR) {
         *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8) = f32x4{cs[0], cs[1], cs[2], cs[3]};
         *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8 + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
       }
       __syncthreads();
-      if (tid < GBN && n0 + tid < N)
-        atomicAdd(P.dbias + n0 + tid, red[tid] + red[GBN + tid] + red[2 * GBN + tid] + red[3 * GBN + tid]);
+      if (tid < GBN && n0 + tid < N) {
+        float sum = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) sum += red[w * GBN + tid];
+        atomicAdd(P.dbias + n0 + tid, sum);
+      }
     }
   } else {
     // acc[i][j]: rows = m (sub-tile i), cols = n (sub-tile j)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + 32 * j + r;
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * TN * 32 + 32 * j + r;
         if (n >= N) continue;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wm * 64 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (m < M) epi_scalar<EPI>(P, alpha, m, n, acc[i][j][e]);
+          const int m = m0 + wm * TM * 32 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (m < M) epi_scalar<EPI>(P, o32, alpha, m, n, acc[i][j][e]);
         }
       }
   }
 }
 
-template <int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
+template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
 static void launch_v(const GemmBatch& b, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<BK, ST, A_KC, B_KC, SWAP, EPI>), grid, dim3(256), 0, s, b);
+  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI>), grid, dim3(TL::NT), 0, s, b);
 }
 
-template <bool A_KC, bool B_KC, bool SWAP, int EPI>
-static hipError_t launch_t(const GemmBatch& b, int splits, hipStream_t s) {
-  int maxtiles = 0;
+template <class TL>
+static int max_tiles(const GemmBatch& b, int* total) {
+  int maxtiles = 0, sum = 0;
   for (int g = 0; g < b.count; ++g) {
     const GemmProblem& P = b.p[g];
-    const int t = ((P.M + GBM - 1) / GBM) * ((P.N + GBN - 1) / GBN);
-    if (t > maxtiles) maxtiles = t;
+    const int t = ((P.M + TL::BM - 1) / TL::BM) * ((P.N + TL::BN - 1) / TL::BN);
+    maxtiles = t > maxtiles ? t : maxtiles;
+    sum += t;
   }
-  if (maxtiles == 0 || b.count == 0) return hipSuccess;
-  dim3 grid(maxtiles, splits, b.count);
+  if (total) *total = sum;
+  return maxtiles;
+}
+
+// split-K factor of a weight-gradient launch (splits <= 0: automatic). Every split adds one fp32
+// atomic per output element and an epilogue, so aim at ~2 blocks per CU for the 128x128 tile and
+// ~1 for the 256x256 one, keeping >= 8 K-steps per split. Measured at C1 (128x128, grouped
+// launches): 8 tiles 44.5 -> 29.2 us going from 8 to 32 splits, 24 tiles 50.7 -> 64.9 us from 8 to 22.
+template <class TL>
+static int auto_splits(const GemmBatch& b, int splits) {
+  if (splits > 0) return splits;
+  int tiles = 0, maxk = 0;
+  max_tiles<TL>(b, &tiles);
+  for (int g = 0; g < b.count; ++g) maxk = b.p[g].K > maxk ? b.p[g].K : maxk;
+  if (tiles <= 0) return 1;
+  const int target = TL::BM == 128 ? 512 : 256;
+  const int cap = TL::BM == 128 ? (tiles <= 8 ? 32 : 8) : 32;
+  const int s = (target + tiles - 1) / tiles;
+  const int maxs = std::max(1, std::min(cap, maxk / 512));
+  return std::max(1, std::min(s, maxs));
+}
+
+// 256x256 pipeline: 0 = BK 64 x 2 stages, 1 = BK 32 x 4 (three K-steps in flight), 2 = BK 32 x 3
+static int g_big_variant = [] {
+  const char* e = getenv("MMT_GEMM_BIG_VARIANT");
+  return e ? atoi(e) : 0;
+}();
+
+template <bool A_KC, bool B_KC, bool SWAP, int EPI>
+static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t s) {
+  if (b.count == 0) return hipSuccess;
+  if (big) {
+    const int mt = max_tiles<TileL>(b, nullptr);
+    if (mt == 0) return hipSuccess;
+    dim3 grid(mt, EPI == EPI_ATOMIC_F32 ? auto_splits<TileL>(b, splits) : std::max(1, splits), b.count);
+    switch (g_big_variant) {
+      case 1: launch_v<TileL, 32, 4, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+      case 2: launch_v<TileL, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+      default: launch_v<TileL, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    }
+    return hipGetLastError();
+  }
+  const int mt = max_tiles<TileS>(b, nullptr);
+  if (mt == 0) return hipSuccess;
+  dim3 grid(mt, EPI == EPI_ATOMIC_F32 ? auto_splits<TileS>(b, splits) : std::max(1, splits), b.count);
   switch (EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw : g_gemm_variant) {
-    case 1: launch_v<32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
-    case 2: launch_v<32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
-    case 3: launch_v<32, 4, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
-    case 4: launch_v<64, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
-    default: launch_v<64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    case 1: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    case 2: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    case 3: launch_v<TileS, 32, 4, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    case 4: launch_v<TileS, 64, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    default: launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
   }
   return hipGetLastError();
 }
 
+// tile policy: the 256x256 tile where every problem of the launch fills it (M, N >= 256) and the
+// K loop is long enough to amortise its prologue/epilogue (K >= g_big_kmin; weight gradients
+// always qualify: K = B*T). MMT_GEMM_BIG=0 disables it, MMT_GEMM_BIG_KMIN sets the K threshold.
+static int g_big_mode = [] {
+  const char* e = getenv("MMT_GEMM_BIG");
+  return e ? atoi(e) : 1;
+}();
+static int g_big_kmin = [] {
+  const char* e = getenv("MMT_GEMM_BIG_KMIN");
+  return e ? atoi(e) : 512;
+}();
+static bool use_big(const GemmBatch& b) {
+  if (!g_big_mode || b.count == 0) return false;
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& P = b.p[g];
+    if (P.M < TileL::BM || P.N < TileL::BN || P.K < g_big_kmin) return false;
+  }
+  return true;
+}
+
 hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, int splits, hipStream_t s) {
-  if (splits < 1) splits = 1;
   for (int g = 0; g < b.count; ++g) {
     const GemmProblem& P = b.p[g];
     // 16-byte LDS-DMA pieces need 8-element-aligned leading dimensions and 16-byte aligned bases
     if ((P.lda & 7) || (P.ldb & 7) || (((uintptr_t)P.A | (uintptr_t)P.B) & 15)) return hipErrorInvalidValue;
   }
+  const bool big = use_big(b);
   if (a_kc && b_kc) {
     switch (epi) {
-      case EPI_STORE_BF16: return launch_t<true, true, true, EPI_STORE_BF16>(b, 1, s);
-      case EPI_BIAS_TANH_BF16: return launch_t<true, true, true, EPI_BIAS_TANH_BF16>(b, 1, s);
-      case EPI_BIAS_RELU_BF16: return launch_t<true, true, true, EPI_BIAS_RELU_BF16>(b, 1, s);
-      case EPI_BIAS_RESID_F32: return launch_t<true, true, true, EPI_BIAS_RESID_F32>(b, 1, s);
-      case EPI_STORE_F32: return launch_t<true, true, true, EPI_STORE_F32>(b, 1, s);
-      case EPI_ACC_F32: return launch_t<true, true, true, EPI_ACC_F32>(b, 1, s);
+      case EPI_STORE_BF16: return launch_t<true, true, true, EPI_STORE_BF16>(b, 1, big, s);
+      case EPI_BIAS_TANH_BF16: return launch_t<true, true, true, EPI_BIAS_TANH_BF16>(b, 1, big, s);
+      case EPI_BIAS_RELU_BF16: return launch_t<true, true, true, EPI_BIAS_RELU_BF16>(b, 1, big, s);
+      case EPI_BIAS_RESID_F32: return launch_t<true, true, true, EPI_BIAS_RESID_F32>(b, 1, big, s);
+      case EPI_STORE_F32: return launch_t<true, true, true, EPI_STORE_F32>(b, 1, big, s);
+      case EPI_ACC_F32: return launch_t<true, true, true, EPI_ACC_F32>(b, 1, big, s);
       default: break;
     }
   } else if (a_kc && !b_kc) {
     switch (epi) {
-      case EPI_STORE_BF16: return launch_t<true, false, true, EPI_STORE_BF16>(b, 1, s);
-      case EPI_DTANH_BF16: return launch_t<true, false, true, EPI_DTANH_BF16>(b, 1, s);
-      case EPI_DRELU_BF16: return launch_t<true, false, true, EPI_DRELU_BF16>(b, 1, s);
-      case EPI_STORE_F32: return launch_t<true, false, true, EPI_STORE_F32>(b, 1, s);
-      case EPI_ACC_F32: return launch_t<true, false, true, EPI_ACC_F32>(b, 1, s);
+      case EPI_STORE_BF16: return launch_t<true, false, true, EPI_STORE_BF16>(b, 1, big, s);
+      case EPI_DTANH_BF16: return launch_t<true, false, true, EPI_DTANH_BF16>(b, 1, big, s);
+      case EPI_DRELU_BF16: return launch_t<true, false, true, EPI_DRELU_BF16>(b, 1, big, s);
+      case EPI_STORE_F32: return launch_t<true, false, true, EPI_STORE_F32>(b, 1, big, s);
+      case EPI_ACC_F32: return launch_t<true, false, true, EPI_ACC_F32>(b, 1, big, s);
       default: break;
     }
   } else if (!a_kc && !b_kc) {
     switch (epi) {
-      case EPI_ATOMIC_F32: return launch_t<false, false, false, EPI_ATOMIC_F32>(b, splits, s);
-      case EPI_STORE_F32: return launch_t<false, false, true, EPI_STORE_F32>(b, 1, s);
+      case EPI_ATOMIC_F32: return launch_t<false, false, false, EPI_ATOMIC_F32>(b, splits, big, s);
+      case EPI_STORE_F32: return launch_t<false, false, true, EPI_STORE_F32>(b, splits, big, s);
+      case EPI_ACC_F32: return launch_t<false, false, true, EPI_ACC_F32>(b, 1, big, s);
       default: break;
     }
   } else {
     switch (epi) {
-      case EPI_ATOMIC_F32: return launch_t<false, true, false, EPI_ATOMIC_F32>(b, splits, s);
-      case EPI_STORE_F32: return launch_t<false, true, true, EPI_STORE_F32>(b, 1, s);
+      case EPI_ATOMIC_F32: return launch_t<false, true, false, EPI_ATOMIC_F32>(b, splits, big, s);
+      case EPI_STORE_F32: return launch_t<false, true, true, EPI_STORE_F32>(b, 1, big, s);
       default: break;
     }
   }
   return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradients dW[M, N] += alpha * dY[K, M]^T X[K, N] (both operands MN-contiguous, K = rows).
+// K = B*T is long and M x N small, so the K loop is split over workgroups. Each split writes a
+// plain fp32 slab (row-coalesced 16-B stores of the staged epilogue) and one reduce pass adds the
+// slabs into the gradient: fp32 atomics per element were the bottleneck (C1 FFN weight grads:
+// 16.7 M atomics per grouped launch, ~60 of its ~85 us).
+// ---------------------------------------------------------------------------------------------
+struct SlabProblem {
+  const float* slab;  // [splits][M * N]
+  float* out;         // [M][ldc]
+  int M, N, ldc;
+  int64_t stride;     // elements per slab
+};
+struct SlabBatch {
+  SlabProblem p[MMT_MAX_GROUP];
+  int count, splits;
+};
+
+__global__ __launch_bounds__(256) void slab_reduce_kernel(SlabBatch b) {
+  const SlabProblem& P = b.p[blockIdx.y];
+  const bool vec = (P.N % 4 == 0) && (P.ldc % 4 == 0) && (((uintptr_t)P.out & 15) == 0);
+  if (vec) {
+    const int64_t n4 = (int64_t)P.M * P.N / 4;
+    const int N4 = P.N / 4;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+      f32x4 acc = reinterpret_cast<const f32x4*>(P.slab)[i];
+      for (int sp = 1; sp < b.splits; ++sp) acc += reinterpret_cast<const f32x4*>(P.slab + sp * P.stride)[i];
+      const int m = (int)(i / N4), c = (int)(i % N4) * 4;
+      float* o = P.out + (int64_t)m * P.ldc + c;
+      *reinterpret_cast<f32x4*>(o) = *reinterpret_cast<const f32x4*>(o) + acc;
+    }
+  } else {
+    const int64_t n = (int64_t)P.M * P.N;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+      float acc = P.slab[i];
+      for (int sp = 1; sp < b.splits; ++sp) acc += P.slab[sp * P.stride + i];
+      P.out[(int64_t)(i / P.N) * P.ldc + i % P.N] += acc;
+    }
+  }
+}
+
+hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_bytes, hipStream_t s) {
+  if (b.count == 0) return hipSuccess;
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& P = b.p[g];
+    if ((P.lda & 7) || (P.ldb & 7) || (((uintptr_t)P.A | (uintptr_t)P.B) & 15)) return hipErrorInvalidValue;
+  }
+  const bool big = use_big(b);
+  int splits = big ? auto_splits<TileL>(b, 0) : auto_splits<TileS>(b, 0);
+  int64_t per = 0;  // slab elements of one split over all problems (each slab 16-B aligned)
+  for (int g = 0; g < b.count; ++g) per += ((int64_t)b.p[g].M * b.p[g].N + 3) / 4 * 4;
+  if (slab) {
+    const int64_t cap = slab_bytes / (int64_t)sizeof(float) / std::max<int64_t>(1, per);
+    if (splits > cap) splits = (int)cap;
+  } else {
+    splits = 1;
+  }
+  if (splits <= 1) {  // one K pass: accumulate straight into the gradient
+    GemmBatch d = b;
+    for (int g = 0; g < d.count; ++g) d.p[g].split_stride = 0;
+    return launch_t<false, false, true, EPI_ACC_F32>(d, 1, big, s);
+  }
+  GemmBatch d = b;
+  SlabBatch sb{};
+  sb.count = b.count;
+  sb.splits = splits;
+  int64_t off = 0;
+  for (int g = 0; g < d.count; ++g) {
+    GemmProblem& P = d.p[g];
+    const int64_t mn = ((int64_t)P.M * P.N + 3) / 4 * 4;
+    sb.p[g] = SlabProblem{slab + off, P.o32, P.M, P.N, P.ldc, per};
+    P.o32 = slab + off;
+    P.ldc = P.N;
+    P.split_stride = per;
+    off += mn;
+  }
+  hipError_t e = launch_t<false, false, true, EPI_STORE_F32>(d, splits, big, s);
+  if (e != hipSuccess) return e;
+  int64_t maxn4 = 0;
+  for (int g = 0; g < b.count; ++g) maxn4 = std::max<int64_t>(maxn4, ((int64_t)b.p[g].M * b.p[g].N + 3) / 4);
+  const int blocks = (int)std::min<int64_t>(2048, (maxn4 + 255) / 256);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks, b.count), dim3(256), 0, s, sb);
+  return hipGetLastError();
 }

@@ -47,6 +47,8 @@ struct GemmProblem {
   float drop_scale;
   // fused bias gradient (bf16-output epilogues, SWAP layouts): dbias[n] += sum_m out[m, n]
   float* dbias;
+  // split-K slabs: split s writes o32 + s * split_stride (elements); 0 = one output
+  int64_t split_stride;
 };
 
 struct GemmBatch {
@@ -55,6 +57,9 @@ struct GemmBatch {
 };
 
 hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, int splits, hipStream_t s);
+// weight gradients o32 += alpha * A^T B over K rows (both operands MN-contiguous): split-K into fp32
+// slabs in `slab` (capacity slab_bytes) + one reduce pass; without room, one K pass accumulating
+hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_bytes, hipStream_t s);
 
 // ------------------------------------------------------------------------------------------
 // LayerNorm (eps = 1e-5, weight+bias). Row-major [R, C] fp32 in, bf16 out; saves mean/rstd.

@@ -26,6 +26,19 @@ int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t s
   return st(e);
 }
 
+int mmt_op_gemm_wgrad(void* stream, int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, const void* B,
+                      int32_t ldb, float* out, int32_t ldc, float alpha, void* slab, int64_t slab_bytes) {
+  if (M < 0 || N < 0 || K < 0 || (lda & 7) || (ldb & 7) || !out) return MMT_ERR_INVALID;
+  GemmBatch b{};
+  b.count = 1;
+  GemmProblem& p = b.p[0];
+  p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
+  p.o32 = out; p.ldc = ldc; p.alpha = alpha; p.M = M; p.N = N; p.K = K;
+  const hipError_t e = mmt_launch_gemm_wgrad(b, (float*)slab, slab ? slab_bytes : 0, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return MMT_ERR_UNSUPPORTED;
+  return st(e);
+}
+
 int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
                          void* y16, float* mean, float* rstd) {
   LnBatch b{};

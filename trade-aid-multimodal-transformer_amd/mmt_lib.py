@@ -73,6 +73,7 @@ _SIGS = {
     "mmt_gemm_set_variant": (c_i32, [ctypes.c_int]),
     "mmt_op_gemm": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp,
                             c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32]),
+    "mmt_op_gemm_wgrad": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32, c_vp, c_i64]),
     "mmt_op_layernorm_fwd": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mmt_op_layernorm_bwd": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mmt_op_attention_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(c_vp),
