@@ -20,6 +20,10 @@ SHAPES = [
     # name, a_kc, b_kc, epi, M, N, K, splits
     ("ffn0_fwd", 1, 1, "bias_relu_bf16", R, 1024, 256, 1),
     ("ffn0_store", 1, 1, "store_bf16", R, 1024, 256, 1),
+    ("ffn0_loop_only", 1, 1, "store_bf16", R, 1024, 256, -1),
+    ("ffn0_epi_only", 1, 1, "store_bf16", R, 1024, 0, 1),
+    ("ffn2dx_loop_only", 1, 0, "drelu_bf16", R, 1024, 256, -1),
+    ("ffn2dx_epi_only", 1, 0, "drelu_bf16", R, 1024, 0, 1),
     ("ffn0_f32", 1, 1, "store_f32", R, 1024, 256, 1),
     ("qkv1_store", 1, 1, "store_bf16", R, 384, 256, 1),
     ("ffn2_fwd", 1, 1, "bias_resid_f32", R, 256, 1024, 1),
@@ -82,9 +86,12 @@ def run(variant, reps):
         o16 = torch.zeros(M, r8(N), dtype=torch.bfloat16, device="cuda")
         s = ML.stream_ptr()
 
+        alpha = -12345.0 if splits < 0 else 1.0  # splits -1: main loop only (debug build knob)
+        sp = max(1, splits)
+
         def call():
-            rc = L.mmt_op_gemm(s, akc, bkc, ML.EPI[epi], splits, M, N, K, ML.ptr(A), lda, ML.ptr(B), ldb, ML.ptr(bias),
-                               ML.ptr(aux), r8(N), ML.ptr(resid), N, ML.ptr(o32), N, ML.ptr(o16), r8(N), 1.0)
+            rc = L.mmt_op_gemm(s, akc, bkc, ML.EPI[epi], sp, M, N, K, ML.ptr(A), lda, ML.ptr(B), ldb, ML.ptr(bias),
+                               ML.ptr(aux), r8(N), ML.ptr(resid), N, ML.ptr(o32), N, ML.ptr(o16), r8(N), alpha)
             assert rc == 0
 
         for _ in range(3):
@@ -96,7 +103,7 @@ def run(variant, reps):
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / reps * 1e3
-        tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+        tf = 2.0 * M * N * max(K, 1) / (us * 1e-6) / 1e12
         out[name] = (us, tf)
     return out
 
