@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -114,6 +115,12 @@ struct mmt_ctx {
   std::string probe_label;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> probe_events;
   int ldv[MAXM], ldvh[MAXM];
+  // backward side stream: the weight-gradient GEMMs (nothing in the data-gradient chain reads
+  // them) run there, overlapping the latency-bound data-gradient kernels; joined at stage ends
+  hipStream_t side = nullptr;
+  int side_device = -1;
+  std::vector<hipEvent_t> evpool;
+  size_t evnext = 0;
 };
 
 namespace {
@@ -435,8 +442,27 @@ struct Runner {
     ok(mmt_launch_gemm(b, akc, bkc, epi, splits, s), what);
     probe_end(what);
   }
+  // fork the side stream off the main one (everything enqueued on `s` so far happens first)
+  hipStream_t side() {
+    if (!c->side) return s;
+    hipEvent_t e = c->evpool[c->evnext++ % c->evpool.size()];
+    ok(hipEventRecord(e, s), "event record");
+    ok(hipStreamWaitEvent(c->side, e, 0), "stream wait");
+    return c->side;
+  }
+  // the main stream waits for everything enqueued on the side stream
+  void join() {
+    if (!c->side) return;
+    hipEvent_t e = c->evpool[c->evnext++ % c->evpool.size()];
+    ok(hipEventRecord(e, c->side), "event record");
+    ok(hipStreamWaitEvent(s, e, 0), "stream wait");
+  }
   void dwgemm(const GemmBatch& b, const char* what) {
     if (rc != MMT_OK) return;
+    if (c->side && !probing(what)) {
+      ok(mmt_launch_gemm_wgrad(b, W<float>(c->plan.slab), (int64_t)c->plan.slab_bytes, side()), what);
+      return;
+    }
     probe_begin(what);
     ok(mmt_launch_gemm_wgrad(b, W<float>(c->plan.slab), (int64_t)c->plan.slab_bytes, s), what);
     probe_end(what);
@@ -696,6 +722,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       set_dres16_consumer(c, r, lb.p[i], i, L - 1, grads);
       lb.p[i].dgamma = grads + c->post[i].lnw; lb.p[i].dbeta = grads + c->post[i].lnb;
     }
+    r.join();  // lnf_bwd rewrites dres16 (read by side-stream weight-gradient GEMMs)
     r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "lnf_bwd");
     return r.rc;
   }
@@ -801,6 +828,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       db.p[i].src = r.W<float>(p.dres[i]); db.p[i].dst = r.W<bf16_t>(p.dres16[i]); db.p[i].dsum = grads + x[i].bf2;
       r.set_drop(db.p[i], l, i, DS_FFN);
     }
+    r.join();
     r.ok(mmt_launch_drop_copy(db, R, C, r.s), "dres16");
   }
   if (r.rc != MMT_OK) return r.rc;
@@ -834,6 +862,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     r.set_drop(lb.p[i], l, i, DS_SA_PROJ);  // the copy feeds the SA projection backward
     lb.p[i].dsum = grads + x[i].bp2;
   }
+  r.join();
   r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln2_bwd");
   // SA output projection
   for (int i = 0; i < M; ++i) {
@@ -889,6 +918,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     lb.p[i].dgamma = grads + x[i].ln1w; lb.p[i].dbeta = grads + x[i].ln1b;
     set_dres16_consumer(c, r, lb.p[i], i, l - 1, grads);
   }
+  r.join();
   r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln1_bwd");
   return r.rc;
 }
@@ -954,6 +984,8 @@ void mmt_destroy(mmt_ctx* c) {
   if (c->d_segs) (void)hipFree(c->d_segs);
   if (c->d_tasks) (void)hipFree(c->d_tasks);
   for (auto& e : c->probe_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  for (auto& e : c->evpool) (void)hipEventDestroy(e);
+  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
 }
 
@@ -1034,6 +1066,25 @@ int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* los
   if (!c) return MMT_ERR_INVALID;
   if (!c->fwd_ready) return fail(c, MMT_ERR_STATE, "mmt_backward: no forward with targets to differentiate");
   if (stage < 0 || stage > c->L + 1) return fail(c, MMT_ERR_INVALID, "bad backward stage");
+  {
+    static const bool use_side = [] {
+      const char* e = getenv("MMT_SIDE_STREAM");
+      return !e || atoi(e) != 0;
+    }();
+    int dev = -1;
+    if (use_side && hipGetDevice(&dev) == hipSuccess && (!c->side || c->side_device != dev)) {
+      if (c->side) (void)hipStreamDestroy(c->side);
+      c->side = nullptr;
+      if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
+      c->side_device = dev;
+      while (c->side && c->evpool.size() < 64) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) break;
+        c->evpool.push_back(e);
+      }
+      if (c->evpool.empty() && c->side) { (void)hipStreamDestroy(c->side); c->side = nullptr; }
+    }
+  }
   Runner r{c, (hipStream_t)stream, workspace, params, nullptr, c->plan.B, c->plan.B * c->T};
   r.drop = c->fwd_drop;
   r.seed = c->fwd_seed;
@@ -1046,7 +1097,9 @@ int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* los
     r.ok(mmt_launch_embed_bwd(eb, r.B, c->T, c->C, r.s), "embed_bwd");
     return r.rc;
   }
-  return run_backward_stage(c, r, stage, loss_grads, grads);
+  const int rc = run_backward_stage(c, r, stage, loss_grads, grads);
+  r.join();  // the stage's gradient range is complete on the caller's stream (DP all-reduce order)
+  return rc ? rc : r.rc;
 }
 
 int mmt_backward(mmt_ctx* c, void* stream, const float* loss_grads, const float* params, float* grads,
