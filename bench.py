@@ -76,15 +76,16 @@ def dominant_kernel_bytes(label, M, C, H, T, B, V):
     raise ValueError(label)
 
 
-def pmc_traffic(label):
-    """HBM bytes per launch of `label` from the committed PMC passes (profiles/pmc_traffic.json:
-    rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate runs of this bench, FETCH_SIZE doubled
-    per the gfx950 correction of MI355X_MICROARCH.md); None when not collected for this kernel."""
+def pmc_traffic(config, label):
+    """HBM bytes per launch of `label` at `config` from the committed PMC passes
+    (profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate runs of this
+    bench, FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md); None when not
+    collected for this kernel and config."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(label, {}).get("bytes_per_launch")
-    except (OSError, ValueError):
+            return json.load(f).get(config, {}).get(label, {}).get("bytes_per_launch")
+    except (OSError, ValueError, AttributeError):
         return None
 
 
@@ -220,7 +221,7 @@ def main():
         else:
             roof = {"bound": "hbm", "achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
         roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-        roof.update({"traffic": pmc_traffic(args.probe), "kernel": args.probe, "launches": probe_n.value,
+        roof.update({"traffic": pmc_traffic(args.config, args.probe), "kernel": args.probe, "launches": probe_n.value,
                      "avg_launch_us": round(per_launch_ms * 1e3, 2), "flops_per_launch": fl,
                      "algorithmic_bytes_per_launch": by, "tflops": round(fl / sec / 1e12, 1),
                      "gbs": round(by / sec / 1e9, 1)})

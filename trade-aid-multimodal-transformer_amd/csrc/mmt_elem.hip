@@ -11,47 +11,62 @@
 // LayerNorm (reference: nn.LayerNorm(n_embd), eps 1e-5; model.py:189-190, 210, 330)
 // one wave per row; each lane holds NV float4 of the row in registers
 // ============================================================================================
-template <int NV>
+template <int NV, int RPI>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(LnBatch batch, int R, int C) {
+  // RPI rows per wave with every row's loads issued before any reduction (memory-level parallelism)
   const LnProblem& P = batch.p[blockIdx.z];
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= R) return;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPI;
   const int C4 = C >> 2;
-  const float* x = P.x + (int64_t)row * C;
-  f32x4 v[NV];
-  float s = 0.f;
+  f32x4 v[RPI][NV];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c4 = lane + 64 * i;
-    v[i] = (c4 < C4) ? reinterpret_cast<const f32x4*>(x)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
-    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-  }
-  const float mean = warp_sum(s) / C;
-  float q = 0.f;
+  for (int u = 0; u < RPI; ++u) {
+    const int row = row0 + u;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c4 = lane + 64 * i;
-    if (c4 < C4) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      v[u][i] = (row < R && c4 < C4) ? reinterpret_cast<const f32x4*>(P.x + (int64_t)row * C)[c4]
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  const float rstd = rsqrtf(warp_sum(q) / C + 1e-5f);
-  bf16_t* y = P.y + (int64_t)row * C;
+  f32x4 g[NV], b[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c4 = lane + 64 * i;
-    if (c4 < C4) {
-      const f32x4 g = reinterpret_cast<const f32x4*>(P.gamma)[c4];
-      const f32x4 b = reinterpret_cast<const f32x4*>(P.beta)[c4];
-      float o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
-      reinterpret_cast<u32x2*>(y)[c4] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
-    }
+    g[i] = c4 < C4 ? reinterpret_cast<const f32x4*>(P.gamma)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    b[i] = c4 < C4 ? reinterpret_cast<const f32x4*>(P.beta)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  if (lane == 0) { P.mean[row] = mean; P.rstd[row] = rstd; }
+#pragma unroll
+  for (int u = 0; u < RPI; ++u) {
+    const int row = row0 + u;
+    if (row >= R) break;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s += v[u][i][0] + v[u][i][1] + v[u][i][2] + v[u][i][3];
+    const float mean = warp_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { const float d = v[u][i][e] - mean; q += d * d; }
+      }
+    }
+    const float rstd = rsqrtf(warp_sum(q) / C + 1e-5f);
+    bf16_t* y = P.y + (int64_t)row * C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (v[u][i][e] - mean) * rstd * g[i][e] + b[i][e];
+        reinterpret_cast<u32x2*>(y)[c4] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+      }
+    }
+    if (lane == 0) { P.mean[row] = mean; P.rstd[row] = rstd; }
+  }
 }
 
 // backward: dx += rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dgamma/dbeta column sums.
@@ -164,11 +179,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBatch batch, int R, int C
 
 hipError_t mmt_launch_ln_fwd(const LnBatch& b, int R, int C, hipStream_t s) {
   if (C % 4 != 0 || C > 1024 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
-  dim3 grid((R + 3) / 4, 1, b.count);
   const int nv = (C / 4 + 63) / 64;
-  if (nv <= 1) hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, dim3(256), 0, s, b, R, C);
-  else if (nv <= 2) hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, dim3(256), 0, s, b, R, C);
-  else hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, dim3(256), 0, s, b, R, C);
+  if (nv <= 1) hipLaunchKernelGGL((ln_fwd_kernel<1, 4>), dim3((R + 15) / 16, 1, b.count), dim3(256), 0, s, b, R, C);
+  else if (nv <= 2) hipLaunchKernelGGL((ln_fwd_kernel<2, 2>), dim3((R + 7) / 8, 1, b.count), dim3(256), 0, s, b, R, C);
+  else hipLaunchKernelGGL((ln_fwd_kernel<4, 1>), dim3((R + 3) / 4, 1, b.count), dim3(256), 0, s, b, R, C);
   return hipGetLastError();
 }
 

@@ -643,8 +643,17 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(SlabBatch b) {
     const int64_t n4 = (int64_t)P.M * P.N / 4;
     const int N4 = P.N / 4;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-      f32x4 acc = reinterpret_cast<const f32x4*>(P.slab)[i];
-      for (int sp = 1; sp < b.splits; ++sp) acc += reinterpret_cast<const f32x4*>(P.slab + sp * P.stride)[i];
+      // 8 slab loads in flight per thread (independent partial sums)
+      f32x4 part[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      int sp = 0;
+      for (; sp + 8 <= b.splits; sp += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) part[u] += reinterpret_cast<const f32x4*>(P.slab + (sp + u) * P.stride)[i];
+      }
+      for (; sp < b.splits; ++sp) part[0] += reinterpret_cast<const f32x4*>(P.slab + sp * P.stride)[i];
+      const f32x4 acc = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
       const int m = (int)(i / N4), c = (int)(i % N4) * 4;
       float* o = P.out + (int64_t)m * P.ldc + c;
       *reinterpret_cast<f32x4*>(o) = *reinterpret_cast<const f32x4*>(o) + acc;
@@ -698,7 +707,7 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
   if (e != hipSuccess) return e;
   int64_t maxn4 = 0;
   for (int g = 0; g < b.count; ++g) maxn4 = std::max<int64_t>(maxn4, ((int64_t)b.p[g].M * b.p[g].N + 3) / 4);
-  const int blocks = (int)std::min<int64_t>(2048, (maxn4 + 255) / 256);
+  const int blocks = (int)std::min<int64_t>(4096, (maxn4 + 255) / 256);
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks, b.count), dim3(256), 0, s, sb);
   return hipGetLastError();
 }
