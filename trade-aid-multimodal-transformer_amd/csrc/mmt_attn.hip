@@ -129,8 +129,8 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
 // forward: one 32x32 (keys x queries) tile of S^T, online softmax, O^T += V^T P^T
-template <int HS>
-__device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq, bool diag,
+template <int HS, bool diag, bool DROP>
+__device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq,
                                          const bf16x8 (&qf)[Geo<HS>::NKS], float& m, float& l,
                                          f32x16 (&oacc)[Geo<HS>::ND], float c2, const AttnProblem& P, uint32_t dkey,
                                          uint32_t drow, int lane) {
@@ -172,7 +172,7 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
   rs += __shfl_xor(rs, 32, 64);
   l = l * alpha + rs;
   m = mnew;
-  if (P.drop_thr) {  // dropout on the probabilities (the normaliser l keeps every term)
+  if (DROP) {  // dropout on the probabilities (the normaliser l keeps every term)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const uint32_t key = (uint32_t)(k0 + (e & 3) + 8 * (e >> 2) + 4 * h);
@@ -204,10 +204,14 @@ struct ChunkWalk {
 };
 
 // =============================================================================================
-// forward: grid (ceil(nt/8), B*H, G)
+// forward: grid (ceil(nt/8) * B*H, 1, G). Wave w owns query tiles qa = 8*bx + w and qb = 8*bx + 7 - w
+// and walks them TOGETHER: while both need a key tile the two online softmaxes run as one
+// straight-line body (no branches: the diagonal and dropout variants are compile-time), so two
+// independent MFMA -> softmax -> MFMA chains interleave in the wave; the resident K/V chunk of each
+// (stream, chunk) is loaded once per block.
 // =============================================================================================
-template <int HS>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
+template <int HS, bool DROP>
+__global__ __launch_bounds__(256, (HS <= 32 && !DROP) ? 2 : 1) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, i
   const int nt = (T + 31) / 32;
   const int qt0 = bx * 8;
   const int qmax = min(qt0 + 7, nt - 1);
-  const ChunkWalk walk{P.nstreams, (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS};
+  const int nch = (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS;
   const int64_t rowbase = (int64_t)b * T;
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];
@@ -234,52 +238,78 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, i
   st.store(ks, G::RW, vs, G::TW, tid);
   __syncthreads();
 
+  const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb
+  const bool la = qa < nt, lb = qb < nt;     // lb implies la
+  const int tqa = qa * 32 + r, tqb = qb * 32 + r;
+  const uint32_t drowa = (uint32_t)(bh * T + tqa), drowb = (uint32_t)(bh * T + tqb);
+  bf16x8 qfa[G::NKS], qfb[G::NKS];
+  f32x16 ota[G::ND], otb[G::ND];
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s) {
+    const int d0 = 16 * s + 8 * h;
+    qfa[s] = ld8(P.q + (rowbase + tqa) * P.q_ld + head * HS + d0, la && tqa < T && d0 < HS);
+    qfb[s] = ld8(P.q + (rowbase + tqb) * P.q_ld + head * HS + d0, lb && tqb < T && d0 < HS);
+  }
+#pragma unroll
+  for (int dt = 0; dt < G::ND; ++dt) { zero16(ota[dt]); zero16(otb[dt]); }
+  for (int j = 0; j < P.nstreams; ++j) {
+    const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+    float ma = -INFINITY, lsa = 0.f, mb = -INFINITY, lsb = 0.f;
+    f32x16 oa[G::ND], ob[G::ND];
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) { zero16(oa[dt]); zero16(ob[dt]); }
+    for (int c = 0; c < nch; ++c) {
+      const int kt_lo = c * (ROWS / 32);
+      const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
+      if (lb) {
+        int kt = kt_lo;
 #pragma unroll 1
-  for (int u = 0; u < 2; ++u) {
-    const int qt = u == 0 ? qt0 + w : qt0 + 7 - w;
-    const bool live = qt < nt;
-    const int tq = qt * 32 + r;
-    const uint32_t drow = (uint32_t)(bh * T + tq);
-    bf16x8 qf[G::NKS];
-    f32x16 otot[G::ND];
-#pragma unroll
-    for (int s = 0; s < G::NKS; ++s) {
-      const int d0 = 16 * s + 8 * h;
-      qf[s] = ld8(P.q + (rowbase + tq) * P.q_ld + head * HS + d0, live && tq < T && d0 < HS);
-    }
-#pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt) zero16(otot[dt]);
-    for (int j = 0; j < P.nstreams; ++j) {
-      const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
-      float m = -INFINITY, l = 0.f;
-      f32x16 oacc[G::ND];
-#pragma unroll
-      for (int dt = 0; dt < G::ND; ++dt) zero16(oacc[dt]);
-      for (int c = 0; c < walk.nch; ++c) {
-        int nj, nc;
-        const bool reload = walk.next(u, j, c, nj, nc);
-        if (live) {
-          const int kt_lo = c * (ROWS / 32);
-          const int last = min(qt, min(kt_lo + ROWS / 32, nt) - 1);
-          #pragma unroll 1
-          for (int kt = kt_lo; kt <= last; ++kt)
-            fwd_tile<HS>(ks, vs, (kt - kt_lo) * 32, kt * 32, tq, kt == qt, qf, m, l, oacc, c2, P, dkey, drow, lane);
+        for (; kt <= min(qa - 1, kt_hi); ++kt) {  // both tiles, off the diagonal
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, P, dkey, drowa, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, P, dkey, drowb, lane);
         }
-        if (reload) {
-          __syncthreads();
-          st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
-                  T, tid);
-          st.store(ks, G::RW, vs, G::TW, tid);
-          __syncthreads();
+        if (qa >= kt_lo && qa <= kt_hi) {  // tile a's diagonal, tile b off it
+          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, P, dkey, drowa, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, mb, lsb, ob, c2, P, dkey, drowb, lane);
         }
+#pragma unroll 1
+        for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, P, dkey, drowb, lane);
+        if (qb >= kt_lo && qb <= kt_hi)
+          fwd_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, mb, lsb, ob, c2, P, dkey, drowb, lane);
+      } else if (la) {
+#pragma unroll 1
+        for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, P, dkey, drowa, lane);
+        if (qa >= kt_lo && qa <= kt_hi)
+          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, P, dkey, drowa, lane);
       }
+      // next (stream, chunk) resident for the whole block
+      int nj = j, nc = c + 1;
+      if (nc == nch) { nc = 0; ++nj; }
+      if (nj < P.nstreams && (nj != j || nc != c)) {
+        __syncthreads();
+        st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
+                T, tid);
+        st.store(ks, G::RW, vs, G::TW, tid);
+        __syncthreads();
+      }
+    }
+    // normalise this stream's outputs, keep its LSE (and its own output when several are summed)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool live = u == 0 ? la : lb;
+      const int tq = u == 0 ? tqa : tqb;
+      f32x16* o = u == 0 ? oa : ob;
+      f32x16* ot = u == 0 ? ota : otb;
+      const float m = u == 0 ? ma : mb, l = u == 0 ? lsa : lsb;
       const float inv = (l > 0.f) ? 1.f / l : 0.f;
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          oacc[dt][e] *= inv;
-          otot[dt][e] += oacc[dt][e];
+          o[dt][e] *= inv;
+          ot[dt][e] += o[dt][e];
         }
       if (live && tq < T) {
         if (h == 0) P.lse[j][(int64_t)bh * T + tq] = (m + __log2f(l)) * kLn2;
@@ -291,11 +321,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, i
               const int d0 = dt * 32 + 8 * g + 4 * h;
               if (d0 < HS)
                 *reinterpret_cast<u32x2*>(P.oj[j] + (rowbase + tq) * P.o_ld + head * HS + d0) =
-                    u32x2{pack2bf(oacc[dt][4 * g], oacc[dt][4 * g + 1]), pack2bf(oacc[dt][4 * g + 2], oacc[dt][4 * g + 3])};
+                    u32x2{pack2bf(o[dt][4 * g], o[dt][4 * g + 1]), pack2bf(o[dt][4 * g + 2], o[dt][4 * g + 3])};
             }
         }
       }
     }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const bool live = u == 0 ? la : lb;
+    const int tq = u == 0 ? tqa : tqb;
+    const f32x16* ot = u == 0 ? ota : otb;
     if (live && tq < T) {
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt)
@@ -304,7 +340,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBatch batch, int T, i
           const int d0 = dt * 32 + 8 * g + 4 * h;
           if (d0 < HS)
             *reinterpret_cast<u32x2*>(P.o + (rowbase + tq) * P.o_ld + head * HS + d0) =
-                u32x2{pack2bf(otot[dt][4 * g], otot[dt][4 * g + 1]), pack2bf(otot[dt][4 * g + 2], otot[dt][4 * g + 3])};
+                u32x2{pack2bf(ot[dt][4 * g], ot[dt][4 * g + 1]), pack2bf(ot[dt][4 * g + 2], ot[dt][4 * g + 3])};
         }
     }
   }
@@ -615,7 +651,10 @@ template <int HS>
 static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
   const int nb = ((T + 31) / 32 + 7) / 8;
   if (!bwd) {
-    hipLaunchKernelGGL(attn_fwd_kernel<HS>, dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    bool drop = false;
+    for (int g = 0; g < bt.count; ++g) drop = drop || bt.p[g].drop_thr != 0;
+    if (drop) hipLaunchKernelGGL((attn_fwd_kernel<HS, true>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_fwd_kernel<HS, false>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
   } else {
     const int ns = bt.p[0].nstreams;
     hipLaunchKernelGGL(attn_bwd_dq_kernel<HS>, dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
