@@ -19,6 +19,8 @@
 // Dropout (model.py:69, 151: applied to the normalised probabilities): a counter-hash mask
 // regenerated identically in all three kernels; O = (P.Z) V with Z = mask / (1 - p), so
 // dV = (P.Z)^T dO, dS = P.(Z.dP - D) with D = rowsum(dO.O) unchanged.
+#include <stdlib.h>
+
 #include "mmt_common.h"
 #include "mmt_kernels.h"
 
@@ -191,18 +193,6 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
   }
 }
 
-// Block-uniform walk over (tile u, stream j, chunk c): the chunk (j, c) resident in LDS is reused
-// while consecutive steps share it (T <= ROWS with one stream: a single load for the whole block).
-struct ChunkWalk {
-  int ns, nch;
-  __device__ __forceinline__ bool next(int u, int j, int c, int& nj, int& nc) const {
-    nj = j; nc = c + 1;
-    int nu = u;
-    if (nc == nch) { nc = 0; ++nj; if (nj == ns) { nj = 0; ++nu; } }
-    return nu < 2 && (nj != j || nc != c);
-  }
-};
-
 // =============================================================================================
 // forward: grid (ceil(nt/8) * B*H, 1, G). Wave w owns query tiles qa = 8*bx + w and qb = 8*bx + 7 - w
 // and walks them TOGETHER: while both need a key tile the two online softmaxes run as one
@@ -347,8 +337,8 @@ __global__ __launch_bounds__(256, (HS <= 32 && !DROP) ? 2 : 1) void attn_fwd_ker
 }
 
 // dQ: one 32x32 tile; S^T, dP^T recomputed, dQ^T += K^T dS^T
-template <int HS>
-__device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq, bool diag,
+template <int HS, bool diag, bool DROP>
+__device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq,
                                         const bf16x8 (&qf)[Geo<HS>::NKS], const bf16x8 (&dof)[Geo<HS>::NKS],
                                         float lse2, float dsum, f32x16 (&dq)[Geo<HS>::ND], float c2,
                                         const AttnProblem& P, uint32_t dkey, uint32_t drow, int lane) {
@@ -370,7 +360,7 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
     float pv = ex2(sacc[e] * c2 - lse2);
     if (diag && key > tq) pv = 0.f;
     float dp = dpacc[e];
-    if (P.drop_thr) dp = (mmt_hash(dkey, drow, (uint32_t)key) >= P.drop_thr) ? dp * P.drop_scale : 0.f;
+    if (DROP) dp = (mmt_hash(dkey, drow, (uint32_t)key) >= P.drop_thr) ? dp * P.drop_scale : 0.f;
     sacc[e] = pv * (dp - dsum);  // dS^T
   }
 #pragma unroll
@@ -382,15 +372,15 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
 }
 
 // =============================================================================================
-// backward dQ (also writes D_j = rowsum(dO * O_j) for the dK/dV pass); grid as forward
+// backward dQ (also writes D_j = rowsum(dO * O_j) for the dK/dV pass); grid as forward, and like the
+// forward each wave walks its two query tiles together
 // =============================================================================================
-template <int HS>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H, float scale) {
+template <int HS, bool DROP>
+__global__ __launch_bounds__(256, (HS <= 32 && !DROP) ? 2 : 1) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H,
+                                                                                       float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
-  // grid.x = nb * B*H in XCD-aware logical order: the heads of one batch row (halves of the same
-  // Q/K/V cache lines) run on one XCD together
   const int nb = ((T + 31) / 32 + 7) / 8;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const int bh = tile / nb, b = bh / H, head = bh % H;
@@ -400,7 +390,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T
   const int nt = (T + 31) / 32;
   const int qt0 = bx * 8;
   const int qmax = min(qt0 + 7, nt - 1);
-  const ChunkWalk walk{P.nstreams, (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS};
+  const int nch = (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS;
   const int64_t rowbase = (int64_t)b * T;
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row + tr reads
@@ -412,58 +402,97 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T
   st.store(ks, G::RW, vs, G::RW, tid);
   __syncthreads();
 
-#pragma unroll 1
-  for (int u = 0; u < 2; ++u) {
-    const int qt = u == 0 ? qt0 + w : qt0 + 7 - w;
-    const bool live = qt < nt;
-    const int tq = qt * 32 + r;
-    const bool qok = live && tq < T;
-    const uint32_t drow = (uint32_t)(bh * T + tq);
-    bf16x8 qf[G::NKS], dof[G::NKS];
-    f32x16 dq[G::ND];
+  const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb; lb implies la
+  const bool la = qa < nt, lb = qb < nt;
+  const int tqa = qa * 32 + r, tqb = qb * 32 + r;
+  const bool oka = la && tqa < T, okb = lb && tqb < T;
+  const uint32_t drowa = (uint32_t)(bh * T + tqa), drowb = (uint32_t)(bh * T + tqb);
+  bf16x8 qfa[G::NKS], dofa[G::NKS], qfb[G::NKS], dofb[G::NKS];
+  f32x16 dqa[G::ND], dqb[G::ND];
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s) {
+    const int d0 = 16 * s + 8 * h;
+    qfa[s] = ld8(P.q + (rowbase + tqa) * P.q_ld + head * HS + d0, oka && d0 < HS);
+    dofa[s] = ld8(P.dout + (rowbase + tqa) * P.dout_ld + head * HS + d0, oka && d0 < HS);
+    qfb[s] = ld8(P.q + (rowbase + tqb) * P.q_ld + head * HS + d0, okb && d0 < HS);
+    dofb[s] = ld8(P.dout + (rowbase + tqb) * P.dout_ld + head * HS + d0, okb && d0 < HS);
+  }
+#pragma unroll
+  for (int dt = 0; dt < G::ND; ++dt) { zero16(dqa[dt]); zero16(dqb[dt]); }
+  for (int j = 0; j < P.nstreams; ++j) {
+    const bf16_t* oj = (P.nstreams > 1) ? P.oj[j] : P.o;
+    float dsa = 0.f, dsb = 0.f;
 #pragma unroll
     for (int s = 0; s < G::NKS; ++s) {
       const int d0 = 16 * s + 8 * h;
-      qf[s] = ld8(P.q + (rowbase + tq) * P.q_ld + head * HS + d0, qok && d0 < HS);
-      dof[s] = ld8(P.dout + (rowbase + tq) * P.dout_ld + head * HS + d0, qok && d0 < HS);
-    }
+      const bf16x8 ova = ld8(oj + (rowbase + tqa) * P.o_ld + head * HS + d0, oka && d0 < HS);
+      const bf16x8 ovb = ld8(oj + (rowbase + tqb) * P.o_ld + head * HS + d0, okb && d0 < HS);
 #pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt) zero16(dq[dt]);
-    for (int j = 0; j < P.nstreams; ++j) {
-      const bf16_t* oj = (P.nstreams > 1) ? P.oj[j] : P.o;
-      float dsum = 0.f;
-#pragma unroll
-      for (int s = 0; s < G::NKS; ++s) {
-        const int d0 = 16 * s + 8 * h;
-        const bf16x8 ov = ld8(oj + (rowbase + tq) * P.o_ld + head * HS + d0, qok && d0 < HS);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dsum += (float)ov[e] * (float)dof[s][e];
-      }
-      dsum += __shfl_xor(dsum, 32, 64);
-      if (qok && h == 0) P.dvec[j][(int64_t)bh * T + tq] = dsum;
-      const float lse2 = qok ? P.lse[j][(int64_t)bh * T + tq] * kLog2e : 0.f;
-      const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
-      for (int c = 0; c < walk.nch; ++c) {
-        int nj, nc;
-        const bool reload = walk.next(u, j, c, nj, nc);
-        if (live) {
-          const int kt_lo = c * (ROWS / 32);
-          const int last = min(qt, min(kt_lo + ROWS / 32, nt) - 1);
-          #pragma unroll 1
-          for (int kt = kt_lo; kt <= last; ++kt)
-            dq_tile<HS>(ks, vs, (kt - kt_lo) * 32, kt * 32, tq, kt == qt, qf, dof, lse2, dsum, dq, c2, P, dkey, drow,
-                        lane);
-        }
-        if (reload) {
-          __syncthreads();
-          st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
-                  T, tid);
-          st.store(ks, G::RW, vs, G::RW, tid);
-          __syncthreads();
-        }
+      for (int e = 0; e < 8; ++e) {
+        dsa += (float)ova[e] * (float)dofa[s][e];
+        dsb += (float)ovb[e] * (float)dofb[s][e];
       }
     }
-    if (qok) {
+    dsa += __shfl_xor(dsa, 32, 64);
+    dsb += __shfl_xor(dsb, 32, 64);
+    if (h == 0) {
+      if (oka) P.dvec[j][(int64_t)bh * T + tqa] = dsa;
+      if (okb) P.dvec[j][(int64_t)bh * T + tqb] = dsb;
+    }
+    const float lsa = oka ? P.lse[j][(int64_t)bh * T + tqa] * kLog2e : 0.f;
+    const float lsb = okb ? P.lse[j][(int64_t)bh * T + tqb] * kLog2e : 0.f;
+    const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+    for (int c = 0; c < nch; ++c) {
+      const int kt_lo = c * (ROWS / 32);
+      const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
+      if (lb) {
+        int kt = kt_lo;
+#pragma unroll 1
+        for (; kt <= min(qa - 1, kt_hi); ++kt) {
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, dkey, drowa,
+                                   lane);
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, dkey, drowb,
+                                   lane);
+        }
+        if (qa >= kt_lo && qa <= kt_hi) {
+          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, dkey, drowa,
+                                  lane);
+          dq_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, dkey, drowb,
+                                   lane);
+        }
+#pragma unroll 1
+        for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, dkey, drowb,
+                                   lane);
+        if (qb >= kt_lo && qb <= kt_hi)
+          dq_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, dkey, drowb,
+                                  lane);
+      } else if (la) {
+#pragma unroll 1
+        for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, dkey, drowa,
+                                   lane);
+        if (qa >= kt_lo && qa <= kt_hi)
+          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, dkey, drowa,
+                                  lane);
+      }
+      int nj = j, nc = c + 1;
+      if (nc == nch) { nc = 0; ++nj; }
+      if (nj < P.nstreams && (nj != j || nc != c)) {
+        __syncthreads();
+        st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
+                T, tid);
+        st.store(ks, G::RW, vs, G::RW, tid);
+        __syncthreads();
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const bool ok = u == 0 ? oka : okb;
+    const int tq = u == 0 ? tqa : tqb;
+    const f32x16* dq = u == 0 ? dqa : dqb;
+    if (ok) {
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
@@ -478,9 +507,223 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBatch batch, int T
   }
 }
 
+#ifndef MMT_DKDV_MINB
+#define MMT_DKDV_MINB 1
+#endif
+// dK, dV: one 32x32 (queries x keys) tile; S, dP recomputed, dV += P^T dO, dK += dS^T Q
+template <int HS, bool masked, bool DROP>
+__device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, const float* lsl, const float* dsl,
+                                          int ql, int q0, int tk, int T,
+                                          const bf16x8 (&kf)[Geo<HS>::NKS], const bf16x8 (&vf)[Geo<HS>::NKS],
+                                          f32x16 (&dk)[Geo<HS>::ND], f32x16 (&dv)[Geo<HS>::ND], float c2,
+                                          const AttnProblem& P, uint32_t dkey, int bhT, int lane) {
+  using G = Geo<HS>;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 sacc, dpacc, pm;
+  zero16(sacc);
+  zero16(dpacc);
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s) {
+    const bf16x8 qa = *reinterpret_cast<const bf16x8*>(qs + (ql + r) * G::RW + 16 * s + 8 * h);
+    const bf16x8 da = *reinterpret_cast<const bf16x8*>(dos + (ql + r) * G::RW + 16 * s + 8 * h);
+    sacc = mfma32(qa, kf[s], sacc);    // S[q][key]
+    dpacc = mfma32(da, vf[s], dpacc);  // dP[q][key]
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsl + ql + 8 * g + 4 * h);
+    const f32x4 d4 = *reinterpret_cast<const f32x4*>(dsl + ql + 8 * g + 4 * h);
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      const int e = 4 * g + e4;
+      const int tq = q0 + 8 * g + 4 * h + e4;
+      float pv = ex2(sacc[e] * c2 - l4[e4]);
+      if (masked && !(tk <= tq && tq < T)) pv = 0.f;
+      if (DROP) {
+        const bool keep = mmt_hash(dkey, (uint32_t)(bhT + tq), (uint32_t)tk) >= P.drop_thr;
+        pm[e] = keep ? pv * P.drop_scale : 0.f;
+        sacc[e] = pv * ((keep ? dpacc[e] * P.drop_scale : 0.f) - d4[e4]);
+      } else {
+        pm[e] = pv;
+        sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 pf = acc_frag(pm, s);
+    const bf16x8 df = acc_frag(sacc, s);
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) {
+      dv[dt] = mfma32(pf, tr_frag(dos + ql * G::RW, G::RW, dt, s, lane), dv[dt]);
+      dk[dt] = mfma32(df, tr_frag(qs + ql * G::RW, G::RW, dt, s, lane), dk[dt]);
+    }
+  }
+}
+
+// =============================================================================================
+// backward dK, dV: grid (ceil(nt/8) * B*H*nstreams, 1, G); wave w owns key tiles ka = 8*bx + w and
+// kb = 8*bx + 7 - w and walks the query tiles of both together (queries >= kb feed both, the
+// ones in [ka, kb) only ka); the Q/dO chunk of the block is staged once per chunk
+// =============================================================================================
+template <int HS, bool DROP>
+__global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnBatch batch, int T,
+                                                                                         int H, float scale) {
+  using G = Geo<HS>;
+  constexpr int ROWS = Chunk<HS>::ROWS;
+  const AttnProblem& P = batch.p[blockIdx.z];
+  const int nb = ((T + 31) / 32 + 7) / 8;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int yy = tile / nb, bx = tile % nb;
+  const int nbh = gridDim.x / nb / P.nstreams;
+  if (yy >= nbh * P.nstreams) return;
+  const int j = yy / nbh;
+  const int bh = yy % nbh;
+  const int b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int nt = (T + 31) / 32;
+  const int kt0 = bx * 8;
+  const int q_lo = kt0 * 32;
+  const int nch = (T - q_lo + ROWS - 1) / ROWS;
+  const bool ragged = (T & 31) != 0;
+  const int64_t rowbase = (int64_t)b * T;
+  const float c2 = scale * kLog2e;
+  __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
+  __shared__ __attribute__((aligned(16))) bf16_t dos[ROWS * G::RW];  // dO chunk: row + tr reads
+  __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // log2-domain LSE, D of the chunk rows
+  for (int q = tid; q < ROWS * G::RW; q += 256)
+    if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
+
+  const bf16_t* kp = P.k[j] + head * P.kv_hstride;
+  const bf16_t* vp = P.v[j] + head * P.kv_hstride;
+  const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+  const float* lsep = P.lse[j] + (int64_t)bh * T;
+  const float* dvp = P.dvec[j] + (int64_t)bh * T;
+  const bf16_t* qp = P.q + head * HS;
+  const bf16_t* dop = P.dout + head * HS;
+  constexpr int NSL = 2 * ROWS / 256;
+  Stager<HS> st;
+  float sl[NSL];
+  auto load = [&](int r0) {
+    st.load(qp, P.q_ld, dop, P.dout_ld, rowbase, r0, T, tid);
+#pragma unroll
+    for (int u = 0; u < NSL; ++u) {
+      const int c = tid + 256 * u;
+      const int t = r0 + (c % ROWS);
+      sl[u] = t < T ? ((c < ROWS) ? lsep[t] * kLog2e : dvp[t]) : 0.f;
+    }
+  };
+  auto store = [&]() {
+    st.store(qs, G::RW, dos, G::RW, tid);
+#pragma unroll
+    for (int u = 0; u < NSL; ++u) {
+      const int c = tid + 256 * u;
+      lsd[c / ROWS][c % ROWS] = sl[u];
+    }
+  };
+  load(q_lo);
+  store();
+  __syncthreads();
+
+  const int ka = kt0 + w, kb = kt0 + 7 - w;  // ka < kb; lb implies la
+  const bool la = ka < nt, lb = kb < nt;
+  const int tka = ka * 32 + r, tkb = kb * 32 + r;
+  bf16x8 kfa[G::NKS], vfa[G::NKS], kfb[G::NKS], vfb[G::NKS];
+  f32x16 dka[G::ND], dva[G::ND], dkb[G::ND], dvb[G::ND];
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s) {
+    const int d0 = 16 * s + 8 * h;
+    const bool oka = la && tka < T && d0 < HS, okb = lb && tkb < T && d0 < HS;
+    kfa[s] = ld8(kp + (rowbase + tka) * P.kv_ld + d0, oka);
+    vfa[s] = ld8(vp + (rowbase + tka) * P.kv_ld + d0, oka);
+    kfb[s] = ld8(kp + (rowbase + tkb) * P.kv_ld + d0, okb);
+    vfb[s] = ld8(vp + (rowbase + tkb) * P.kv_ld + d0, okb);
+  }
+#pragma unroll
+  for (int dt = 0; dt < G::ND; ++dt) { zero16(dka[dt]); zero16(dva[dt]); zero16(dkb[dt]); zero16(dvb[dt]); }
+  for (int c = 0; c < nch; ++c) {
+    const int r0 = q_lo + c * ROWS;
+    const int qt_lo = r0 / 32, qt_hi = min(qt_lo + ROWS / 32, nt) - 1;
+    if (la) {
+      // queries in [ka, kb): tile a only (qt == ka its diagonal)
+      const int s_hi = lb ? min(kb - 1, qt_hi) : qt_hi;
+#pragma unroll 1
+      for (int qt = max(ka, qt_lo); qt <= s_hi; ++qt) {
+        if (qt == ka || (ragged && qt == nt - 1))
+          dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
+                                    dkey, bh * T, lane);
+        else
+          dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
+                                     dkey, bh * T, lane);
+      }
+    }
+    if (lb) {
+      // queries >= kb: both tiles (qt == kb is b's diagonal)
+#pragma unroll 1
+      for (int qt = max(kb, qt_lo); qt <= qt_hi; ++qt) {
+        if (qt == kb || (ragged && qt == nt - 1)) {
+          dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
+                                    dkey, bh * T, lane);
+          dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tkb, T, kfb, vfb, dkb, dvb, c2, P,
+                                    dkey, bh * T, lane);
+        } else {
+          dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
+                                     dkey, bh * T, lane);
+          dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tkb, T, kfb, vfb, dkb, dvb, c2, P,
+                                     dkey, bh * T, lane);
+        }
+      }
+    }
+    if (c + 1 < nch) {
+      __syncthreads();
+      load(q_lo + (c + 1) * ROWS);
+      store();
+      __syncthreads();
+    }
+  }
+  // dK/dV tiles: rows = key ((e&3)+8(e>>2)+4h), cols = d (lane)
+  bf16_t* dkp = P.dk[j] + head * P.dkv_hstride;
+  bf16_t* dvo = P.dv[j] + head * P.dkv_hstride;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const bool live = u == 0 ? la : lb;
+    if (!live) continue;
+    const f32x16* dk = u == 0 ? dka : dkb;
+    const f32x16* dv = u == 0 ? dva : dvb;
+    const int k0 = (u == 0 ? ka : kb) * 32;
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) {
+      const int d = dt * 32 + r;
+      if (d >= HS) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (key < T) {
+          dkp[(rowbase + key) * P.dkv_ld + d] = f2bf(dk[dt][e] * scale);
+          dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(dv[dt][e]);
+        }
+      }
+    }
+  }
+}
+
+// Block-uniform walk over (tile u, stream j, chunk c): the chunk (j, c) resident in LDS is reused
+// while consecutive steps share it (T <= ROWS with one stream: a single load for the whole block).
+struct ChunkWalk {
+  int ns, nch;
+  __device__ __forceinline__ bool next(int u, int j, int c, int& nj, int& nc) const {
+    nj = j; nc = c + 1;
+    int nu = u;
+    if (nc == nch) { nc = 0; ++nj; if (nj == ns) { nj = 0; ++nu; } }
+    return nu < 2 && (nj != j || nc != c);
+  }
+};
+
+// (one key tile at a time: the variant with two waves per SIMD at hs <= 32)
 // dK, dV: one 32x32 (queries x keys) tile; S, dP recomputed, dV += P^T dO, dK += dS^T Q
 template <int HS>
-__device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, const float* lsl, const float* dsl,
+__device__ __forceinline__ void dkdv1_tile(const bf16_t* qs, const bf16_t* dos, const float* lsl, const float* dsl,
                                           int ql, int q0, int tk, bool masked, int T,
                                           const bf16x8 (&kf)[Geo<HS>::NKS], const bf16x8 (&vf)[Geo<HS>::NKS],
                                           f32x16 (&dk)[Geo<HS>::ND], f32x16 (&dv)[Geo<HS>::ND], float c2,
@@ -533,7 +776,7 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
 // backward dK, dV: grid (ceil(nt/8), B*H*nstreams, G); wave w owns key tiles 8*bx + w, 8*bx + 7 - w
 // =============================================================================================
 template <int HS>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBatch batch, int T, int H, float scale) {
+__global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
@@ -615,7 +858,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBatch batch, int
         const int qt_lo = r0 / 32, qt_hi = min(qt_lo + ROWS / 32, nt) - 1;
         #pragma unroll 1
         for (int qt = max(kt, qt_lo); qt <= qt_hi; ++qt)
-          dkdv_tile<HS>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tk, qt == kt || (ragged && qt == nt - 1), T,
+          dkdv1_tile<HS>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tk, qt == kt || (ragged && qt == nt - 1), T,
                         kf, vf, dk, dv, c2, P, dkey, bh * T, lane);
       }
       if (reload) {
@@ -657,8 +900,25 @@ static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, b
     else hipLaunchKernelGGL((attn_fwd_kernel<HS, false>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
   } else {
     const int ns = bt.p[0].nstreams;
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<HS>, dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<HS>, dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    bool drop = false;
+    for (int g = 0; g < bt.count; ++g) drop = drop || bt.p[g].drop_thr != 0;
+    if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, true>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, false>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    // dK/dV: the paired walk needs 4 accumulator sets; at hs <= 32 the single-tile kernel keeps 2
+    // waves per SIMD and measured faster (C1: 103 vs 127 us), at hs = 64 the paired one
+    static const int pair = [] {
+      const char* e = getenv("MMT_DKDV_PAIR");
+      return e ? atoi(e) : -1;
+    }();
+    const bool paired = pair < 0 ? HS > 32 : pair != 0;
+    if (!paired)
+      hipLaunchKernelGGL(attn_bwd_dkdv1_kernel<HS>, dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    else if (drop)
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HS, true>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H,
+                         scale);
+    else
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HS, false>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T,
+                         H, scale);
   }
 }
 
