@@ -171,14 +171,18 @@ class HashDropout:
     def __init__(self, seed, p):
         self.seed = int(seed) & ((1 << 64) - 1)
         self.p = float(p)
-        self.thr = int(min(4294967295.0, max(1.0, math.floor(self.p * 4294967296.0))))
+        self.thr = int(min(65535.0, max(1.0, math.floor(self.p * 65536.0))))  # 16-bit (mmt_keep)
         self.scale = float(np.float32(1.0 / (1.0 - self.p)))
 
     def key(self, l, i, site):
         return int(mask_hash(self.seed & 0xFFFFFFFF, self.seed >> 32, (l * MAX_MOD + i) * 8 + site))
 
     def _mask(self, key, rows, cols):
-        keep = mask_hash(key, rows, cols) >= _U32(self.thr)
+        # one hash per column pair (2c, 2c+1), its 16-bit halves against thr (mmt_common.h mmt_keep)
+        cols = np.asarray(cols, dtype=np.int64)
+        h = mask_hash(key, rows, cols >> 1)
+        half = (h >> ((cols & 1).astype(_U32) * _U32(16))) & _U32(0xFFFF)
+        keep = half >= _U32(self.thr)
         return torch.from_numpy(keep.astype(np.float32) * np.float32(self.scale))
 
     def rowcol(self, l, i, site, B, T, C):

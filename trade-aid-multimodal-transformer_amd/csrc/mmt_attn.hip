@@ -176,9 +176,11 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
   m = mnew;
   if (DROP) {  // dropout on the probabilities (the normaliser l keeps every term)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
+    for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
       const uint32_t key = (uint32_t)(k0 + (e & 3) + 8 * (e >> 2) + 4 * h);
-      sacc[e] = (mmt_hash(dkey, drow, key) >= P.drop_thr) ? sacc[e] * P.drop_scale : 0.f;
+      const uint32_t hk = mmt_hash(dkey, drow, key >> 1);
+      sacc[e] = mmt_keep(hk, 0, P.drop_thr) ? sacc[e] * P.drop_scale : 0.f;
+      sacc[e + 1] = mmt_keep(hk, 1, P.drop_thr) ? sacc[e + 1] * P.drop_scale : 0.f;
     }
   }
 #pragma unroll
@@ -201,7 +203,7 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
 // (stream, chunk) is loaded once per block.
 // =============================================================================================
 template <int HS, bool DROP>
-__global__ __launch_bounds__(256, (HS <= 32 && !DROP) ? 2 : 1) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
+__global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
@@ -354,14 +356,20 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
     sacc = mfma32(kf, qf[s], sacc);
     dpacc = mfma32(vf, dof[s], dpacc);
   }
+  if (DROP) {
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
+      const uint32_t hk = mmt_hash(dkey, drow, (uint32_t)(k0 + (e & 3) + 8 * (e >> 2) + 4 * h) >> 1);
+      dpacc[e] = mmt_keep(hk, 0, P.drop_thr) ? dpacc[e] * P.drop_scale : 0.f;
+      dpacc[e + 1] = mmt_keep(hk, 1, P.drop_thr) ? dpacc[e + 1] * P.drop_scale : 0.f;
+    }
+  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
     float pv = ex2(sacc[e] * c2 - lse2);
     if (diag && key > tq) pv = 0.f;
-    float dp = dpacc[e];
-    if (DROP) dp = (mmt_hash(dkey, drow, (uint32_t)key) >= P.drop_thr) ? dp * P.drop_scale : 0.f;
-    sacc[e] = pv * (dp - dsum);  // dS^T
+    sacc[e] = pv * (dpacc[e] - dsum);  // dS^T
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -376,7 +384,7 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
 // forward each wave walks its two query tiles together
 // =============================================================================================
 template <int HS, bool DROP>
-__global__ __launch_bounds__(256, (HS <= 32 && !DROP) ? 2 : 1) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H,
+__global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H,
                                                                                        float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
@@ -540,7 +548,7 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
       float pv = ex2(sacc[e] * c2 - l4[e4]);
       if (masked && !(tk <= tq && tq < T)) pv = 0.f;
       if (DROP) {
-        const bool keep = mmt_hash(dkey, (uint32_t)(bhT + tq), (uint32_t)tk) >= P.drop_thr;
+        const bool keep = mmt_keep(mmt_hash(dkey, (uint32_t)(bhT + tq), (uint32_t)tk >> 1), (uint32_t)tk, P.drop_thr);
         pm[e] = keep ? pv * P.drop_scale : 0.f;
         sacc[e] = pv * ((keep ? dpacc[e] * P.drop_scale : 0.f) - d4[e4]);
       } else {
@@ -751,7 +759,7 @@ __device__ __forceinline__ void dkdv1_tile(const bf16_t* qs, const bf16_t* dos, 
       float pv = ex2(sacc[e] * c2 - l4[e4]);
       if (masked && !(tk <= tq && tq < T)) pv = 0.f;
       if (P.drop_thr) {
-        const bool keep = mmt_hash(dkey, (uint32_t)(bhT + tq), (uint32_t)tk) >= P.drop_thr;
+        const bool keep = mmt_keep(mmt_hash(dkey, (uint32_t)(bhT + tq), (uint32_t)tk >> 1), (uint32_t)tk, P.drop_thr);
         pm[e] = keep ? pv * P.drop_scale : 0.f;
         sacc[e] = pv * ((keep ? dpacc[e] * P.drop_scale : 0.f) - d4[e4]);
       } else {

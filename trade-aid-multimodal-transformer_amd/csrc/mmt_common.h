@@ -81,6 +81,13 @@ __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
   return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + bid / 8;
 }
 
+// dropout keep test: ONE 32-bit hash per column pair (2c, 2c+1) of a row, its 16-bit halves
+// compared against a 16-bit threshold thr = floor(p * 65536) (keep probability 1 - thr/65536):
+// half the hashing of one hash per element. `h` = mmt_hash(key, row, col >> 1).
+__host__ __device__ __forceinline__ bool mmt_keep(uint32_t h, uint32_t col, uint32_t thr) {
+  return ((h >> ((col & 1u) << 4)) & 0xFFFFu) >= thr;
+}
+
 // counter-based hash RNG (dropout masks); identical in forward and backward, and restated
 // bit-for-bit by the host (mmt_engine.hip: drop keys) and by oracle/mmt_oracle.py (mask_hash)
 #define MMT_STREAM_SALT 0x5BD1E995u

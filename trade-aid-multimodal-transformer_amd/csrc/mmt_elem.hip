@@ -141,9 +141,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBatch batch, int R, int C
           if (P.dx16) {
             if (drop) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e)
-                o[e] = (mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(4 * c4 + e)) >= P.drop_thr) ? o[e] * P.drop_scale
-                                                                                                   : 0.f;
+              for (int q = 0; q < 2; ++q) {  // columns 4*c4 .. +3: one hash per pair
+                const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(2 * c4 + q));
+                o[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? o[2 * q] * P.drop_scale : 0.f;
+                o[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? o[2 * q + 1] * P.drop_scale : 0.f;
+              }
             }
             reinterpret_cast<u32x2*>(P.dx16)[off] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
 #pragma unroll
@@ -539,9 +541,11 @@ __global__ __launch_bounds__(256) void drop_copy_kernel(DropCopyBatch batch, int
           if (row >= R) break;
           if (P.drop_thr) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              o[u][e] = (mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(4 * q + e)) >= P.drop_thr) ? o[u][e] * P.drop_scale
-                                                                                                   : 0.f;
+            for (int pq = 0; pq < 2; ++pq) {
+              const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(2 * q + pq));
+              o[u][2 * pq] = mmt_keep(hq, 0, P.drop_thr) ? o[u][2 * pq] * P.drop_scale : 0.f;
+              o[u][2 * pq + 1] = mmt_keep(hq, 1, P.drop_thr) ? o[u][2 * pq + 1] * P.drop_scale : 0.f;
+            }
           }
           reinterpret_cast<u32x2*>(P.dst)[(int64_t)row * C4 + q] =
               u32x2{pack2bf(o[u][0], o[u][1]), pack2bf(o[u][2], o[u][3])};

@@ -409,13 +409,13 @@ struct Runner {
   bool drop = false;  // dropout active for this forward / its backward
   uint64_t seed = 0;
 
-  // element kept iff mmt_hash(key, row, col) >= thr ; kept values scaled by 1 / (1 - p)
+  // element kept iff mmt_keep(mmt_hash(key, row, col >> 1), col, thr) ; kept values scaled by 1 / (1 - p)
   template <class Pm>
   void set_drop(Pm& p, int l, int i, int site) const {
     if (!drop) { p.drop_key = 0; p.drop_thr = 0; p.drop_scale = 1.f; return; }
     const double pr = c->cfg.dropout;
     p.drop_key = mmt_hash((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)((l * MAXM + i) * 8 + site));
-    p.drop_thr = (uint32_t)std::min(4294967295.0, std::max(1.0, std::floor(pr * 4294967296.0)));
+    p.drop_thr = (uint32_t)std::min(65535.0, std::max(1.0, std::floor(pr * 65536.0)));  // 16-bit halves (mmt_keep)
     p.drop_scale = (float)(1.0 / (1.0 - pr));
   }
 

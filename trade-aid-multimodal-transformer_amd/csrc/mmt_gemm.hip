@@ -151,7 +151,8 @@ __device__ __forceinline__ float epi_scalar(const GemmProblem& P, float* o32, fl
   if (EPI == EPI_DTANH_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r *= (1.0f - t * t); }
   if (EPI == EPI_DRELU_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r = t > 0.0f ? r : 0.0f; }
   if (EPI == EPI_BIAS_RESID_F32) {
-    if (P.drop_thr) r = (mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)n) >= P.drop_thr) ? r * P.drop_scale : 0.0f;
+    if (P.drop_thr)
+      r = mmt_keep(mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)n >> 1), (uint32_t)n, P.drop_thr) ? r * P.drop_scale : 0.0f;
     r += P.resid[(int64_t)m * P.ldres + n];
   }
   const int64_t o = (int64_t)m * P.ldc + n;
@@ -406,8 +407,11 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
           }
           if (EPI == EPI_BIAS_RESID_F32 && P.drop_thr) {  // dropout on the branch output, then residual add
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              r[e] = (mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n + e)) >= P.drop_thr) ? r[e] * P.drop_scale : 0.0f;
+            for (int q = 0; q < 4; ++q) {  // n is even: one hash per column pair
+              const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n >> 1) + q);
+              r[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? r[2 * q] * P.drop_scale : 0.0f;
+              r[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? r[2 * q + 1] * P.drop_scale : 0.0f;
+            }
           }
           if (HAS_RES) {
 #pragma unroll

@@ -42,7 +42,8 @@ struct GemmProblem {
   int M, N, K;
   int lda, ldb, ldc, ldaux, ldres, ldo16;
   // dropout of the branch output (EPI_BIAS_RESID_F32 only; drop_thr == 0: off):
-  // element (m, n) kept iff mmt_hash(drop_key, m, n) >= drop_thr, kept values scaled by drop_scale
+  // element (m, n) kept iff mmt_keep(mmt_hash(drop_key, m, n >> 1), n, drop_thr) (16-bit threshold,
+  // mmt_common.h), kept values scaled by drop_scale
   uint32_t drop_key, drop_thr;
   float drop_scale;
   // fused bias gradient (bf16-output epilogues, SWAP layouts): dbias[n] += sum_m out[m, n]
@@ -111,7 +112,7 @@ struct AttnProblem {
   int nstreams;
   // dropout on the normalised probabilities (drop_thr == 0: off): element (query t, key s) of
   // stream j, head slot bh = b*H + h, kept iff mmt_hash(mmt_hash(drop_key, j, MMT_STREAM_SALT),
-  // bh*T + t, s) >= drop_thr; kept probabilities scaled by drop_scale
+  // bh*T + t, s >> 1) passes mmt_keep(., s, drop_thr); kept probabilities scaled by drop_scale
   uint32_t drop_key, drop_thr;
   float drop_scale;
 };
