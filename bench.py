@@ -127,7 +127,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0)
-    ap.add_argument("--dropout", type=float, default=0.0)
+    ap.add_argument("--dropout", type=float, default=0.1,
+                    help="dropout p; SURVEY.md §8d: 0.1 for throughput runs (0.0 only for parity runs)")
     ap.add_argument("--probe", default="ffn0", help="engine launch label timed live for the roofline line")
     ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM pipeline variant (mmt_gemm_set_variant)")
     ap.add_argument("--bucket-mb", type=int, default=32, help="DP gradient all-reduce bucket size")

@@ -126,6 +126,48 @@ def test_dropout_step_matches_oracle_masks(name, p):
         assert rel(lg[i], torch.from_numpy(z[f"logits.{i}"])) < 2e-2, i
 
 
+@pytest.mark.parametrize("C,H,T,cross,p", [(64, 2, 288, [True, False], 0.2), (128, 2, 160, [False, True], 0.1)])
+def test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p):
+    """Dropout at sequence lengths past one LDS chunk (hs 32: 256 rows, hs 64: 128 rows) with a
+    ragged last tile: the keep bits of attn_mask_kernel, staged chunk by chunk in all three
+    attention kernels, against the oracle's hash masks (random init, the oracle as reference)."""
+    import mmt_oracle as O
+    import model as mmt_model
+    V = [13, 7]
+    ocfg = O.OracleConfig(C, H, 1, T, V, cross)
+    g = torch.Generator().manual_seed(5)
+    sd = O.init_params(ocfg, g)
+    config_utils._config_cache = {"n_embd": C, "n_head": H, "n_layer": 1, "block_size": T, "dropout": p,
+                                  "device": "cuda", "batch_size": 2, "eval_iters": 1}
+    params = [[None] * 8 + [c] + [None] * 3 for c in cross]
+    m = mmt_model.MultimodalTransformer(len(V), V, params).to("cuda")
+    full = {k: v for k, v in m.state_dict().items() if k.endswith("tril")}
+    full.update(sd)
+    m.load_state_dict(full, strict=True)
+    m.train()
+    idx = [torch.randint(0, v, (2, T), generator=g) for v in V]
+    tgt = [torch.randint(0, v, (2, T), generator=g) for v in V]
+    logits, losses = m([t.cuda() for t in idx], [t.cuda() for t in tgt])
+    sum(losses).backward()
+    torch.cuda.synchronize()
+    ocfg.dropout = p
+    r_logits, r_losses, r_grads = O.forward_backward(sd, ocfg, idx, tgt, hash_dropout=O.HashDropout(m.last_dropout_seed, p))
+    ocfg.dropout = 0.0
+    _, _, n_grads = O.forward_backward(sd, ocfg, idx, tgt)
+    got = torch.stack([l.detach().cpu() for l in losses])
+    assert torch.allclose(got, torch.stack(r_losses), rtol=5e-3, atol=5e-3)
+    for i in range(len(V)):
+        assert rel(logits[i], r_logits[i]) < 2e-2, i
+    names = [n for n, _ in m.named_reference_tensors()]
+    pairs = [(g_.flatten().cpu(), r_grads[k].flatten(), n_grads[k].flatten())
+             for k, g_ in zip(names, _grad_views(m)) if r_grads.get(k) is not None and g_.numel()]
+    allg = torch.cat([a for a, _, _ in pairs])
+    allr = torch.cat([b for _, b, _ in pairs])
+    alln = torch.cat([c for _, _, c in pairs])
+    assert rel(allg, allr) < 3e-2
+    assert rel(allg, alln) > 3 * max(rel(allg, allr), 1e-2)  # the masks act
+
+
 def _grad_views(m):
     g = m.flat_params.grad
     for name, off, shp, _ in m._tensors:

@@ -16,9 +16,14 @@
 //   dK, dV   S = Q K^T, dP = dO V^T (queries on rows); dV += P^T dO, dK += dS^T Q with P and dS
 //            taken from registers as the A operand and dO / Q by transposed LDS reads.
 // Head sizes 8..64: padded to 16 on the reduction side and to 32 on the output side.
-// Dropout (model.py:69, 151: applied to the normalised probabilities): a counter-hash mask
-// regenerated identically in all three kernels; O = (P.Z) V with Z = mask / (1 - p), so
-// dV = (P.Z)^T dO, dS = P.(Z.dP - D) with D = rowsum(dO.O) unchanged.
+// Dropout (model.py:69, 151: applied to the normalised probabilities): a counter-hash mask,
+// O = (P.Z) V with Z = mask / (1 - p), so dV = (P.Z)^T dO, dS = P.(Z.dP - D) with D = rowsum(dO.O)
+// unchanged. The hash runs once, in attn_mask_kernel (launched on a side stream, overlapping the
+// GEMMs before the attention), which stores one keep bit per element in the S^T accumulator order
+// (AttnProblem::dmask). The three attention kernels stage the bits of their chunk in LDS next to
+// K/V (Q/dO) and apply them with no hashing: the forward and dQ pass turn a pair of mask dwords
+// into the lane mask of a v_cndmask (inverse ballot), the dK/dV pass (keys on lanes) extracts its
+// bit per element. 1/(1-p) is folded into the output normalisation / dV write-out.
 #include <stdlib.h>
 
 #include "mmt_common.h"
@@ -77,6 +82,17 @@ __device__ __forceinline__ void zero16(f32x16& a) {
   for (int e = 0; e < 16; ++e) a[e] = 0.f;
 }
 
+// keep predicate of accumulator element e of an S^T tile (queries on lanes) whose 32 mask dwords
+// lanes 0..31 hold in mv: dwords 2e, 2e+1 are exactly the lane mask of element e
+__device__ __forceinline__ bool keep_st(uint32_t mv, int e) {
+  const uint64_t mk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mv, 2 * e + 1) << 32) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mv, 2 * e);
+  return __builtin_amdgcn_inverse_ballot_w64(mk);
+}
+
+// dword of an S^T mask tile that holds key r's keep bits over the tile's 32 queries
+__device__ __forceinline__ int key_dword(int r) { return 2 * ((r & 3) + 4 * (r >> 3)) + ((r >> 2) & 1); }
+
 }  // namespace
 
 // =============================================================================================
@@ -125,6 +141,40 @@ struct Stager {
   }
 };
 
+// Dropout keep bits of one staged chunk: LDS [8 block tiles][KT chunk tiles][32 dwords]. The block
+// tiles are the block's 8 query tiles (forward, dQ) or key tiles (dK/dV); the chunk tiles are the
+// key (query) tiles of the staged chunk. Tiles above the causal diagonal are left as zeros.
+template <int HS>
+struct MaskStager {
+  static constexpr int KT = Chunk<HS>::ROWS / 32;
+  static constexpr int N4 = 8 * KT * 8;  // 16-B pieces
+  static constexpr int PER = (N4 + 255) / 256;
+  static constexpr int DWORDS = 8 * KT * 32;
+  u32x4 v[PER];
+  // b0: first block tile, c0: first chunk tile; blk_q: block tiles are query tiles
+  __device__ __forceinline__ void load(const uint32_t* base, int bh, int nt, int b0, int c0, bool blk_q, int tid) {
+    const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = tid + 256 * u;
+      v[u] = u32x4{0u, 0u, 0u, 0u};
+      if (N4 % 256 == 0 || c < N4) {
+        const int i = c / (KT * 8), k = (c / 8) % KT, p = c % 8;
+        const int qt = blk_q ? b0 + i : c0 + k, kt = blk_q ? c0 + k : b0 + i;
+        if (qt < nt && kt <= qt)
+          v[u] = *reinterpret_cast<const u32x4*>(base + ((int64_t)bh * ntri + qt * (qt + 1) / 2 + kt) * 32 + p * 4);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(uint32_t* lds, int tid) const {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = tid + 256 * u;
+      if (N4 % 256 == 0 || c < N4) *reinterpret_cast<u32x4*>(lds + 4 * c) = v[u];
+    }
+  }
+};
+
 __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -134,10 +184,10 @@ constexpr float kLn2 = 0.6931471805599453f;
 template <int HS, bool diag, bool DROP>
 __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq,
                                          const bf16x8 (&qf)[Geo<HS>::NKS], float& m, float& l,
-                                         f32x16 (&oacc)[Geo<HS>::ND], float c2, const AttnProblem& P, uint32_t dkey,
-                                         uint32_t drow, int lane) {
+                                         f32x16 (&oacc)[Geo<HS>::ND], float c2, const uint32_t* mt, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
+  const uint32_t mv = DROP ? mt[r] : 0u;  // this tile's keep bits (LDS)
   f32x16 sacc;
   zero16(sacc);
 #pragma unroll
@@ -174,14 +224,9 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
   rs += __shfl_xor(rs, 32, 64);
   l = l * alpha + rs;
   m = mnew;
-  if (DROP) {  // dropout on the probabilities (the normaliser l keeps every term)
+  if (DROP) {  // dropout on the probabilities (the normaliser l keeps every term; 1/(1-p) at the end)
 #pragma unroll
-    for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
-      const uint32_t key = (uint32_t)(k0 + (e & 3) + 8 * (e >> 2) + 4 * h);
-      const uint32_t hk = mmt_hash(dkey, drow, key >> 1);
-      sacc[e] = mmt_keep(hk, 0, P.drop_thr) ? sacc[e] * P.drop_scale : 0.f;
-      sacc[e + 1] = mmt_keep(hk, 1, P.drop_thr) ? sacc[e + 1] * P.drop_scale : 0.f;
-    }
+    for (int e = 0; e < 16; ++e) sacc[e] = keep_st(mv, e) ? sacc[e] : 0.f;
   }
 #pragma unroll
   for (int dt = 0; dt < G::ND; ++dt)
@@ -223,17 +268,23 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBat
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::TW];
+  using MS = MaskStager<HS>;
+  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];
   for (int q = tid; q < ROWS * G::RW; q += 256) if (q % G::RW >= HS) ks[q] = 0;
   for (int q = tid; q < ROWS * G::TW; q += 256) if (q % G::TW >= HS) vs[q] = 0;
   Stager<HS> st;
+  MS mst;
   st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
+  if (DROP) mst.load(P.dmask[0], bh, nt, qt0, 0, true, tid);
   st.store(ks, G::RW, vs, G::TW, tid);
+  if (DROP) mst.store(msk, tid);
   __syncthreads();
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb
   const bool la = qa < nt, lb = qb < nt;     // lb implies la
   const int tqa = qa * 32 + r, tqb = qb * 32 + r;
-  const uint32_t drowa = (uint32_t)(bh * T + tqa), drowb = (uint32_t)(bh * T + tqb);
+  const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
+  const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
   bf16x8 qfa[G::NKS], qfb[G::NKS];
   f32x16 ota[G::ND], otb[G::ND];
 #pragma unroll
@@ -245,7 +296,6 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBat
 #pragma unroll
   for (int dt = 0; dt < G::ND; ++dt) { zero16(ota[dt]); zero16(otb[dt]); }
   for (int j = 0; j < P.nstreams; ++j) {
-    const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
     float ma = -INFINITY, lsa = 0.f, mb = -INFINITY, lsb = 0.f;
     f32x16 oa[G::ND], ob[G::ND];
 #pragma unroll
@@ -257,24 +307,24 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBat
         int kt = kt_lo;
 #pragma unroll 1
         for (; kt <= min(qa - 1, kt_hi); ++kt) {  // both tiles, off the diagonal
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, P, dkey, drowa, lane);
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, P, dkey, drowb, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mska + (kt - kt_lo) * 32, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (kt - kt_lo) * 32, lane);
         }
         if (qa >= kt_lo && qa <= kt_hi) {  // tile a's diagonal, tile b off it
-          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, P, dkey, drowa, lane);
-          fwd_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, mb, lsb, ob, c2, P, dkey, drowb, lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mska + (qa - kt_lo) * 32, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (qa - kt_lo) * 32, lane);
         }
 #pragma unroll 1
         for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, P, dkey, drowb, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (kt - kt_lo) * 32, lane);
         if (qb >= kt_lo && qb <= kt_hi)
-          fwd_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, mb, lsb, ob, c2, P, dkey, drowb, lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (qb - kt_lo) * 32, lane);
       } else if (la) {
 #pragma unroll 1
         for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, P, dkey, drowa, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mska + (kt - kt_lo) * 32, lane);
         if (qa >= kt_lo && qa <= kt_hi)
-          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, P, dkey, drowa, lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mska + (qa - kt_lo) * 32, lane);
       }
       // next (stream, chunk) resident for the whole block
       int nj = j, nc = c + 1;
@@ -283,7 +333,9 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBat
         __syncthreads();
         st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
                 T, tid);
+        if (DROP) mst.load(P.dmask[nj], bh, nt, qt0, nc * (ROWS / 32), true, tid);
         st.store(ks, G::RW, vs, G::TW, tid);
+        if (DROP) mst.store(msk, tid);
         __syncthreads();
       }
     }
@@ -295,7 +347,7 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBat
       f32x16* o = u == 0 ? oa : ob;
       f32x16* ot = u == 0 ? ota : otb;
       const float m = u == 0 ? ma : mb, l = u == 0 ? lsa : lsb;
-      const float inv = (l > 0.f) ? 1.f / l : 0.f;
+      const float inv = (l > 0.f) ? (DROP ? P.drop_scale : 1.f) / l : 0.f;
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
@@ -343,9 +395,10 @@ template <int HS, bool diag, bool DROP>
 __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq,
                                         const bf16x8 (&qf)[Geo<HS>::NKS], const bf16x8 (&dof)[Geo<HS>::NKS],
                                         float lse2, float dsum, f32x16 (&dq)[Geo<HS>::ND], float c2,
-                                        const AttnProblem& P, uint32_t dkey, uint32_t drow, int lane) {
+                                        const AttnProblem& P, const uint32_t* mt, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
+  const uint32_t mv = DROP ? mt[r] : 0u;  // this tile's keep bits (LDS)
   f32x16 sacc, dpacc;
   zero16(sacc);
   zero16(dpacc);
@@ -356,20 +409,13 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
     sacc = mfma32(kf, qf[s], sacc);
     dpacc = mfma32(vf, dof[s], dpacc);
   }
-  if (DROP) {
-#pragma unroll
-    for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
-      const uint32_t hk = mmt_hash(dkey, drow, (uint32_t)(k0 + (e & 3) + 8 * (e >> 2) + 4 * h) >> 1);
-      dpacc[e] = mmt_keep(hk, 0, P.drop_thr) ? dpacc[e] * P.drop_scale : 0.f;
-      dpacc[e + 1] = mmt_keep(hk, 1, P.drop_thr) ? dpacc[e + 1] * P.drop_scale : 0.f;
-    }
-  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
     float pv = ex2(sacc[e] * c2 - lse2);
     if (diag && key > tq) pv = 0.f;
-    sacc[e] = pv * (dpacc[e] - dsum);  // dS^T
+    if (DROP) sacc[e] = pv * (keep_st(mv, e) ? fmaf(dpacc[e], P.drop_scale, -dsum) : -dsum);  // dS^T
+    else sacc[e] = pv * (dpacc[e] - dsum);
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -403,18 +449,24 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_bwd_dq_kernel(Attn
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::RW];  // V chunk: row reads
+  using MS = MaskStager<HS>;
+  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];
   for (int q = tid; q < ROWS * G::RW; q += 256)
     if (q % G::RW >= HS) { ks[q] = 0; vs[q] = 0; }
   Stager<HS> st;
+  MS mst;
   st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
+  if (DROP) mst.load(P.dmask[0], bh, nt, qt0, 0, true, tid);
   st.store(ks, G::RW, vs, G::RW, tid);
+  if (DROP) mst.store(msk, tid);
   __syncthreads();
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb; lb implies la
   const bool la = qa < nt, lb = qb < nt;
   const int tqa = qa * 32 + r, tqb = qb * 32 + r;
   const bool oka = la && tqa < T, okb = lb && tqb < T;
-  const uint32_t drowa = (uint32_t)(bh * T + tqa), drowb = (uint32_t)(bh * T + tqb);
+  const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
+  const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
   bf16x8 qfa[G::NKS], dofa[G::NKS], qfb[G::NKS], dofb[G::NKS];
   f32x16 dqa[G::ND], dqb[G::ND];
 #pragma unroll
@@ -449,7 +501,6 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_bwd_dq_kernel(Attn
     }
     const float lsa = oka ? P.lse[j][(int64_t)bh * T + tqa] * kLog2e : 0.f;
     const float lsb = okb ? P.lse[j][(int64_t)bh * T + tqb] * kLog2e : 0.f;
-    const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
     for (int c = 0; c < nch; ++c) {
       const int kt_lo = c * (ROWS / 32);
       const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
@@ -457,31 +508,31 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_bwd_dq_kernel(Attn
         int kt = kt_lo;
 #pragma unroll 1
         for (; kt <= min(qa - 1, kt_hi); ++kt) {
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, dkey, drowa,
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (kt - kt_lo) * 32,
                                    lane);
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, dkey, drowb,
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (kt - kt_lo) * 32,
                                    lane);
         }
         if (qa >= kt_lo && qa <= kt_hi) {
-          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, dkey, drowa,
+          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (qa - kt_lo) * 32,
                                   lane);
-          dq_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, dkey, drowb,
+          dq_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (qa - kt_lo) * 32,
                                    lane);
         }
 #pragma unroll 1
         for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, dkey, drowb,
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (kt - kt_lo) * 32,
                                    lane);
         if (qb >= kt_lo && qb <= kt_hi)
-          dq_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, dkey, drowb,
+          dq_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (qb - kt_lo) * 32,
                                   lane);
       } else if (la) {
 #pragma unroll 1
         for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, dkey, drowa,
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (kt - kt_lo) * 32,
                                    lane);
         if (qa >= kt_lo && qa <= kt_hi)
-          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, dkey, drowa,
+          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (qa - kt_lo) * 32,
                                   lane);
       }
       int nj = j, nc = c + 1;
@@ -490,7 +541,9 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_bwd_dq_kernel(Attn
         __syncthreads();
         st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
                 T, tid);
+        if (DROP) mst.load(P.dmask[nj], bh, nt, qt0, nc * (ROWS / 32), true, tid);
         st.store(ks, G::RW, vs, G::RW, tid);
+        if (DROP) mst.store(msk, tid);
         __syncthreads();
       }
     }
@@ -524,9 +577,11 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
                                           int ql, int q0, int tk, int T,
                                           const bf16x8 (&kf)[Geo<HS>::NKS], const bf16x8 (&vf)[Geo<HS>::NKS],
                                           f32x16 (&dk)[Geo<HS>::ND], f32x16 (&dv)[Geo<HS>::ND], float c2,
-                                          const AttnProblem& P, uint32_t dkey, int bhT, int lane) {
+                                          const AttnProblem& P, const uint32_t* mt, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
+  // key r's keep bits over the tile's queries, this lane's half (queries 8g + 4h + e4) at bits 8g + e4
+  const uint32_t mw = DROP ? mt[key_dword(r)] >> (4 * h) : 0u;
   f32x16 sacc, dpacc, pm;
   zero16(sacc);
   zero16(dpacc);
@@ -547,10 +602,12 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
       const int tq = q0 + 8 * g + 4 * h + e4;
       float pv = ex2(sacc[e] * c2 - l4[e4]);
       if (masked && !(tk <= tq && tq < T)) pv = 0.f;
-      if (DROP) {
-        const bool keep = mmt_keep(mmt_hash(dkey, (uint32_t)(bhT + tq), (uint32_t)tk >> 1), (uint32_t)tk, P.drop_thr);
-        pm[e] = keep ? pv * P.drop_scale : 0.f;
-        sacc[e] = pv * ((keep ? dpacc[e] * P.drop_scale : 0.f) - d4[e4]);
+      if (DROP) {  // pm = Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
+        const int km = (int)(mw << (31 - (8 * g + e4))) >> 31;  // all ones iff kept
+        const float nd = -d4[e4];
+        const float t = fmaf(dpacc[e], P.drop_scale, nd);
+        pm[e] = __int_as_float(__float_as_int(pv) & km);
+        sacc[e] = pv * __int_as_float((__float_as_int(t) & km) | (__float_as_int(nd) & ~km));
       } else {
         pm[e] = pv;
         sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
@@ -600,21 +657,24 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
   __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) bf16_t dos[ROWS * G::RW];  // dO chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // log2-domain LSE, D of the chunk rows
+  using MS = MaskStager<HS>;
+  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // [key tile][chunk q tile]
   for (int q = tid; q < ROWS * G::RW; q += 256)
     if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
 
   const bf16_t* kp = P.k[j] + head * P.kv_hstride;
   const bf16_t* vp = P.v[j] + head * P.kv_hstride;
-  const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
   const float* lsep = P.lse[j] + (int64_t)bh * T;
   const float* dvp = P.dvec[j] + (int64_t)bh * T;
   const bf16_t* qp = P.q + head * HS;
   const bf16_t* dop = P.dout + head * HS;
   constexpr int NSL = 2 * ROWS / 256;
   Stager<HS> st;
+  MS mst;
   float sl[NSL];
   auto load = [&](int r0) {
     st.load(qp, P.q_ld, dop, P.dout_ld, rowbase, r0, T, tid);
+    if (DROP) mst.load(P.dmask[j], bh, nt, kt0, r0 / 32, false, tid);
 #pragma unroll
     for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
@@ -624,6 +684,7 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
   };
   auto store = [&]() {
     st.store(qs, G::RW, dos, G::RW, tid);
+    if (DROP) mst.store(msk, tid);
 #pragma unroll
     for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
@@ -637,6 +698,8 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
   const int ka = kt0 + w, kb = kt0 + 7 - w;  // ka < kb; lb implies la
   const bool la = ka < nt, lb = kb < nt;
   const int tka = ka * 32 + r, tkb = kb * 32 + r;
+  const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of ka, kb
+  const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile qt - qt_lo)
   bf16x8 kfa[G::NKS], vfa[G::NKS], kfb[G::NKS], vfb[G::NKS];
   f32x16 dka[G::ND], dva[G::ND], dkb[G::ND], dvb[G::ND];
 #pragma unroll
@@ -660,10 +723,10 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
       for (int qt = max(ka, qt_lo); qt <= s_hi; ++qt) {
         if (qt == ka || (ragged && qt == nt - 1))
           dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
-                                    dkey, bh * T, lane);
+                                    mska + (qt - qt_lo) * 32, lane);
         else
           dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
-                                     dkey, bh * T, lane);
+                                     mska + (qt - qt_lo) * 32, lane);
       }
     }
     if (lb) {
@@ -672,14 +735,14 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
       for (int qt = max(kb, qt_lo); qt <= qt_hi; ++qt) {
         if (qt == kb || (ragged && qt == nt - 1)) {
           dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
-                                    dkey, bh * T, lane);
+                                    mska + (qt - qt_lo) * 32, lane);
           dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tkb, T, kfb, vfb, dkb, dvb, c2, P,
-                                    dkey, bh * T, lane);
+                                    mskb + (qt - qt_lo) * 32, lane);
         } else {
           dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
-                                     dkey, bh * T, lane);
+                                     mska + (qt - qt_lo) * 32, lane);
           dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tkb, T, kfb, vfb, dkb, dvb, c2, P,
-                                     dkey, bh * T, lane);
+                                     mskb + (qt - qt_lo) * 32, lane);
         }
       }
     }
@@ -709,7 +772,7 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
         const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (key < T) {
           dkp[(rowbase + key) * P.dkv_ld + d] = f2bf(dk[dt][e] * scale);
-          dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(dv[dt][e]);
+          dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
         }
       }
     }
@@ -730,14 +793,16 @@ struct ChunkWalk {
 
 // (one key tile at a time: the variant with two waves per SIMD at hs <= 32)
 // dK, dV: one 32x32 (queries x keys) tile; S, dP recomputed, dV += P^T dO, dK += dS^T Q
-template <int HS>
+template <int HS, bool DROP>
 __device__ __forceinline__ void dkdv1_tile(const bf16_t* qs, const bf16_t* dos, const float* lsl, const float* dsl,
                                           int ql, int q0, int tk, bool masked, int T,
                                           const bf16x8 (&kf)[Geo<HS>::NKS], const bf16x8 (&vf)[Geo<HS>::NKS],
                                           f32x16 (&dk)[Geo<HS>::ND], f32x16 (&dv)[Geo<HS>::ND], float c2,
-                                          const AttnProblem& P, uint32_t dkey, int bhT, int lane) {
+                                          const AttnProblem& P, const uint32_t* mt, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
+  // key r's keep bits over the tile's queries, this lane's half (queries 8g + 4h + e4) at bits 8g + e4
+  const uint32_t mw = DROP ? mt[key_dword(r)] >> (4 * h) : 0u;
   f32x16 sacc, dpacc, pm;
   zero16(sacc);
   zero16(dpacc);
@@ -758,10 +823,12 @@ __device__ __forceinline__ void dkdv1_tile(const bf16_t* qs, const bf16_t* dos, 
       const int tq = q0 + 8 * g + 4 * h + e4;
       float pv = ex2(sacc[e] * c2 - l4[e4]);
       if (masked && !(tk <= tq && tq < T)) pv = 0.f;
-      if (P.drop_thr) {
-        const bool keep = mmt_keep(mmt_hash(dkey, (uint32_t)(bhT + tq), (uint32_t)tk >> 1), (uint32_t)tk, P.drop_thr);
-        pm[e] = keep ? pv * P.drop_scale : 0.f;
-        sacc[e] = pv * ((keep ? dpacc[e] * P.drop_scale : 0.f) - d4[e4]);
+      if (DROP) {  // pm = Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
+        const int km = (int)(mw << (31 - (8 * g + e4))) >> 31;  // all ones iff kept
+        const float nd = -d4[e4];
+        const float t = fmaf(dpacc[e], P.drop_scale, nd);
+        pm[e] = __int_as_float(__float_as_int(pv) & km);
+        sacc[e] = pv * __int_as_float((__float_as_int(t) & km) | (__float_as_int(nd) & ~km));
       } else {
         pm[e] = pv;
         sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
@@ -783,7 +850,7 @@ __device__ __forceinline__ void dkdv1_tile(const bf16_t* qs, const bf16_t* dos, 
 // =============================================================================================
 // backward dK, dV: grid (ceil(nt/8), B*H*nstreams, G); wave w owns key tiles 8*bx + w, 8*bx + 7 - w
 // =============================================================================================
-template <int HS>
+template <int HS, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
@@ -808,21 +875,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, in
   __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) bf16_t dos[ROWS * G::RW];  // dO chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // log2-domain LSE, D of the chunk rows
+  using MS = MaskStager<HS>;
+  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // [key tile][chunk q tile]
   for (int q = tid; q < ROWS * G::RW; q += 256)
     if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
 
   const bf16_t* kp = P.k[j] + head * P.kv_hstride;
   const bf16_t* vp = P.v[j] + head * P.kv_hstride;
-  const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
   const float* lsep = P.lse[j] + (int64_t)bh * T;
   const float* dvp = P.dvec[j] + (int64_t)bh * T;
   const bf16_t* qp = P.q + head * HS;
   const bf16_t* dop = P.dout + head * HS;
   constexpr int NSL = 2 * ROWS / 256;
   Stager<HS> st;
+  MS mst;
   float sl[NSL];
   auto load = [&](int r0) {
     st.load(qp, P.q_ld, dop, P.dout_ld, rowbase, r0, T, tid);
+    if (DROP) mst.load(P.dmask[j], bh, nt, kt0, r0 / 32, false, tid);
 #pragma unroll
     for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
@@ -832,6 +902,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, in
   };
   auto store = [&]() {
     st.store(qs, G::RW, dos, G::RW, tid);
+    if (DROP) mst.store(msk, tid);
 #pragma unroll
     for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
@@ -866,8 +937,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, in
         const int qt_lo = r0 / 32, qt_hi = min(qt_lo + ROWS / 32, nt) - 1;
         #pragma unroll 1
         for (int qt = max(kt, qt_lo); qt <= qt_hi; ++qt)
-          dkdv1_tile<HS>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tk, qt == kt || (ragged && qt == nt - 1), T,
-                        kf, vf, dk, dv, c2, P, dkey, bh * T, lane);
+          dkdv1_tile<HS, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tk, qt == kt || (ragged && qt == nt - 1),
+                               T, kf, vf, dk, dv, c2, P, msk + ((kt - kt0) * MS::KT + (qt - qt_lo)) * 32, lane);
       }
       if (reload) {
         __syncthreads();
@@ -890,7 +961,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, in
           const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
           if (key < T) {
             dkp[(rowbase + key) * P.dkv_ld + d] = f2bf(dk[dt][e] * scale);
-            dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(dv[dt][e]);
+            dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
           }
         }
       }
@@ -919,8 +990,12 @@ static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, b
       return e ? atoi(e) : -1;
     }();
     const bool paired = pair < 0 ? HS > 32 : pair != 0;
-    if (!paired)
-      hipLaunchKernelGGL(attn_bwd_dkdv1_kernel<HS>, dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    if (!paired && drop)
+      hipLaunchKernelGGL((attn_bwd_dkdv1_kernel<HS, true>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H,
+                         scale);
+    else if (!paired)
+      hipLaunchKernelGGL((attn_bwd_dkdv1_kernel<HS, false>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T,
+                         H, scale);
     else if (drop)
       hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HS, true>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H,
                          scale);
@@ -933,8 +1008,12 @@ static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, b
 static hipError_t attn_dispatch(const AttnBatch& b, int B, int T, int H, int hs, float scale, bool bwd,
                                 hipStream_t s) {
   if (b.count == 0 || B == 0 || T == 0) return hipSuccess;
-  for (int g = 0; g < b.count; ++g)
+  for (int g = 0; g < b.count; ++g) {
     if (b.p[g].nstreams < 1 || b.p[g].nstreams > MMT_MAX_STREAMS) return hipErrorInvalidValue;
+    if (b.p[g].drop_thr)  // dropout reads the keep bits of mmt_launch_attn_mask
+      for (int j = 0; j < b.p[g].nstreams; ++j)
+        if (!b.p[g].dmask[j]) return hipErrorInvalidValue;
+  }
   if (bwd) {  // all problems in a bwd batch must share nstreams (grid.y = B*H*nstreams)
     for (int g = 1; g < b.count; ++g)
       if (b.p[g].nstreams != b.p[0].nstreams) return hipErrorInvalidValue;
@@ -956,4 +1035,60 @@ hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, 
 }
 hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s) {
   return attn_dispatch(b, B, T, H, hs, scale, true, s);
+}
+
+// =============================================================================================
+// Dropout keep bits (AttnProblem::dmask): one wave per 32x32 (query tile, key tile <= query tile)
+// tile of one (stream, bh). Lane (r, h) hashes query r's key pairs in the accumulator order of an
+// S^T tile (one hash per key pair, mmt_keep on its 16-bit halves), and the ballot of each element
+// is the element's two mask dwords. Pure VALU work with no inputs: launched on a side stream it
+// overlaps the MFMA-bound GEMMs ahead of the attention.
+// =============================================================================================
+__global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH, int T) {
+  const AttnProblem& P = batch.p[blockIdx.z];
+  const int nt = (T + 31) / 32;
+  const int ntri = nt * (nt + 1) / 2;
+  const int64_t per = (int64_t)BH * ntri;  // tiles per stream
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (P.drop_thr == 0 || t >= per * P.nstreams) return;  // wave-uniform
+  const int j = (int)(t / per);
+  const int64_t tt = t - (int64_t)j * per;
+  const int bh = (int)(tt / ntri), tri = (int)(tt % ntri);
+  int qt = (int)((sqrtf(8.f * (float)tri + 1.f) - 1.f) * 0.5f);
+  while (qt > 0 && qt * (qt + 1) / 2 > tri) --qt;
+  while ((qt + 1) * (qt + 2) / 2 <= tri) ++qt;
+  const int kt = tri - qt * (qt + 1) / 2;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+  const uint32_t drow = (uint32_t)(bh * T + qt * 32 + r);
+  uint32_t out = 0;  // lane L < 32 collects dword L = half (L & 1) of element (L >> 1)'s ballot
+#pragma unroll
+  for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
+    const uint32_t key = (uint32_t)(kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h);
+    const uint32_t hk = mmt_hash(dkey, drow, key >> 1);
+    const uint64_t b0 = __builtin_amdgcn_ballot_w64(mmt_keep(hk, 0, P.drop_thr));
+    const uint64_t b1 = __builtin_amdgcn_ballot_w64(mmt_keep(hk, 1, P.drop_thr));
+    const uint32_t w0 = (lane & 1) ? (uint32_t)(b0 >> 32) : (uint32_t)b0;
+    const uint32_t w1 = (lane & 1) ? (uint32_t)(b1 >> 32) : (uint32_t)b1;
+    out = ((lane >> 1) == e) ? w0 : ((lane >> 1) == e + 1) ? w1 : out;
+  }
+  if (lane < 32) P.dmask[j][tt * 32 + lane] = out;
+}
+
+hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStream_t s) {
+  if (b.count == 0 || B == 0 || T == 0) return hipSuccess;
+  int ns = 0;
+  for (int g = 0; g < b.count; ++g) {
+    const AttnProblem& P = b.p[g];
+    if (!P.drop_thr) continue;
+    if (P.nstreams < 1 || P.nstreams > MMT_MAX_STREAMS) return hipErrorInvalidValue;
+    for (int j = 0; j < P.nstreams; ++j)
+      if (!P.dmask[j]) return hipErrorInvalidValue;
+    ns = P.nstreams > ns ? P.nstreams : ns;
+  }
+  if (ns == 0) return hipSuccess;
+  const int64_t nt = (T + 31) / 32;
+  const int64_t waves = (int64_t)B * H * (nt * (nt + 1) / 2) * ns;
+  hipLaunchKernelGGL(attn_mask_kernel, dim3((unsigned)((waves + 3) / 4), 1, b.count), dim3(256), 0, s, b, B * H, T);
+  return hipGetLastError();
 }

@@ -62,6 +62,7 @@ struct PostM {
 struct ActLM {  // byte offsets of one (layer, modality)'s saved activations in the workspace
   size_t a, mean1, rstd1, h1, qkv, o, lse, p1, x1, c, mean2, rstd2, f, x2, x2h;
   size_t d, meanc, rstdc, qc, kv[MAXM], oc, ocj[MAXM], lsej[MAXM], pc, x3;
+  size_t dm, dmj[MAXM];  // attention dropout keep bits (SA; CA per KV stream), dropout > 0 only
 };
 
 struct Plan {
@@ -317,6 +318,7 @@ void make_plan(mmt_ctx* c, int B) {
   const size_t f4 = 4, b2 = 2;
   const int ldh1 = r8(3 * H * c->hh), ldp = r8(C / 2);
   const size_t bhT = (size_t)B * H * c->T;
+  const size_t mbytes = c->cfg.dropout > 0.f ? (size_t)mmt_attn_mask_dwords(B, H, c->T) * 4 : 0;
   p.pack = A((size_t)c->pack_elems * b2);
   p.act.resize((size_t)c->L * M);
   for (int i = 0; i < M; ++i) p.xemb[i] = A(R * C * f4);
@@ -330,12 +332,14 @@ void make_plan(mmt_ctx* c, int B) {
       a.c = A(R * C * b2); a.mean2 = A(R * f4); a.rstd2 = A(R * f4);
       a.f = A(R * 4 * C * b2); a.x2 = A(R * C * f4);
       a.x2h = c->any_cross ? A(R * C * b2) : 0;
+      a.dm = mbytes ? A(mbytes) : 0;
       if (x.cross) {
         a.d = A(R * C * b2); a.meanc = A(R * f4); a.rstdc = A(R * f4); a.qc = A(R * C * b2);
         for (int j = 0; j < M - 1; ++j) {
           a.kv[j] = A(R * 2 * C * b2);
           a.ocj[j] = A(R * C * b2);
           a.lsej[j] = A(bhT * f4);
+          a.dmj[j] = mbytes ? A(mbytes) : 0;
         }
         a.oc = A(R * C * b2); a.pc = A(R * ldp * b2); a.x3 = A(R * C * f4);
       }
@@ -499,6 +503,16 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   for (int l = 0; l < c->L && r.rc == MMT_OK; ++l) {
     const LM* x = &c->lm[(size_t)l * M];
     const ActLM* a = &p.act[(size_t)l * M];
+    // self-attention dropout keep bits of this layer: made on the side stream while LayerNorm and
+    // the Q/K/V GEMMs run, joined before the attention forward
+    if (r.drop) {
+      AttnBatch mb{}; mb.count = M;
+      for (int i = 0; i < M; ++i) {
+        r.set_drop(mb.p[i], l, i, DS_SA_PROB);
+        mb.p[i].nstreams = 1; mb.p[i].dmask[0] = r.W<uint32_t>(a[i].dm);
+      }
+      r.ok(mmt_launch_attn_mask(mb, B, T, H, r.side()), "attn_mask");
+    }
     LnBatch lb{}; lb.count = M;
     for (int i = 0; i < M; ++i) {
       lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].beta = r.P(x[i].ln1b);
@@ -523,10 +537,24 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       q.q = qkv + C; q.q_ld = 3 * C; q.k[0] = qkv; q.v[0] = qkv + 2 * C; q.kv_ld = 3 * C; q.kv_hstride = hs;
       q.o = r.W<bf16_t>(a[i].o); q.o_ld = C; q.lse[0] = r.W<float>(a[i].lse); q.nstreams = 1;
       r.set_drop(q, l, i, DS_SA_PROB);
+      if (r.drop) q.dmask[0] = r.W<uint32_t>(a[i].dm);
     }
+    if (r.drop) r.join();
     r.probe_begin("attn_fwd");
     r.ok(mmt_launch_attn_fwd(ab, B, T, H, hs, scale, r.s), "attn_fwd");
     r.probe_end("attn_fwd");
+    // cross-attention keep bits, overlapping the rest of the layer up to the CA forward
+    if (r.drop && c->any_cross) {
+      AttnBatch mc{}; mc.count = 0;
+      for (int i = 0; i < M; ++i) {
+        if (!x[i].cross) continue;
+        AttnProblem& q = mc.p[mc.count++];
+        r.set_drop(q, l, i, DS_CA_PROB);
+        q.nstreams = M - 1;
+        for (int j = 0; j < M - 1; ++j) q.dmask[j] = r.W<uint32_t>(a[i].dmj[j]);
+      }
+      r.ok(mmt_launch_attn_mask(mc, B, T, H, r.side()), "ca_attn_mask");
+    }
     for (int i = 0; i < M; ++i) {
       g.p[i] = gp_fwd(r.W<bf16_t>(a[i].o), C, wpk, x[i].P0, R);
       g.p[i].bias = r.P(x[i].bp0); g.p[i].o16 = r.W<bf16_t>(a[i].p1); g.p[i].ldo16 = ldp;
@@ -597,7 +625,10 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         }
         q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(a[i].oc); q.o_ld = C; q.nstreams = M - 1;
         r.set_drop(q, l, i, DS_CA_PROB);
+        if (r.drop)
+          for (int j = 0; j < M - 1; ++j) q.dmask[j] = r.W<uint32_t>(a[i].dmj[j]);
       }
+      if (r.drop) r.join();
       r.probe_begin("ca_attn_fwd");
       r.ok(mmt_launch_attn_fwd(cb, B, T, H, hs, scale, r.s), "ca_attn_fwd");
       r.probe_end("ca_attn_fwd");
@@ -780,6 +811,8 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dq = r.W<bf16_t>(p.gq[i]); q.dq_ld = C;
       q.dkv_ld = 2 * C; q.dkv_hstride = 2 * hs;
       r.set_drop(q, l, i, DS_CA_PROB);
+      if (r.drop)
+        for (int j = 0; j < M - 1; ++j) q.dmask[j] = r.W<uint32_t>(a[i].dmj[j]);
     }
     r.probe_begin("ca_attn_bwd");
     r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "ca_attn_bwd");
@@ -892,6 +925,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dvec[0] = r.W<float>(p.dvec[i][0]);
     q.dq = gq + C; q.dq_ld = 3 * C; q.dk[0] = gq; q.dv[0] = gq + 2 * C; q.dkv_ld = 3 * C; q.dkv_hstride = hs;
     r.set_drop(q, l, i, DS_SA_PROB);
+    if (r.drop) q.dmask[0] = r.W<uint32_t>(a[i].dm);
   }
   r.probe_begin("attn_bwd");
   r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "attn_bwd");
@@ -950,6 +984,27 @@ int ensure_device_tables(mmt_ctx* c) {
   HIPCHK(c, hipMemcpy(c->d_segs, c->segs.data(), sizeof(PackSeg) * c->segs.size(), hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_tasks, c->tasks.data(), sizeof(int) * c->tasks.size(), hipMemcpyHostToDevice));
   return MMT_OK;
+}
+
+// the side stream (weight-gradient GEMMs in the backward, dropout keep bits in the forward), made
+// lazily on the caller's current device; MMT_SIDE_STREAM=0 runs everything on the caller's stream
+void ensure_side(mmt_ctx* c) {
+  static const bool use_side = [] {
+    const char* e = getenv("MMT_SIDE_STREAM");
+    return !e || atoi(e) != 0;
+  }();
+  int dev = -1;
+  if (!use_side || hipGetDevice(&dev) != hipSuccess || (c->side && c->side_device == dev)) return;
+  if (c->side) (void)hipStreamDestroy(c->side);
+  c->side = nullptr;
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
+  c->side_device = dev;
+  while (c->side && c->evpool.size() < 64) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) break;
+    c->evpool.push_back(e);
+  }
+  if (c->evpool.empty() && c->side) { (void)hipStreamDestroy(c->side); c->side = nullptr; }
 }
 
 }  // namespace
@@ -1034,6 +1089,7 @@ int mmt_forward(mmt_ctx* c, void* stream, int32_t batch, const int64_t* const* i
     c->next_seed_set = false;
     ++c->step_counter;
   }
+  if (r.drop) ensure_side(c);
   c->fwd_drop = r.drop;
   c->fwd_seed = r.seed;
   c->fwd_ready = false;
@@ -1066,25 +1122,7 @@ int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* los
   if (!c) return MMT_ERR_INVALID;
   if (!c->fwd_ready) return fail(c, MMT_ERR_STATE, "mmt_backward: no forward with targets to differentiate");
   if (stage < 0 || stage > c->L + 1) return fail(c, MMT_ERR_INVALID, "bad backward stage");
-  {
-    static const bool use_side = [] {
-      const char* e = getenv("MMT_SIDE_STREAM");
-      return !e || atoi(e) != 0;
-    }();
-    int dev = -1;
-    if (use_side && hipGetDevice(&dev) == hipSuccess && (!c->side || c->side_device != dev)) {
-      if (c->side) (void)hipStreamDestroy(c->side);
-      c->side = nullptr;
-      if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
-      c->side_device = dev;
-      while (c->side && c->evpool.size() < 64) {
-        hipEvent_t e;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) break;
-        c->evpool.push_back(e);
-      }
-      if (c->evpool.empty() && c->side) { (void)hipStreamDestroy(c->side); c->side = nullptr; }
-    }
-  }
+  ensure_side(c);
   Runner r{c, (hipStream_t)stream, workspace, params, nullptr, c->plan.B, c->plan.B * c->T};
   r.drop = c->fwd_drop;
   r.seed = c->fwd_seed;

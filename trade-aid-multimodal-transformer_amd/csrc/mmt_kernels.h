@@ -115,10 +115,22 @@ struct AttnProblem {
   // bh*T + t, s >> 1) passes mmt_keep(., s, drop_thr); kept probabilities scaled by drop_scale
   uint32_t drop_key, drop_thr;
   float drop_scale;
+  // keep bits of that mask (required when drop_thr != 0), made by mmt_launch_attn_mask and read by
+  // the forward and both backward kernels: per stream, per (bh, query tile qt, key tile kt <= qt)
+  // 32 dwords at ((bh * ntri + qt*(qt+1)/2 + kt) * 32), ntri = nt*(nt+1)/2; dword 2e + u, bit r =
+  // keep(query qt*32 + r, key kt*32 + (e&3) + 8(e>>2) + 4u) — the accumulator order of an S^T tile
+  uint32_t* dmask[MMT_MAX_STREAMS];
 };
+// dwords of keep bits for one stream of one attention problem (see AttnProblem::dmask)
+inline int64_t mmt_attn_mask_dwords(int B, int H, int T) {
+  const int64_t nt = (T + 31) / 32;
+  return (int64_t)B * H * (nt * (nt + 1) / 2) * 32;
+}
 struct AttnBatch { AttnProblem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
 hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
+// fill dmask[j] (j < nstreams) of every problem with drop_thr != 0 from its counter hash
+hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStream_t s);
 
 // ------------------------------------------------------------------------------------------
 // Per-head Q/K/V stage 2: block-diagonal [hs/2 -> hs] maps (model.py:39,44,49), nblk = 3*H.
