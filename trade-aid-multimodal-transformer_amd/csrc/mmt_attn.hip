@@ -26,6 +26,8 @@
 // bit per element. 1/(1-p) is folded into the output normalisation / dV write-out.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "mmt_common.h"
 #include "mmt_kernels.h"
 
@@ -179,6 +181,7 @@ __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x)
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kTau = 8.0f;  // lazy-rescale threshold of the forward's running max (log2 units)
 
 // forward: one 32x32 (keys x queries) tile of S^T, online softmax, O^T += V^T P^T
 template <int HS, bool diag, bool DROP>
@@ -195,43 +198,48 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
     const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
     sacc = mfma32(kf, qf[s], sacc);
   }
+  // row max on the raw scores (c2 > 0 commutes with max), then into the log2 domain
   float tmax = -INFINITY;
   if (diag) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      const float sv = (key <= tq) ? sacc[e] * c2 : -INFINITY;
-      sacc[e] = sv;
-      tmax = fmaxf(tmax, sv);
+      if (key > tq) sacc[e] = -INFINITY;
+      tmax = fmaxf(tmax, sacc[e]);
     }
   } else {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      sacc[e] *= c2;
-      tmax = fmaxf(tmax, sacc[e]);
-    }
+    for (int e = 0; e < 16; ++e) tmax = fmaxf(tmax, sacc[e]);
   }
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-  const float mnew = fmaxf(m, tmax);  // finite: key 0 of tile 0 is valid for every query
-  const float alpha = ex2(m - mnew);
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
+  // lazy rescale: the running max m moves only when a tile's max exceeds it by more than kTau
+  // (log2 units; always on the first tile, m = -inf). Until then exp2(s - m) <= 2^kTau keeps P, l
+  // and O comfortably in fp32/bf16 range, and the O accumulators (AGPRs at hs = 64: a read,
+  // multiply and write back per element) are not touched on the common path. l and O share m,
+  // so the normalised output and the LSE m + log2(l) are unchanged.
+  const bool up = tmax > m + kTau;
+  if (__builtin_amdgcn_ballot_w64(up)) {  // wave-uniform
+    const float alpha = up ? ex2(m - tmax) : 1.f;
+    m = up ? tmax : m;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
+  }
   float rs = 0.f;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const float pv = ex2(sacc[e] - mnew);
+    const float pv = ex2(fmaf(sacc[e], c2, -m));
     sacc[e] = pv;
     rs += pv;
   }
   rs += __shfl_xor(rs, 32, 64);
-  l = l * alpha + rs;
-  m = mnew;
+  l += rs;
   if (DROP) {  // dropout on the probabilities (the normaliser l keeps every term; 1/(1-p) at the end)
 #pragma unroll
     for (int e = 0; e < 16; ++e) sacc[e] = keep_st(mv, e) ? sacc[e] : 0.f;
   }
-#pragma unroll
-  for (int dt = 0; dt < G::ND; ++dt)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const bf16x8 pf = acc_frag(sacc, s);
@@ -286,15 +294,12 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBat
   const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
   const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
   bf16x8 qfa[G::NKS], qfb[G::NKS];
-  f32x16 ota[G::ND], otb[G::ND];
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
     const int d0 = 16 * s + 8 * h;
     qfa[s] = ld8(P.q + (rowbase + tqa) * P.q_ld + head * HS + d0, la && tqa < T && d0 < HS);
     qfb[s] = ld8(P.q + (rowbase + tqb) * P.q_ld + head * HS + d0, lb && tqb < T && d0 < HS);
   }
-#pragma unroll
-  for (int dt = 0; dt < G::ND; ++dt) { zero16(ota[dt]); zero16(otb[dt]); }
   for (int j = 0; j < P.nstreams; ++j) {
     float ma = -INFINITY, lsa = 0.f, mb = -INFINITY, lsb = 0.f;
     f32x16 oa[G::ND], ob[G::ND];
@@ -339,52 +344,52 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBat
         __syncthreads();
       }
     }
-    // normalise this stream's outputs, keep its LSE (and its own output when several are summed)
+    // normalise this stream's outputs and keep its LSE. One stream: the output itself; several:
+    // each stream's own output (the backward reads it), summed below
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const bool live = u == 0 ? la : lb;
       const int tq = u == 0 ? tqa : tqb;
       f32x16* o = u == 0 ? oa : ob;
-      f32x16* ot = u == 0 ? ota : otb;
       const float m = u == 0 ? ma : mb, l = u == 0 ? lsa : lsb;
       const float inv = (l > 0.f) ? (DROP ? P.drop_scale : 1.f) / l : 0.f;
-#pragma unroll
-      for (int dt = 0; dt < G::ND; ++dt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          o[dt][e] *= inv;
-          ot[dt][e] += o[dt][e];
-        }
       if (live && tq < T) {
         if (h == 0) P.lse[j][(int64_t)bh * T + tq] = (m + __log2f(l)) * kLn2;
-        if (P.nstreams > 1 && P.oj[j]) {
+        bf16_t* dst = (P.nstreams > 1 ? P.oj[j] : P.o) + (rowbase + tq) * P.o_ld + head * HS;
 #pragma unroll
-          for (int dt = 0; dt < G::ND; ++dt)
+        for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const int d0 = dt * 32 + 8 * g + 4 * h;
-              if (d0 < HS)
-                *reinterpret_cast<u32x2*>(P.oj[j] + (rowbase + tq) * P.o_ld + head * HS + d0) =
-                    u32x2{pack2bf(o[dt][4 * g], o[dt][4 * g + 1]), pack2bf(o[dt][4 * g + 2], o[dt][4 * g + 3])};
-            }
-        }
+          for (int g = 0; g < 4; ++g) {
+            const int d0 = dt * 32 + 8 * g + 4 * h;
+            if (d0 < HS)
+              *reinterpret_cast<u32x2*>(dst + d0) = u32x2{pack2bf(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv),
+                                                          pack2bf(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv)};
+          }
       }
     }
   }
+  // several streams: the output is the sum of the per-stream outputs this lane just wrote (kept
+  // out of registers: a running fp32 total would pin another O-sized accumulator set)
+  if (P.nstreams > 1) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const bool live = u == 0 ? la : lb;
-    const int tq = u == 0 ? tqa : tqb;
-    const f32x16* ot = u == 0 ? ota : otb;
-    if (live && tq < T) {
+    for (int u = 0; u < 2; ++u) {
+      const bool live = u == 0 ? la : lb;
+      const int tq = u == 0 ? tqa : tqb;
+      if (!(live && tq < T)) continue;
+      const int64_t off = (rowbase + tq) * P.o_ld + head * HS;
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int d0 = dt * 32 + 8 * g + 4 * h;
-          if (d0 < HS)
-            *reinterpret_cast<u32x2*>(P.o + (rowbase + tq) * P.o_ld + head * HS + d0) =
-                u32x2{pack2bf(ot[dt][4 * g], ot[dt][4 * g + 1]), pack2bf(ot[dt][4 * g + 2], ot[dt][4 * g + 3])};
+          if (d0 >= HS) continue;
+          float t[4] = {0.f, 0.f, 0.f, 0.f};
+          for (int jj = 0; jj < P.nstreams; ++jj) {
+            const u32x2 v = *reinterpret_cast<const u32x2*>(P.oj[jj] + off + d0);
+            t[0] += bf2f(v[0] & 0xffff); t[1] += bf2f(v[0] >> 16);
+            t[2] += bf2f(v[1] & 0xffff); t[3] += bf2f(v[1] >> 16);
+          }
+          *reinterpret_cast<u32x2*>(P.o + off + d0) = u32x2{pack2bf(t[0], t[1]), pack2bf(t[2], t[3])};
         }
     }
   }
@@ -572,7 +577,7 @@ __global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_bwd_dq_kernel(Attn
 #define MMT_DKDV_MINB 1
 #endif
 // dK, dV: one 32x32 (queries x keys) tile; S, dP recomputed, dV += P^T dO, dK += dS^T Q
-template <int HS, bool masked, bool DROP>
+template <int HS, bool MASKED, bool DROP>
 __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, const float* lsl, const float* dsl,
                                           int ql, int q0, int tk, int T,
                                           const bf16x8 (&kf)[Geo<HS>::NKS], const bf16x8 (&vf)[Geo<HS>::NKS],
@@ -600,14 +605,12 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
     for (int e4 = 0; e4 < 4; ++e4) {
       const int e = 4 * g + e4;
       const int tq = q0 + 8 * g + 4 * h + e4;
-      float pv = ex2(sacc[e] * c2 - l4[e4]);
-      if (masked && !(tk <= tq && tq < T)) pv = 0.f;
+      float pv = ex2(fmaf(sacc[e], c2, -l4[e4]));
+      if (MASKED && !(tk <= tq && tq < T)) pv = 0.f;
       if (DROP) {  // pm = Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
         const int km = (int)(mw << (31 - (8 * g + e4))) >> 31;  // all ones iff kept
-        const float nd = -d4[e4];
-        const float t = fmaf(dpacc[e], P.drop_scale, nd);
         pm[e] = __int_as_float(__float_as_int(pv) & km);
-        sacc[e] = pv * __int_as_float((__float_as_int(t) & km) | (__float_as_int(nd) & ~km));
+        sacc[e] = pv * fmaf(__int_as_float(__float_as_int(dpacc[e]) & km), P.drop_scale, -d4[e4]);
       } else {
         pm[e] = pv;
         sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
@@ -652,6 +655,7 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
   const int q_lo = kt0 * 32;
   const int nch = (T - q_lo + ROWS - 1) / ROWS;
   const bool ragged = (T & 31) != 0;
+  const int qlast = ragged ? nt - 1 : nt;  // the ragged last query tile (masked); nt: none
   const int64_t rowbase = (int64_t)b * T;
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
@@ -716,35 +720,36 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
   for (int c = 0; c < nch; ++c) {
     const int r0 = q_lo + c * ROWS;
     const int qt_lo = r0 / 32, qt_hi = min(qt_lo + ROWS / 32, nt) - 1;
-    if (la) {
-      // queries in [ka, kb): tile a only (qt == ka its diagonal)
+    // per key tile, the diagonal query tile and a ragged last one take the masked variant, peeled
+    // off the plain loop: every accumulator set sees one straight chain of call sites (inlined
+    // variants merging inside a loop made the register allocator copy the dK/dV accumulators
+    // between AGPR sets every iteration)
+    auto tile_a = [&](auto mc, int qt) {
+      dkdv_tile<HS, decltype(mc)::value, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka,
+                                               dva, c2, P, mska + (qt - qt_lo) * 32, lane);
+    };
+    auto tile_b = [&](auto mc, int qt) {
+      dkdv_tile<HS, decltype(mc)::value, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tkb, T, kfb, vfb, dkb,
+                                               dvb, c2, P, mskb + (qt - qt_lo) * 32, lane);
+    };
+    const std::true_type msk_on;
+    const std::false_type msk_off;
+    if (la) {  // queries in [ka, kb): tile a only
       const int s_hi = lb ? min(kb - 1, qt_hi) : qt_hi;
+      int qt = max(ka, qt_lo);
+      if (qt == ka && qt <= s_hi) tile_a(msk_on, qt++);
+      const int qe = min(s_hi, qlast - 1);
 #pragma unroll 1
-      for (int qt = max(ka, qt_lo); qt <= s_hi; ++qt) {
-        if (qt == ka || (ragged && qt == nt - 1))
-          dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
-                                    mska + (qt - qt_lo) * 32, lane);
-        else
-          dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
-                                     mska + (qt - qt_lo) * 32, lane);
-      }
+      for (; qt <= qe; ++qt) tile_a(msk_off, qt);
+      if (qt <= s_hi) tile_a(msk_on, qt);  // qt == qlast
     }
-    if (lb) {
-      // queries >= kb: both tiles (qt == kb is b's diagonal)
+    if (lb) {  // queries >= kb: both tiles
+      int qt = max(kb, qt_lo);
+      if (qt == kb && qt <= qt_hi) { tile_a(msk_on, qt); tile_b(msk_on, qt++); }
+      const int qe = min(qt_hi, qlast - 1);
 #pragma unroll 1
-      for (int qt = max(kb, qt_lo); qt <= qt_hi; ++qt) {
-        if (qt == kb || (ragged && qt == nt - 1)) {
-          dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
-                                    mska + (qt - qt_lo) * 32, lane);
-          dkdv_tile<HS, true, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tkb, T, kfb, vfb, dkb, dvb, c2, P,
-                                    mskb + (qt - qt_lo) * 32, lane);
-        } else {
-          dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka, dva, c2, P,
-                                     mska + (qt - qt_lo) * 32, lane);
-          dkdv_tile<HS, false, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tkb, T, kfb, vfb, dkb, dvb, c2, P,
-                                     mskb + (qt - qt_lo) * 32, lane);
-        }
-      }
+      for (; qt <= qe; ++qt) { tile_a(msk_off, qt); tile_b(msk_off, qt); }
+      if (qt <= qt_hi) { tile_a(msk_on, qt); tile_b(msk_on, qt); }
     }
     if (c + 1 < nch) {
       __syncthreads();
@@ -791,62 +796,6 @@ struct ChunkWalk {
   }
 };
 
-// (one key tile at a time: the variant with two waves per SIMD at hs <= 32)
-// dK, dV: one 32x32 (queries x keys) tile; S, dP recomputed, dV += P^T dO, dK += dS^T Q
-template <int HS, bool DROP>
-__device__ __forceinline__ void dkdv1_tile(const bf16_t* qs, const bf16_t* dos, const float* lsl, const float* dsl,
-                                          int ql, int q0, int tk, bool masked, int T,
-                                          const bf16x8 (&kf)[Geo<HS>::NKS], const bf16x8 (&vf)[Geo<HS>::NKS],
-                                          f32x16 (&dk)[Geo<HS>::ND], f32x16 (&dv)[Geo<HS>::ND], float c2,
-                                          const AttnProblem& P, const uint32_t* mt, int lane) {
-  using G = Geo<HS>;
-  const int r = lane & 31, h = lane >> 5;
-  // key r's keep bits over the tile's queries, this lane's half (queries 8g + 4h + e4) at bits 8g + e4
-  const uint32_t mw = DROP ? mt[key_dword(r)] >> (4 * h) : 0u;
-  f32x16 sacc, dpacc, pm;
-  zero16(sacc);
-  zero16(dpacc);
-#pragma unroll
-  for (int s = 0; s < G::NKS; ++s) {
-    const bf16x8 qa = *reinterpret_cast<const bf16x8*>(qs + (ql + r) * G::RW + 16 * s + 8 * h);
-    const bf16x8 da = *reinterpret_cast<const bf16x8*>(dos + (ql + r) * G::RW + 16 * s + 8 * h);
-    sacc = mfma32(qa, kf[s], sacc);    // S[q][key]
-    dpacc = mfma32(da, vf[s], dpacc);  // dP[q][key]
-  }
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsl + ql + 8 * g + 4 * h);
-    const f32x4 d4 = *reinterpret_cast<const f32x4*>(dsl + ql + 8 * g + 4 * h);
-#pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
-      const int e = 4 * g + e4;
-      const int tq = q0 + 8 * g + 4 * h + e4;
-      float pv = ex2(sacc[e] * c2 - l4[e4]);
-      if (masked && !(tk <= tq && tq < T)) pv = 0.f;
-      if (DROP) {  // pm = Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
-        const int km = (int)(mw << (31 - (8 * g + e4))) >> 31;  // all ones iff kept
-        const float nd = -d4[e4];
-        const float t = fmaf(dpacc[e], P.drop_scale, nd);
-        pm[e] = __int_as_float(__float_as_int(pv) & km);
-        sacc[e] = pv * __int_as_float((__float_as_int(t) & km) | (__float_as_int(nd) & ~km));
-      } else {
-        pm[e] = pv;
-        sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
-      }
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const bf16x8 pf = acc_frag(pm, s);
-    const bf16x8 df = acc_frag(sacc, s);
-#pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt) {
-      dv[dt] = mfma32(pf, tr_frag(dos + ql * G::RW, G::RW, dt, s, lane), dv[dt]);
-      dk[dt] = mfma32(df, tr_frag(qs + ql * G::RW, G::RW, dt, s, lane), dk[dt]);
-    }
-  }
-}
-
 // =============================================================================================
 // backward dK, dV: grid (ceil(nt/8), B*H*nstreams, G); wave w owns key tiles 8*bx + w, 8*bx + 7 - w
 // =============================================================================================
@@ -870,6 +819,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, in
   const int q_lo = kt0 * 32;
   const ChunkWalk walk{1, (T - q_lo + ROWS - 1) / ROWS};
   const bool ragged = (T & 31) != 0;
+  const int qlast = ragged ? nt - 1 : nt;  // the ragged last query tile (masked); nt: none
   const int64_t rowbase = (int64_t)b * T;
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
@@ -935,10 +885,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, in
       const int r0 = q_lo + c * ROWS;
       if (live) {
         const int qt_lo = r0 / 32, qt_hi = min(qt_lo + ROWS / 32, nt) - 1;
-        #pragma unroll 1
-        for (int qt = max(kt, qt_lo); qt <= qt_hi; ++qt)
-          dkdv1_tile<HS, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tk, qt == kt || (ragged && qt == nt - 1),
-                               T, kf, vf, dk, dv, c2, P, msk + ((kt - kt0) * MS::KT + (qt - qt_lo)) * 32, lane);
+        const uint32_t* mk = msk + (kt - kt0) * MS::KT * 32;
+        auto tile = [&](auto mc, int qt) {
+          dkdv_tile<HS, decltype(mc)::value, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tk, T, kf, vf, dk, dv,
+                                                   c2, P, mk + (qt - qt_lo) * 32, lane);
+        };
+        int qt = max(kt, qt_lo);  // diagonal and ragged last tile masked, peeled (see the paired kernel)
+        if (qt == kt && qt <= qt_hi) tile(std::true_type{}, qt++);
+        const int qe = min(qt_hi, qlast - 1);
+#pragma unroll 1
+        for (; qt <= qe; ++qt) tile(std::false_type{}, qt);
+        if (qt <= qt_hi) tile(std::true_type{}, qt);
       }
       if (reload) {
         __syncthreads();
@@ -1010,6 +967,8 @@ static hipError_t attn_dispatch(const AttnBatch& b, int B, int T, int H, int hs,
   if (b.count == 0 || B == 0 || T == 0) return hipSuccess;
   for (int g = 0; g < b.count; ++g) {
     if (b.p[g].nstreams < 1 || b.p[g].nstreams > MMT_MAX_STREAMS) return hipErrorInvalidValue;
+    for (int j = 0; j < b.p[g].nstreams && b.p[g].nstreams > 1; ++j)  // per-stream outputs (summed, and
+      if (!b.p[g].oj[j]) return hipErrorInvalidValue;                   // read by the backward)
     if (b.p[g].drop_thr)  // dropout reads the keep bits of mmt_launch_attn_mask
       for (int j = 0; j < b.p[g].nstreams; ++j)
         if (!b.p[g].dmask[j]) return hipErrorInvalidValue;
