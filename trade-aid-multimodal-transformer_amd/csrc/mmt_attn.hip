@@ -183,6 +183,20 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr float kTau = 8.0f;  // lazy-rescale threshold of the forward's running max (log2 units)
 
+// waves per SIMD the forward / dQ kernels are compiled for (hs <= 32 fits two at no spill; at hs
+// = 64 the forward fits two without AGPRs; the dQ pass spills ~25 VGPRs there and is still faster)
+#ifndef MMT_FWD_MINB
+#define MMT_FWD_MINB(hs) 2
+#endif
+#ifndef MMT_DQ_MINB
+#define MMT_DQ_MINB(hs) 2
+#endif
+// single-tile dK/dV: at hs <= 32 the default bound (the compiler keeps the accumulators in AGPRs
+// and still reaches 2 waves) measured faster than forcing 2; at hs = 64 forcing 2 fits without AGPRs
+#ifndef MMT_DKDV1_MINB
+#define MMT_DKDV1_MINB(hs) ((hs) <= 32 ? 1 : 2)
+#endif
+
 // forward: one 32x32 (keys x queries) tile of S^T, online softmax, O^T += V^T P^T
 template <int HS, bool diag, bool DROP>
 __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq,
@@ -256,7 +270,7 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
 // (stream, chunk) is loaded once per block.
 // =============================================================================================
 template <int HS, bool DROP>
-__global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
+__global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
@@ -435,7 +449,7 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
 // forward each wave walks its two query tiles together
 // =============================================================================================
 template <int HS, bool DROP>
-__global__ __launch_bounds__(256, HS <= 32 ? 2 : 1) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H,
+__global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H,
                                                                                        float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
@@ -800,7 +814,7 @@ struct ChunkWalk {
 // backward dK, dV: grid (ceil(nt/8), B*H*nstreams, G); wave w owns key tiles 8*bx + w, 8*bx + 7 - w
 // =============================================================================================
 template <int HS, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv1_kernel(AttnBatch batch, int T, int H, float scale) {
+__global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
   constexpr int ROWS = Chunk<HS>::ROWS;
   const AttnProblem& P = batch.p[blockIdx.z];
@@ -940,13 +954,14 @@ static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, b
     for (int g = 0; g < bt.count; ++g) drop = drop || bt.p[g].drop_thr != 0;
     if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, true>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, false>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
-    // dK/dV: the paired walk needs 4 accumulator sets; at hs <= 32 the single-tile kernel keeps 2
-    // waves per SIMD and measured faster (C1: 103 vs 127 us), at hs = 64 the paired one
+    // dK/dV: the paired walk needs 4 accumulator sets (1 wave per SIMD); the single-tile kernel
+    // keeps 2 waves per SIMD and measured faster at hs = 32 (C1: 103 vs 127 us) and, once it fits
+    // hs = 64 without AGPRs, there too (target step 25.9 -> 25.4 ms). MMT_DKDV_PAIR=1 forces the pair
     static const int pair = [] {
       const char* e = getenv("MMT_DKDV_PAIR");
       return e ? atoi(e) : -1;
     }();
-    const bool paired = pair < 0 ? HS > 32 : pair != 0;
+    const bool paired = pair > 0;
     if (!paired && drop)
       hipLaunchKernelGGL((attn_bwd_dkdv1_kernel<HS, true>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H,
                          scale);

@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime first; see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmmt_hip.so")
+# MMT_LIB_PATH: an experimental build of the same library (tools/build_variant.py); default in-tree
+LIB_PATH = os.environ.get("MMT_LIB_PATH") or os.path.join(HERE, "libmmt_hip.so")
 MAX_MOD = 8
 
 c_i32 = ctypes.c_int32
