@@ -168,6 +168,47 @@ def test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p):
     assert rel(allg, alln) > 3 * max(rel(allg, allr), 1e-2)  # the masks act
 
 
+@pytest.mark.parametrize("name", ["f_small", "f_hs32"])
+def test_short_sequence_inference_matches_oracle(name):
+    """T < block_size without targets (inference; generate's early steps): the right-padded run's
+    logits at the real positions against the oracle run at that length (model.py:380-402)."""
+    import mmt_oracle as O
+    z, meta, cfg, sd, idx, tgt = model_fixture(name)
+    m = build(meta, sd)
+    m.eval()
+    Ts = meta["block_size"] // 2 + 3
+    short = [t[:, :Ts] for t in idx]
+    with torch.no_grad():
+        lg, none = m([t.cuda() for t in short])
+    assert none is None
+    ref, _ = O.forward(sd, cfg, short)
+    for i in range(cfg.M):
+        assert tuple(lg[i].shape) == tuple(ref[i].shape)
+        assert rel(lg[i], ref[i]) < 2e-2, i
+    with pytest.raises(NotImplementedError):
+        m([t.cuda() for t in short], [t[:, :Ts].cuda() for t in tgt])
+
+
+def test_generate_appends_crops_and_aligns():
+    """generate (model.py:404-446): samples appended to the target modality past block_size (the
+    context is cropped), the other modalities padded with their last token, prefixes unchanged."""
+    z, meta, cfg, sd, idx, tgt = model_fixture("f_small")
+    m = build(meta, sd)
+    m.eval()
+    torch.manual_seed(0)
+    start = [t[:, :10].cuda() for t in idx]
+    n_new = meta["block_size"] + 8 - 10
+    out = m.generate(start, max_new_tokens=n_new, modality_to_generate=1)
+    B = start[0].shape[0]
+    for i, o in enumerate(out):
+        assert tuple(o.shape) == (B, meta["block_size"] + 8), i
+        assert torch.equal(o[:, :10], start[i]), i
+    g = out[1][:, 10:]
+    assert int(g.min()) >= 0 and int(g.max()) < meta["V"][1]
+    for i in (0, 2, 3):
+        assert torch.equal(out[i][:, 10:], start[i][:, -1:].expand(B, n_new)), i
+
+
 def _grad_views(m):
     g = m.flat_params.grad
     for name, off, shp, _ in m._tensors:

@@ -189,6 +189,189 @@ __device__ __forceinline__ void wait_vm(int n) {
   }
 }
 
+// Fused epilogue of a SWAP tile (acc[i][j]: rows = n sub-tile i, cols = m sub-tile j), staged through
+// LDS at `ct` in passes of EPI_ROWS rows, then run row-major: a thread owns 8 consecutive columns,
+// so every global access is 16 B per lane (bf16 x 8, or 2 x f32x4) and GBN/8 lanes cover one row
+// segment. 16-B stores halve the store instructions of the 8-B form (the epilogue of a short-K tile
+// is store-issue bound). Starts with a barrier (the caller's LDS reads of `ct` must be done).
+template <class TL, int EPI, int EPI_ROWS>
+__device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc)[TL::TN][TL::TM], char* lds,
+                                              float* o32, float alpha, int m0, int n0, int tid, int lane, int wave) {
+  constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
+  const int M = P.M, N = P.N;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int h = lane >> 5, r = lane & 31;
+  // Stage the fp32 tile through LDS (EPI_ROWS rows per pass), then run the epilogue row-major:
+  // a thread owns 8 consecutive columns, so every global access is 16 B per lane (bf16 x 8, or
+  // 2 x f32x4) and GBN/8 lanes cover one row segment. 16-B stores halve the store instructions
+  // of the 8-B form (the epilogue of a short-K tile is store-issue bound).
+  // acc[i][j]: rows = n (sub-tile i), cols = m (sub-tile j)
+  constexpr int CT = GBN + 4;  // fp32 row stride of the staged tile (16-B aligned, de-conflicted)
+  constexpr int TPR = GBN / 8;          // threads per row
+  constexpr int RPI = NT / TPR;         // rows per iteration
+  constexpr int IT = EPI_ROWS / RPI;    // iterations per pass
+  float* ct = reinterpret_cast<float*>(lds);
+  const int c8 = tid % TPR;   // 8-column group of this thread
+  const int rsub = tid / TPR; // row within an iteration
+  const int n = n0 + 8 * c8;
+  constexpr bool HAS_AUX = EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
+  constexpr bool HAS_RES = EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32;
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
+                            EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16;
+  // fused bias gradient (bf16-output epilogues): column sums of the stored values
+  constexpr bool CAN_DB = EPI == EPI_STORE_BF16 || EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
+  const bool want_db = CAN_DB && P.dbias != nullptr;
+  // 16-B vector accesses need bf16 leading dimensions % 8 and fp32 ones % 4 (bias pointers are
+  // 64-B aligned by the parameter layout)
+  const bool vec_ok = ((P.ldo16 | P.ldaux) & 7) == 0 && ((P.ldc | P.ldres) & 3) == 0;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x4 bias0 = {0.f, 0.f, 0.f, 0.f}, bias1 = {0.f, 0.f, 0.f, 0.f};
+  if (HAS_BIAS && P.bias && n + 8 <= N) {
+    bias0 = *reinterpret_cast<const f32x4*>(P.bias + n);
+    bias1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll 1
+  for (int pass = 0; pass < GBM / EPI_ROWS; ++pass) {
+    __syncthreads();  // stage-ring / previous pass reads done
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int mf = wm * TM * 32 + 32 * j;  // first row of this sub-tile in the block tile
+        if (mf / EPI_ROWS != pass) continue;
+        const int ml = mf - pass * EPI_ROWS + r;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int nl = wn * TN * 32 + 32 * i + 8 * g + 4 * h;
+          *reinterpret_cast<f32x4*>(ct + ml * CT + nl) =
+              f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        }
+      }
+    __syncthreads();
+    const int mb = m0 + pass * EPI_ROWS;
+    if (n + 8 <= N && vec_ok) {
+      // issue every operand load of this thread's rows first (memory-level parallelism)
+      u32x4 auxv[IT];
+      f32x4 resv[IT][2];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int m = mb + it * RPI + rsub;
+        if (m < M) {
+          if (HAS_AUX) auxv[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
+          const float* rp = EPI == EPI_BIAS_RESID_F32 ? P.resid + (int64_t)m * P.ldres + n
+                                                      : o32 + (int64_t)m * P.ldc + n;
+          if (HAS_RES) {
+            resv[it][0] = *reinterpret_cast<const f32x4*>(rp);
+            resv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+          }
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int ml = it * RPI + rsub;
+        const int m = mb + ml;
+        if (m >= M) continue;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8 + 4);
+        float r[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r[e] = alpha * v0[e] + bias0[e];
+          r[e + 4] = alpha * v1[e] + bias1[e];
+        }
+        if (EPI == EPI_BIAS_TANH_BF16) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) r[e] = fast_tanh(r[e]);
+        }
+        if (EPI == EPI_BIAS_RELU_BF16) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.0f);
+        }
+        if (HAS_AUX) {
+          const u32x4 a = auxv[it];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float t0 = bf2f(a[q] & 0xffff), t1 = bf2f(a[q] >> 16);
+            if (EPI == EPI_DTANH_BF16) {
+              r[2 * q] *= (1.0f - t0 * t0);
+              r[2 * q + 1] *= (1.0f - t1 * t1);
+            } else {
+              r[2 * q] = t0 > 0.0f ? r[2 * q] : 0.0f;
+              r[2 * q + 1] = t1 > 0.0f ? r[2 * q + 1] : 0.0f;
+            }
+          }
+        }
+        if (EPI == EPI_BIAS_RESID_F32 && P.drop_thr) {  // dropout on the branch output, then residual add
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // n is even: one hash per column pair
+            const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n >> 1) + q);
+            r[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? r[2 * q] * P.drop_scale : 0.0f;
+            r[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? r[2 * q + 1] * P.drop_scale : 0.0f;
+          }
+        }
+        if (HAS_RES) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            r[e] += resv[it][0][e];
+            r[e + 4] += resv[it][1][e];
+          }
+        }
+        if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32 || EPI == EPI_ACC_F32) {
+          float* op = o32 + (int64_t)m * P.ldc + n;
+          *reinterpret_cast<f32x4*>(op) = f32x4{r[0], r[1], r[2], r[3]};
+          *reinterpret_cast<f32x4*>(op + 4) = f32x4{r[4], r[5], r[6], r[7]};
+          if (EPI == EPI_BIAS_RESID_F32 && P.o16)
+            *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+                u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+        } else {
+          *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+              u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+          if (CAN_DB) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[e] += r[e];
+          }
+        }
+      }
+    } else if (n < N) {
+      // edge columns (and unaligned leading dimensions): scalar epilogue + zero pad columns
+      for (int it = 0; it < IT; ++it) {
+        const int ml = it * RPI + rsub;
+        const int m = mb + ml;
+        if (m >= M) continue;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = ct[ml * CT + 8 * c8 + e];
+          if (n + e < N) cs[e] += epi_scalar<EPI>(P, o32, alpha, m, n + e, v);
+          else epi_pad<EPI>(P, m, n + e);
+        }
+      }
+    }
+  }
+  if (want_db) {
+    // rows of a column group live in lanes l, l^TPR, ... of every wave: fold those, then the
+    // waves via LDS (the staged tile is dead: every thread has read its own rows), one atomic
+    // per column
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = TPR; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
+    __syncthreads();
+    float* red = ct;  // [NW waves][GBN columns]
+    if (lane < TPR) {
+      *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8 + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+    }
+    __syncthreads();
+    if (tid < GBN && n0 + tid < N) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sum += red[w * GBN + tid];
+      atomicAdd(P.dbias + n0 + tid, sum);
+    }
+  }
+}
+
 template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
 __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
   constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
@@ -303,176 +486,8 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
   // split-K into slabs: split s of the K loop writes its own fp32 slab (reduced by mmt_gemm_slab_reduce)
   float* o32 = P.o32 + (P.split_stride ? (int64_t)blockIdx.y * P.split_stride : (int64_t)0);
   const int h = lane >> 5, r = lane & 31;
-  if (SWAP) {
-    // Stage the fp32 tile through LDS (EPI_ROWS rows per pass), then run the epilogue row-major:
-    // a thread owns 8 consecutive columns, so every global access is 16 B per lane (bf16 x 8, or
-    // 2 x f32x4) and GBN/8 lanes cover one row segment. 16-B stores halve the store instructions
-    // of the 8-B form (the epilogue of a short-K tile is store-issue bound).
-    // acc[i][j]: rows = n (sub-tile i), cols = m (sub-tile j)
-    constexpr int CT = GBN + 4;  // fp32 row stride of the staged tile (16-B aligned, de-conflicted)
-    constexpr int TPR = GBN / 8;          // threads per row
-    constexpr int RPI = NT / TPR;         // rows per iteration
-    constexpr int IT = EPI_ROWS / RPI;    // iterations per pass
-    float* ct = reinterpret_cast<float*>(lds);
-    const int c8 = tid % TPR;   // 8-column group of this thread
-    const int rsub = tid / TPR; // row within an iteration
-    const int n = n0 + 8 * c8;
-    constexpr bool HAS_AUX = EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
-    constexpr bool HAS_RES = EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32;
-    constexpr bool HAS_BIAS = EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
-                              EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16;
-    // fused bias gradient (bf16-output epilogues): column sums of the stored values
-    constexpr bool CAN_DB = EPI == EPI_STORE_BF16 || EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
-    const bool want_db = CAN_DB && P.dbias != nullptr;
-    // 16-B vector accesses need bf16 leading dimensions % 8 and fp32 ones % 4 (bias pointers are
-    // 64-B aligned by the parameter layout)
-    const bool vec_ok = ((P.ldo16 | P.ldaux) & 7) == 0 && ((P.ldc | P.ldres) & 3) == 0;
-    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    f32x4 bias0 = {0.f, 0.f, 0.f, 0.f}, bias1 = {0.f, 0.f, 0.f, 0.f};
-    if (HAS_BIAS && P.bias && n + 8 <= N) {
-      bias0 = *reinterpret_cast<const f32x4*>(P.bias + n);
-      bias1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll 1
-    for (int pass = 0; pass < GBM / EPI_ROWS; ++pass) {
-      __syncthreads();  // stage-ring / previous pass reads done
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) {
-          const int mf = wm * TM * 32 + 32 * j;  // first row of this sub-tile in the block tile
-          if (mf / EPI_ROWS != pass) continue;
-          const int ml = mf - pass * EPI_ROWS + r;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int nl = wn * TN * 32 + 32 * i + 8 * g + 4 * h;
-            *reinterpret_cast<f32x4*>(ct + ml * CT + nl) =
-                f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-          }
-        }
-      __syncthreads();
-      const int mb = m0 + pass * EPI_ROWS;
-      if (n + 8 <= N && vec_ok) {
-        // issue every operand load of this thread's rows first (memory-level parallelism)
-        u32x4 auxv[IT];
-        f32x4 resv[IT][2];
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-          const int m = mb + it * RPI + rsub;
-          if (m < M) {
-            if (HAS_AUX) auxv[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
-            const float* rp = EPI == EPI_BIAS_RESID_F32 ? P.resid + (int64_t)m * P.ldres + n
-                                                        : o32 + (int64_t)m * P.ldc + n;
-            if (HAS_RES) {
-              resv[it][0] = *reinterpret_cast<const f32x4*>(rp);
-              resv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
-            }
-          }
-        }
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-          const int ml = it * RPI + rsub;
-          const int m = mb + ml;
-          if (m >= M) continue;
-          const f32x4 v0 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8);
-          const f32x4 v1 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8 + 4);
-          float r[8];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            r[e] = alpha * v0[e] + bias0[e];
-            r[e + 4] = alpha * v1[e] + bias1[e];
-          }
-          if (EPI == EPI_BIAS_TANH_BF16) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) r[e] = fast_tanh(r[e]);
-          }
-          if (EPI == EPI_BIAS_RELU_BF16) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.0f);
-          }
-          if (HAS_AUX) {
-            const u32x4 a = auxv[it];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float t0 = bf2f(a[q] & 0xffff), t1 = bf2f(a[q] >> 16);
-              if (EPI == EPI_DTANH_BF16) {
-                r[2 * q] *= (1.0f - t0 * t0);
-                r[2 * q + 1] *= (1.0f - t1 * t1);
-              } else {
-                r[2 * q] = t0 > 0.0f ? r[2 * q] : 0.0f;
-                r[2 * q + 1] = t1 > 0.0f ? r[2 * q + 1] : 0.0f;
-              }
-            }
-          }
-          if (EPI == EPI_BIAS_RESID_F32 && P.drop_thr) {  // dropout on the branch output, then residual add
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {  // n is even: one hash per column pair
-              const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n >> 1) + q);
-              r[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? r[2 * q] * P.drop_scale : 0.0f;
-              r[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? r[2 * q + 1] * P.drop_scale : 0.0f;
-            }
-          }
-          if (HAS_RES) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              r[e] += resv[it][0][e];
-              r[e + 4] += resv[it][1][e];
-            }
-          }
-          if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32 || EPI == EPI_ACC_F32) {
-            float* op = o32 + (int64_t)m * P.ldc + n;
-            *reinterpret_cast<f32x4*>(op) = f32x4{r[0], r[1], r[2], r[3]};
-            *reinterpret_cast<f32x4*>(op + 4) = f32x4{r[4], r[5], r[6], r[7]};
-            if (EPI == EPI_BIAS_RESID_F32 && P.o16)
-              *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
-                  u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
-          } else {
-            *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
-                u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
-            if (CAN_DB) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) cs[e] += r[e];
-            }
-          }
-        }
-      } else if (n < N) {
-        // edge columns (and unaligned leading dimensions): scalar epilogue + zero pad columns
-        for (int it = 0; it < IT; ++it) {
-          const int ml = it * RPI + rsub;
-          const int m = mb + ml;
-          if (m >= M) continue;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = ct[ml * CT + 8 * c8 + e];
-            if (n + e < N) cs[e] += epi_scalar<EPI>(P, o32, alpha, m, n + e, v);
-            else epi_pad<EPI>(P, m, n + e);
-          }
-        }
-      }
-    }
-    if (want_db) {
-      // rows of a column group live in lanes l, l^TPR, ... of every wave: fold those, then the
-      // waves via LDS (the staged tile is dead: every thread has read its own rows), one atomic
-      // per column
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-#pragma unroll
-        for (int o = TPR; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
-      __syncthreads();
-      float* red = ct;  // [NW waves][GBN columns]
-      if (lane < TPR) {
-        *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8) = f32x4{cs[0], cs[1], cs[2], cs[3]};
-        *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8 + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
-      }
-      __syncthreads();
-      if (tid < GBN && n0 + tid < N) {
-        float sum = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) sum += red[w * GBN + tid];
-        atomicAdd(P.dbias + n0 + tid, sum);
-      }
-    }
+  if constexpr (SWAP) {
+    epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
   } else {
     // acc[i][j]: rows = m (sub-tile i), cols = n (sub-tile j)
 #pragma unroll

@@ -16,7 +16,9 @@ Differences that are by design:
     oracle/ and is test infrastructure only);
   * logits are outputs without autograd history (the reference training loop differentiates
     only the losses; main.py:646-649);
-  * sequences must be exactly block_size long (the training/eval batches always are).
+  * training batches are exactly block_size long (as the reference's get_batch makes them); a
+    shorter sequence without targets (generate, inference) runs right-padded to block_size: the
+    attention is causal, so the logits of the real positions are exactly those of the short run.
 """
 import ctypes
 
@@ -262,12 +264,21 @@ class MultimodalTransformer(nn.Module):
             raise RuntimeError("MultimodalTransformer (libmmt_hip) runs only on a ROCm GPU: call .to('cuda') "
                                "(there is no CPU path)")
         B, T = idx_list[0].shape
-        if T != self.block_size:
-            raise NotImplementedError(f"sequence length {T} != block_size {self.block_size}")
+        if T > self.block_size:
+            raise ValueError(f"sequence length {T} exceeds block_size {self.block_size}")
+        if T < self.block_size and targets_list is not None:
+            raise NotImplementedError(f"training on sequence length {T} < block_size {self.block_size}: the training "
+                                      f"batches of the reference are always block_size long")
         idx = [t.to(device=flat.device, dtype=torch.long).contiguous() for t in idx_list]
         for t in idx:
             if tuple(t.shape) != (B, T):
                 raise ValueError("all modalities must share the [B, T] batch shape")
+        if T < self.block_size:
+            # causal: position t sees tokens <= t only, so right padding leaves positions < T unchanged
+            pad = self.block_size - T
+            idx = [torch.nn.functional.pad(t, (0, pad)) for t in idx]
+            logits = _MmtStep.apply(flat, self, False, M, *idx)
+            return [lg[:, :T] for lg in logits], None
         tensors = list(idx)
         if targets_list is not None:
             tensors += [t.to(device=flat.device, dtype=torch.long).contiguous() for t in targets_list]
@@ -279,8 +290,29 @@ class MultimodalTransformer(nn.Module):
         losses = outs[M]
         return logits, [losses[i] for i in range(M)]
 
+    @torch.no_grad()
     def generate(self, idx_list, max_new_tokens=1, modality_to_generate=0):
-        raise NotImplementedError("generate (model.py:404-446) is outside this build's hot path (SURVEY.md §8f)")
+        """model.py:404-446: per new token, a forward over the last block_size positions, a sample
+        from the softmax of the target modality's last logits (torch.multinomial, as the
+        reference), appended; the other modalities are padded with their last token or cropped to
+        the same length."""
+        seqs = [idx.clone() for idx in idx_list]
+        T = self.block_size
+        for _ in range(max_new_tokens):
+            cond = [s[:, -T:] for s in seqs]
+            logits, _ = self(cond)
+            probs = torch.softmax(logits[modality_to_generate][:, -1, :], dim=-1)
+            nxt = torch.multinomial(probs, num_samples=1).to(seqs[modality_to_generate].dtype)
+            seqs[modality_to_generate] = torch.cat((seqs[modality_to_generate].to(nxt.device), nxt), dim=1)
+            n = seqs[modality_to_generate].shape[1]
+            for i in range(self.num_modalities):
+                if i == modality_to_generate:
+                    continue
+                if seqs[i].shape[1] < n:
+                    seqs[i] = torch.cat((seqs[i], seqs[i][:, -1:]), dim=1)
+                elif seqs[i].shape[1] > n:
+                    seqs[i] = seqs[i][:, :n]
+        return seqs
 
     def __del__(self):
         try:
