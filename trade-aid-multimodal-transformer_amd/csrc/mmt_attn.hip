@@ -73,10 +73,9 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* lds, int stride, int dt,
 
 // accumulator registers 8s..8s+7 -> bf16 operand fragment
 __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)a[8 * s + j];
-  return r;
+  const u32x4 v = {pack2bf(a[8 * s], a[8 * s + 1]), pack2bf(a[8 * s + 2], a[8 * s + 3]),
+                   pack2bf(a[8 * s + 4], a[8 * s + 5]), pack2bf(a[8 * s + 6], a[8 * s + 7])};
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 __device__ __forceinline__ void zero16(f32x16& a) {
@@ -84,12 +83,19 @@ __device__ __forceinline__ void zero16(f32x16& a) {
   for (int e = 0; e < 16; ++e) a[e] = 0.f;
 }
 
-// keep predicate of accumulator element e of an S^T tile (queries on lanes) whose 32 mask dwords
-// lanes 0..31 hold in mv: dwords 2e, 2e+1 are exactly the lane mask of element e
-__device__ __forceinline__ bool keep_st(uint32_t mv, int e) {
-  const uint64_t mk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mv, 2 * e + 1) << 32) |
-                      (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mv, 2 * e);
-  return __builtin_amdgcn_inverse_ballot_w64(mk);
+// Keep bits of an S^T tile (queries on lanes), for the forward and dQ passes: dwords 2e, 2e+1 of the
+// tile are exactly the lane mask of accumulator element e, so the tile's 16 masks go straight into
+// SGPR pairs by scalar loads (the constant address space marks them read-only here) and each
+// element costs one v_cndmask
+typedef const __attribute__((address_space(4))) uint64_t* mask_sptr;
+__device__ __forceinline__ void load_mask_st(uint64_t (&mk)[16], const uint32_t* tile) {
+  const mask_sptr p = (mask_sptr)tile;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) mk[e] = p[e];
+}
+// the tile of (bh, query tile qt, key tile kt) in one stream's mask (AttnProblem::dmask)
+__device__ __forceinline__ const uint32_t* mask_tile(const uint32_t* base, int bh, int nt, int qt, int kt) {
+  return base + ((int64_t)bh * (nt * (nt + 1) / 2) + qt * (qt + 1) / 2 + kt) * 32;
 }
 
 // dword of an S^T mask tile that holds key r's keep bits over the tile's 32 queries
@@ -179,6 +185,10 @@ struct MaskStager {
 
 __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// packed fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth per instruction)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr float kTau = 8.0f;  // lazy-rescale threshold of the forward's running max (log2 units)
@@ -204,7 +214,8 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
                                          f32x16 (&oacc)[Geo<HS>::ND], float c2, const uint32_t* mt, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
-  const uint32_t mv = DROP ? mt[r] : 0u;  // this tile's keep bits (LDS)
+  uint64_t mk[16];
+  if (DROP) load_mask_st(mk, mt);  // this tile's keep bits (global, scalar loads)
   f32x16 sacc;
   zero16(sacc);
 #pragma unroll
@@ -241,18 +252,22 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
 #pragma unroll
       for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
   }
-  float rs = 0.f;
+  f32x2 rs2 = {0.f, 0.f};
+  const f32x2 c2v = {c2, c2}, nm = {-m, -m};
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const float pv = ex2(fmaf(sacc[e], c2, -m));
-    sacc[e] = pv;
-    rs += pv;
+  for (int e = 0; e < 16; e += 2) {
+    const f32x2 a = pk_fma(f32x2{sacc[e], sacc[e + 1]}, c2v, nm);
+    const f32x2 pv = {ex2(a.x), ex2(a.y)};
+    sacc[e] = pv.x;
+    sacc[e + 1] = pv.y;
+    rs2 += pv;
   }
+  float rs = rs2.x + rs2.y;
   rs += __shfl_xor(rs, 32, 64);
   l += rs;
   if (DROP) {  // dropout on the probabilities (the normaliser l keeps every term; 1/(1-p) at the end)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) sacc[e] = keep_st(mv, e) ? sacc[e] : 0.f;
+    for (int e = 0; e < 16; ++e) sacc[e] = __builtin_amdgcn_inverse_ballot_w64(mk[e]) ? sacc[e] : 0.f;
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -290,23 +305,16 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::TW];
-  using MS = MaskStager<HS>;
-  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];
   for (int q = tid; q < ROWS * G::RW; q += 256) if (q % G::RW >= HS) ks[q] = 0;
   for (int q = tid; q < ROWS * G::TW; q += 256) if (q % G::TW >= HS) vs[q] = 0;
   Stager<HS> st;
-  MS mst;
   st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
-  if (DROP) mst.load(P.dmask[0], bh, nt, qt0, 0, true, tid);
   st.store(ks, G::RW, vs, G::TW, tid);
-  if (DROP) mst.store(msk, tid);
   __syncthreads();
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb
   const bool la = qa < nt, lb = qb < nt;     // lb implies la
   const int tqa = qa * 32 + r, tqb = qb * 32 + r;
-  const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
-  const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
   bf16x8 qfa[G::NKS], qfb[G::NKS];
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
@@ -315,6 +323,7 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
     qfb[s] = ld8(P.q + (rowbase + tqb) * P.q_ld + head * HS + d0, lb && tqb < T && d0 < HS);
   }
   for (int j = 0; j < P.nstreams; ++j) {
+    const uint32_t* mj = DROP ? P.dmask[j] : nullptr;  // this stream's keep bits
     float ma = -INFINITY, lsa = 0.f, mb = -INFINITY, lsb = 0.f;
     f32x16 oa[G::ND], ob[G::ND];
 #pragma unroll
@@ -326,24 +335,24 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
         int kt = kt_lo;
 #pragma unroll 1
         for (; kt <= min(qa - 1, kt_hi); ++kt) {  // both tiles, off the diagonal
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mska + (kt - kt_lo) * 32, lane);
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (kt - kt_lo) * 32, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mask_tile(mj, bh, nt, qa, kt), lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mask_tile(mj, bh, nt, qb, kt), lane);
         }
         if (qa >= kt_lo && qa <= kt_hi) {  // tile a's diagonal, tile b off it
-          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mska + (qa - kt_lo) * 32, lane);
-          fwd_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (qa - kt_lo) * 32, lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mask_tile(mj, bh, nt, qa, qa), lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, mb, lsb, ob, c2, mask_tile(mj, bh, nt, qb, qa), lane);
         }
 #pragma unroll 1
         for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (kt - kt_lo) * 32, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mask_tile(mj, bh, nt, qb, kt), lane);
         if (qb >= kt_lo && qb <= kt_hi)
-          fwd_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (qb - kt_lo) * 32, lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, mb, lsb, ob, c2, mask_tile(mj, bh, nt, qb, qb), lane);
       } else if (la) {
 #pragma unroll 1
         for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mska + (kt - kt_lo) * 32, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mask_tile(mj, bh, nt, qa, kt), lane);
         if (qa >= kt_lo && qa <= kt_hi)
-          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mska + (qa - kt_lo) * 32, lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mask_tile(mj, bh, nt, qa, qa), lane);
       }
       // next (stream, chunk) resident for the whole block
       int nj = j, nc = c + 1;
@@ -352,9 +361,7 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
         __syncthreads();
         st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
                 T, tid);
-        if (DROP) mst.load(P.dmask[nj], bh, nt, qt0, nc * (ROWS / 32), true, tid);
         st.store(ks, G::RW, vs, G::TW, tid);
-        if (DROP) mst.store(msk, tid);
         __syncthreads();
       }
     }
@@ -417,7 +424,8 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
                                         const AttnProblem& P, const uint32_t* mt, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
-  const uint32_t mv = DROP ? mt[r] : 0u;  // this tile's keep bits (LDS)
+  uint64_t mk[16];
+  if (DROP) load_mask_st(mk, mt);  // this tile's keep bits (global, scalar loads)
   f32x16 sacc, dpacc;
   zero16(sacc);
   zero16(dpacc);
@@ -428,13 +436,25 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
     sacc = mfma32(kf, qf[s], sacc);
     dpacc = mfma32(vf, dof[s], dpacc);
   }
+  const f32x2 c2v = {c2, c2}, nl = {-lse2, -lse2}, nd = {-dsum, -dsum};
+  const f32x2 dsc = {DROP ? P.drop_scale : 1.f, DROP ? P.drop_scale : 1.f};
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-    float pv = ex2(sacc[e] * c2 - lse2);
-    if (diag && key > tq) pv = 0.f;
-    if (DROP) sacc[e] = pv * (keep_st(mv, e) ? fmaf(dpacc[e], P.drop_scale, -dsum) : -dsum);  // dS^T
-    else sacc[e] = pv * (dpacc[e] - dsum);
+  for (int e = 0; e < 16; e += 2) {
+    const f32x2 a = pk_fma(f32x2{sacc[e], sacc[e + 1]}, c2v, nl);
+    f32x2 pv = {ex2(a.x), ex2(a.y)};
+    if (diag) {
+      const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;  // keys key, key + 1
+      if (key > tq) pv.x = 0.f;
+      if (key + 1 > tq) pv.y = 0.f;
+    }
+    f32x2 t = pk_fma(f32x2{dpacc[e], dpacc[e + 1]}, dsc, nd);  // Z.dP - D (dropped: -D)
+    if (DROP) {
+      if (!__builtin_amdgcn_inverse_ballot_w64(mk[e])) t.x = nd.x;
+      if (!__builtin_amdgcn_inverse_ballot_w64(mk[e + 1])) t.y = nd.y;
+    }
+    const f32x2 ds = pv * t;  // dS^T
+    sacc[e] = ds.x;
+    sacc[e + 1] = ds.y;
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -468,24 +488,17 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::RW];  // V chunk: row reads
-  using MS = MaskStager<HS>;
-  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];
   for (int q = tid; q < ROWS * G::RW; q += 256)
     if (q % G::RW >= HS) { ks[q] = 0; vs[q] = 0; }
   Stager<HS> st;
-  MS mst;
   st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
-  if (DROP) mst.load(P.dmask[0], bh, nt, qt0, 0, true, tid);
   st.store(ks, G::RW, vs, G::RW, tid);
-  if (DROP) mst.store(msk, tid);
   __syncthreads();
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb; lb implies la
   const bool la = qa < nt, lb = qb < nt;
   const int tqa = qa * 32 + r, tqb = qb * 32 + r;
   const bool oka = la && tqa < T, okb = lb && tqb < T;
-  const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
-  const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
   bf16x8 qfa[G::NKS], dofa[G::NKS], qfb[G::NKS], dofb[G::NKS];
   f32x16 dqa[G::ND], dqb[G::ND];
 #pragma unroll
@@ -520,6 +533,7 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
     }
     const float lsa = oka ? P.lse[j][(int64_t)bh * T + tqa] * kLog2e : 0.f;
     const float lsb = okb ? P.lse[j][(int64_t)bh * T + tqb] * kLog2e : 0.f;
+    const uint32_t* mj = DROP ? P.dmask[j] : nullptr;  // this stream's keep bits
     for (int c = 0; c < nch; ++c) {
       const int kt_lo = c * (ROWS / 32);
       const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
@@ -527,31 +541,31 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
         int kt = kt_lo;
 #pragma unroll 1
         for (; kt <= min(qa - 1, kt_hi); ++kt) {
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (kt - kt_lo) * 32,
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mask_tile(mj, bh, nt, qa, kt),
                                    lane);
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (kt - kt_lo) * 32,
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mask_tile(mj, bh, nt, qb, kt),
                                    lane);
         }
         if (qa >= kt_lo && qa <= kt_hi) {
-          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (qa - kt_lo) * 32,
+          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mask_tile(mj, bh, nt, qa, qa),
                                   lane);
-          dq_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (qa - kt_lo) * 32,
+          dq_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mask_tile(mj, bh, nt, qb, qa),
                                    lane);
         }
 #pragma unroll 1
         for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (kt - kt_lo) * 32,
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mask_tile(mj, bh, nt, qb, kt),
                                    lane);
         if (qb >= kt_lo && qb <= kt_hi)
-          dq_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (qb - kt_lo) * 32,
+          dq_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mask_tile(mj, bh, nt, qb, qb),
                                   lane);
       } else if (la) {
 #pragma unroll 1
         for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (kt - kt_lo) * 32,
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mask_tile(mj, bh, nt, qa, kt),
                                    lane);
         if (qa >= kt_lo && qa <= kt_hi)
-          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (qa - kt_lo) * 32,
+          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mask_tile(mj, bh, nt, qa, qa),
                                   lane);
       }
       int nj = j, nc = c + 1;
@@ -560,9 +574,7 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
         __syncthreads();
         st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
                 T, tid);
-        if (DROP) mst.load(P.dmask[nj], bh, nt, qt0, nc * (ROWS / 32), true, tid);
         st.store(ks, G::RW, vs, G::RW, tid);
-        if (DROP) mst.store(msk, tid);
         __syncthreads();
       }
     }
@@ -616,19 +628,30 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
     const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsl + ql + 8 * g + 4 * h);
     const f32x4 d4 = *reinterpret_cast<const f32x4*>(dsl + ql + 8 * g + 4 * h);
 #pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
+    for (int e4 = 0; e4 < 4; e4 += 2) {  // element pairs in packed fp32
       const int e = 4 * g + e4;
-      const int tq = q0 + 8 * g + 4 * h + e4;
-      float pv = ex2(fmaf(sacc[e], c2, -l4[e4]));
-      if (MASKED && !(tk <= tq && tq < T)) pv = 0.f;
-      if (DROP) {  // pm = Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
-        const int km = (int)(mw << (31 - (8 * g + e4))) >> 31;  // all ones iff kept
-        pm[e] = __int_as_float(__float_as_int(pv) & km);
-        sacc[e] = pv * fmaf(__int_as_float(__float_as_int(dpacc[e]) & km), P.drop_scale, -d4[e4]);
-      } else {
-        pm[e] = pv;
-        sacc[e] = pv * (dpacc[e] - d4[e4]);  // dS[q][key]
+      const f32x2 a = pk_fma(f32x2{sacc[e], sacc[e + 1]}, f32x2{c2, c2}, f32x2{l4[e4], l4[e4 + 1]});
+      f32x2 pv = {ex2(a.x), ex2(a.y)};
+      if (MASKED) {
+        const int tq = q0 + 8 * g + 4 * h + e4;
+        if (!(tk <= tq && tq < T)) pv.x = 0.f;
+        if (!(tk <= tq + 1 && tq + 1 < T)) pv.y = 0.f;
       }
+      f32x2 dp = {dpacc[e], dpacc[e + 1]};
+      if (DROP) {  // pm = Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
+        const int k0 = (int)(mw << (31 - (8 * g + e4))) >> 31;  // all ones iff kept
+        const int k1 = (int)(mw << (30 - (8 * g + e4))) >> 31;
+        pm[e] = __int_as_float(__float_as_int(pv.x) & k0);
+        pm[e + 1] = __int_as_float(__float_as_int(pv.y) & k1);
+        dp = f32x2{__int_as_float(__float_as_int(dp.x) & k0), __int_as_float(__float_as_int(dp.y) & k1)};
+      } else {
+        pm[e] = pv.x;
+        pm[e + 1] = pv.y;
+      }
+      const float sc = DROP ? P.drop_scale : 1.f;
+      const f32x2 ds = pv * pk_fma(dp, f32x2{sc, sc}, f32x2{d4[e4], d4[e4 + 1]});  // dS[q][key]
+      sacc[e] = ds.x;
+      sacc[e + 1] = ds.y;
     }
   }
 #pragma unroll
@@ -674,7 +697,7 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) bf16_t dos[ROWS * G::RW];  // dO chunk: row + tr reads
-  __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // log2-domain LSE, D of the chunk rows
+  __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // -log2-domain LSE, -D of the chunk rows
   using MS = MaskStager<HS>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // [key tile][chunk q tile]
   for (int q = tid; q < ROWS * G::RW; q += 256)
@@ -697,7 +720,7 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
     for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
       const int t = r0 + (c % ROWS);
-      sl[u] = t < T ? ((c < ROWS) ? lsep[t] * kLog2e : dvp[t]) : 0.f;
+      sl[u] = t < T ? ((c < ROWS) ? -lsep[t] * kLog2e : -dvp[t]) : 0.f;  // negated: fma addends
     }
   };
   auto store = [&]() {
@@ -838,7 +861,7 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) bf16_t dos[ROWS * G::RW];  // dO chunk: row + tr reads
-  __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // log2-domain LSE, D of the chunk rows
+  __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // -log2-domain LSE, -D of the chunk rows
   using MS = MaskStager<HS>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // [key tile][chunk q tile]
   for (int q = tid; q < ROWS * G::RW; q += 256)
@@ -861,7 +884,7 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
     for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
       const int t = r0 + (c % ROWS);
-      sl[u] = t < T ? ((c < ROWS) ? lsep[t] * kLog2e : dvp[t]) : 0.f;
+      sl[u] = t < T ? ((c < ROWS) ? -lsep[t] * kLog2e : -dvp[t]) : 0.f;  // negated: fma addends
     }
   };
   auto store = [&]() {

@@ -25,8 +25,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
   return __builtin_bit_cast(bf16_t, b);
 }
+// two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (two scalar conversions joined by an OR
+// cost three instructions)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 // tanh for fp32 epilogues whose result is stored as bf16: exp-based away from 0, odd Taylor
