@@ -83,20 +83,9 @@ __device__ __forceinline__ void zero16(f32x16& a) {
   for (int e = 0; e < 16; ++e) a[e] = 0.f;
 }
 
-// Keep bits of an S^T tile (queries on lanes), for the forward and dQ passes: dwords 2e, 2e+1 of the
-// tile are exactly the lane mask of accumulator element e, so the tile's 16 masks go straight into
-// SGPR pairs by scalar loads (the constant address space marks them read-only here) and each
-// element costs one v_cndmask
-typedef const __attribute__((address_space(4))) uint64_t* mask_sptr;
-__device__ __forceinline__ void load_mask_st(uint64_t (&mk)[16], const uint32_t* tile) {
-  const mask_sptr p = (mask_sptr)tile;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) mk[e] = p[e];
-}
-// the tile of (bh, query tile qt, key tile kt) in one stream's mask (AttnProblem::dmask)
-__device__ __forceinline__ const uint32_t* mask_tile(const uint32_t* base, int bh, int nt, int qt, int kt) {
-  return base + ((int64_t)bh * (nt * (nt + 1) / 2) + qt * (qt + 1) / 2 + kt) * 32;
-}
+// all ones iff bit b of w is set (keep-bit select for float bit patterns: v_bfe_i32)
+__device__ __forceinline__ int bit_mask(uint32_t w, int b) { return (int)(w << (31 - b)) >> 31; }
+__device__ __forceinline__ float keep_f(float v, int m) { return __int_as_float(__float_as_int(v) & m); }
 
 // dword of an S^T mask tile that holds key r's keep bits over the tile's 32 queries
 __device__ __forceinline__ int key_dword(int r) { return 2 * ((r & 3) + 4 * (r >> 3)) + ((r >> 2) & 1); }
@@ -214,8 +203,7 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
                                          f32x16 (&oacc)[Geo<HS>::ND], float c2, const uint32_t* mt, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
-  uint64_t mk[16];
-  if (DROP) load_mask_st(mk, mt);  // this tile's keep bits (global, scalar loads)
+  const uint32_t mw = DROP ? reinterpret_cast<const uint16_t*>(mt)[lane] : 0u;  // this lane's keep bits (LDS)
   f32x16 sacc;
   zero16(sacc);
 #pragma unroll
@@ -267,7 +255,7 @@ __device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int
   l += rs;
   if (DROP) {  // dropout on the probabilities (the normaliser l keeps every term; 1/(1-p) at the end)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) sacc[e] = __builtin_amdgcn_inverse_ballot_w64(mk[e]) ? sacc[e] : 0.f;
+    for (int e = 0; e < 16; ++e) sacc[e] = keep_f(sacc[e], bit_mask(mw, e));
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -305,16 +293,25 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::TW];
+  using MS = MaskStager<HS>;
+  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // keep-bit lane words
   for (int q = tid; q < ROWS * G::RW; q += 256) if (q % G::RW >= HS) ks[q] = 0;
   for (int q = tid; q < ROWS * G::TW; q += 256) if (q % G::TW >= HS) vs[q] = 0;
   Stager<HS> st;
+  MS mst;
+  // lane-word record of the keep bits (AttnProblem::dmask): after the key-major one
+  const int64_t lw_off = (int64_t)(gridDim.x / nb) * (nt * (nt + 1) / 2) * 32;
   st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
+  if (DROP) mst.load(P.dmask[0] + lw_off, bh, nt, qt0, 0, true, tid);
   st.store(ks, G::RW, vs, G::TW, tid);
+  if (DROP) mst.store(msk, tid);
   __syncthreads();
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb
   const bool la = qa < nt, lb = qb < nt;     // lb implies la
   const int tqa = qa * 32 + r, tqb = qb * 32 + r;
+  const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
+  const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
   bf16x8 qfa[G::NKS], qfb[G::NKS];
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
@@ -323,7 +320,6 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
     qfb[s] = ld8(P.q + (rowbase + tqb) * P.q_ld + head * HS + d0, lb && tqb < T && d0 < HS);
   }
   for (int j = 0; j < P.nstreams; ++j) {
-    const uint32_t* mj = DROP ? P.dmask[j] : nullptr;  // this stream's keep bits
     float ma = -INFINITY, lsa = 0.f, mb = -INFINITY, lsb = 0.f;
     f32x16 oa[G::ND], ob[G::ND];
 #pragma unroll
@@ -335,24 +331,24 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
         int kt = kt_lo;
 #pragma unroll 1
         for (; kt <= min(qa - 1, kt_hi); ++kt) {  // both tiles, off the diagonal
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mask_tile(mj, bh, nt, qa, kt), lane);
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mask_tile(mj, bh, nt, qb, kt), lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mska + (kt - kt_lo) * 32, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (kt - kt_lo) * 32, lane);
         }
         if (qa >= kt_lo && qa <= kt_hi) {  // tile a's diagonal, tile b off it
-          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mask_tile(mj, bh, nt, qa, qa), lane);
-          fwd_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, mb, lsb, ob, c2, mask_tile(mj, bh, nt, qb, qa), lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mska + (qa - kt_lo) * 32, lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (qa - kt_lo) * 32, lane);
         }
 #pragma unroll 1
         for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mask_tile(mj, bh, nt, qb, kt), lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (kt - kt_lo) * 32, lane);
         if (qb >= kt_lo && qb <= kt_hi)
-          fwd_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, mb, lsb, ob, c2, mask_tile(mj, bh, nt, qb, qb), lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (qb - kt_lo) * 32, lane);
       } else if (la) {
 #pragma unroll 1
         for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mask_tile(mj, bh, nt, qa, kt), lane);
+          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mska + (kt - kt_lo) * 32, lane);
         if (qa >= kt_lo && qa <= kt_hi)
-          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mask_tile(mj, bh, nt, qa, qa), lane);
+          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mska + (qa - kt_lo) * 32, lane);
       }
       // next (stream, chunk) resident for the whole block
       int nj = j, nc = c + 1;
@@ -361,7 +357,9 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
         __syncthreads();
         st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
                 T, tid);
+        if (DROP) mst.load(P.dmask[nj] + lw_off, bh, nt, qt0, nc * (ROWS / 32), true, tid);
         st.store(ks, G::RW, vs, G::TW, tid);
+        if (DROP) mst.store(msk, tid);
         __syncthreads();
       }
     }
@@ -424,8 +422,7 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
                                         const AttnProblem& P, const uint32_t* mt, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
-  uint64_t mk[16];
-  if (DROP) load_mask_st(mk, mt);  // this tile's keep bits (global, scalar loads)
+  const uint32_t mw = DROP ? reinterpret_cast<const uint16_t*>(mt)[lane] : 0u;  // this lane's keep bits (LDS)
   f32x16 sacc, dpacc;
   zero16(sacc);
   zero16(dpacc);
@@ -447,11 +444,9 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
       if (key > tq) pv.x = 0.f;
       if (key + 1 > tq) pv.y = 0.f;
     }
-    f32x2 t = pk_fma(f32x2{dpacc[e], dpacc[e + 1]}, dsc, nd);  // Z.dP - D (dropped: -D)
-    if (DROP) {
-      if (!__builtin_amdgcn_inverse_ballot_w64(mk[e])) t.x = nd.x;
-      if (!__builtin_amdgcn_inverse_ballot_w64(mk[e + 1])) t.y = nd.y;
-    }
+    f32x2 dp = {dpacc[e], dpacc[e + 1]};
+    if (DROP) dp = f32x2{keep_f(dp.x, bit_mask(mw, e)), keep_f(dp.y, bit_mask(mw, e + 1))};
+    const f32x2 t = pk_fma(dp, dsc, nd);  // Z.dP - D (dropped: -D)
     const f32x2 ds = pv * t;  // dS^T
     sacc[e] = ds.x;
     sacc[e + 1] = ds.y;
@@ -488,16 +483,25 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::RW];  // V chunk: row reads
+  using MS = MaskStager<HS>;
+  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // keep-bit lane words
   for (int q = tid; q < ROWS * G::RW; q += 256)
     if (q % G::RW >= HS) { ks[q] = 0; vs[q] = 0; }
   Stager<HS> st;
+  MS mst;
+  // lane-word record of the keep bits (AttnProblem::dmask): after the key-major one
+  const int64_t lw_off = (int64_t)(gridDim.x / nb) * (nt * (nt + 1) / 2) * 32;
   st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
+  if (DROP) mst.load(P.dmask[0] + lw_off, bh, nt, qt0, 0, true, tid);
   st.store(ks, G::RW, vs, G::RW, tid);
+  if (DROP) mst.store(msk, tid);
   __syncthreads();
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb; lb implies la
   const bool la = qa < nt, lb = qb < nt;
   const int tqa = qa * 32 + r, tqb = qb * 32 + r;
+  const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
+  const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
   const bool oka = la && tqa < T, okb = lb && tqb < T;
   bf16x8 qfa[G::NKS], dofa[G::NKS], qfb[G::NKS], dofb[G::NKS];
   f32x16 dqa[G::ND], dqb[G::ND];
@@ -533,7 +537,6 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
     }
     const float lsa = oka ? P.lse[j][(int64_t)bh * T + tqa] * kLog2e : 0.f;
     const float lsb = okb ? P.lse[j][(int64_t)bh * T + tqb] * kLog2e : 0.f;
-    const uint32_t* mj = DROP ? P.dmask[j] : nullptr;  // this stream's keep bits
     for (int c = 0; c < nch; ++c) {
       const int kt_lo = c * (ROWS / 32);
       const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
@@ -541,31 +544,31 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
         int kt = kt_lo;
 #pragma unroll 1
         for (; kt <= min(qa - 1, kt_hi); ++kt) {
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mask_tile(mj, bh, nt, qa, kt),
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (kt - kt_lo) * 32,
                                    lane);
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mask_tile(mj, bh, nt, qb, kt),
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (kt - kt_lo) * 32,
                                    lane);
         }
         if (qa >= kt_lo && qa <= kt_hi) {
-          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mask_tile(mj, bh, nt, qa, qa),
+          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (qa - kt_lo) * 32,
                                   lane);
-          dq_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mask_tile(mj, bh, nt, qb, qa),
+          dq_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (qa - kt_lo) * 32,
                                    lane);
         }
 #pragma unroll 1
         for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mask_tile(mj, bh, nt, qb, kt),
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (kt - kt_lo) * 32,
                                    lane);
         if (qb >= kt_lo && qb <= kt_hi)
-          dq_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mask_tile(mj, bh, nt, qb, qb),
+          dq_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (qb - kt_lo) * 32,
                                   lane);
       } else if (la) {
 #pragma unroll 1
         for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mask_tile(mj, bh, nt, qa, kt),
+          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (kt - kt_lo) * 32,
                                    lane);
         if (qa >= kt_lo && qa <= kt_hi)
-          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mask_tile(mj, bh, nt, qa, qa),
+          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (qa - kt_lo) * 32,
                                   lane);
       }
       int nj = j, nc = c + 1;
@@ -574,7 +577,9 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
         __syncthreads();
         st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
                 T, tid);
+        if (DROP) mst.load(P.dmask[nj] + lw_off, bh, nt, qt0, nc * (ROWS / 32), true, tid);
         st.store(ks, G::RW, vs, G::RW, tid);
+        if (DROP) mst.store(msk, tid);
         __syncthreads();
       }
     }
@@ -1058,18 +1063,22 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH,
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
   const uint32_t drow = (uint32_t)(bh * T + qt * 32 + r);
-  uint32_t out = 0;  // lane L < 32 collects dword L = half (L & 1) of element (L >> 1)'s ballot
+  uint32_t out = 0;   // lane L < 32 collects key-major dword L = half (L & 1) of element (L >> 1)'s ballot
+  uint32_t word = 0;  // this lane's own 16 bits
 #pragma unroll
   for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
     const uint32_t key = (uint32_t)(kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h);
     const uint32_t hk = mmt_hash(dkey, drow, key >> 1);
-    const uint64_t b0 = __builtin_amdgcn_ballot_w64(mmt_keep(hk, 0, P.drop_thr));
-    const uint64_t b1 = __builtin_amdgcn_ballot_w64(mmt_keep(hk, 1, P.drop_thr));
+    const bool k0 = mmt_keep(hk, 0, P.drop_thr), k1 = mmt_keep(hk, 1, P.drop_thr);
+    const uint64_t b0 = __builtin_amdgcn_ballot_w64(k0);
+    const uint64_t b1 = __builtin_amdgcn_ballot_w64(k1);
     const uint32_t w0 = (lane & 1) ? (uint32_t)(b0 >> 32) : (uint32_t)b0;
     const uint32_t w1 = (lane & 1) ? (uint32_t)(b1 >> 32) : (uint32_t)b1;
     out = ((lane >> 1) == e) ? w0 : ((lane >> 1) == e + 1) ? w1 : out;
+    word |= ((uint32_t)k0 << e) | ((uint32_t)k1 << (e + 1));
   }
   if (lane < 32) P.dmask[j][tt * 32 + lane] = out;
+  reinterpret_cast<uint16_t*>(P.dmask[j] + (per + tt) * 32)[lane] = (uint16_t)word;
 }
 
 hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStream_t s) {

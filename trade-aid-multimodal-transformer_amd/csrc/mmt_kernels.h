@@ -116,16 +116,19 @@ struct AttnProblem {
   uint32_t drop_key, drop_thr;
   float drop_scale;
   // keep bits of that mask (required when drop_thr != 0), made by mmt_launch_attn_mask and read by
-  // the forward and both backward kernels: per stream, per (bh, query tile qt, key tile kt <= qt)
-  // 32 dwords at ((bh * ntri + qt*(qt+1)/2 + kt) * 32), ntri = nt*(nt+1)/2; dword 2e + u, bit r =
-  // keep(query qt*32 + r, key kt*32 + (e&3) + 8(e>>2) + 4u) — the accumulator order of an S^T tile
+  // the forward and both backward kernels. Per stream, per (bh, query tile qt, key tile kt <= qt)
+  // tile index t = bh * ntri + qt*(qt+1)/2 + kt (ntri = nt*(nt+1)/2), two 128-B records of the
+  // S^T tile's accumulator elements e (query qt*32 + r, key kt*32 + (e&3) + 8(e>>2) + 4u, lane
+  // r + 32u): key-major words at dmask[j] + 32 t (dword 2e + u, bit r: the dK/dV pass, keys on
+  // lanes) and lane words at dmask[j] + 32 (ntiles + t) (16 bits per lane, bit e: forward and dQ)
   uint32_t* dmask[MMT_MAX_STREAMS];
 };
-// dwords of keep bits for one stream of one attention problem (see AttnProblem::dmask)
-inline int64_t mmt_attn_mask_dwords(int B, int H, int T) {
+// tiles of one stream's mask, and its dwords (both records; see AttnProblem::dmask)
+inline int64_t mmt_attn_mask_tiles(int B, int H, int T) {
   const int64_t nt = (T + 31) / 32;
-  return (int64_t)B * H * (nt * (nt + 1) / 2) * 32;
+  return (int64_t)B * H * (nt * (nt + 1) / 2);
 }
+inline int64_t mmt_attn_mask_dwords(int B, int H, int T) { return 2 * 32 * mmt_attn_mask_tiles(B, H, T); }
 struct AttnBatch { AttnProblem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
 hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
