@@ -23,39 +23,48 @@ __device__ __forceinline__ void ld4_guarded(const bf16_t* p, int valid, uint32_t
   }
 }
 
-__device__ __forceinline__ bf16x8 pack8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  const u32x4 v = {a, b, c, d};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
 // ---------------------------------------------------------------------------------------------
 template <int HS>
 __global__ __launch_bounds__(256) void qkv2_fwd_mfma(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
   constexpr int HH = HS / 2;
   constexpr int NOT = (HS + 31) / 32;  // output (o) tiles
   constexpr int KS = (HH + 15) / 16;   // k-steps over i
+  constexpr int SHW = KS * 16 + 8;     // h1 tile row (zero padded to the k-steps; +8 de-conflicts)
+  constexpr int SOW = HS + 8;          // out tile row
   const Qkv2Problem& P = batch.p[blockIdx.z];
   // grid.x = row blocks x nblk, blk fastest in logical order (one row's blocks share its lines)
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const int nblk = gridDim.x / ((R + 127) / 128);
   const int blk = tile % nblk, rb = tile / nblk;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int row = rb * 128 + w * 32 + r;
-  const float* w2 = P.w2 + (int64_t)blk * HS * HH;
-  // B operand: h1[row][i = 16s + 8h + j]
-  bf16x8 hb[KS];
+  const int r0 = rb * 128;
+  __shared__ __attribute__((aligned(16))) bf16_t sh[128 * SHW];
+  __shared__ __attribute__((aligned(16))) bf16_t so[128 * SOW];
+  // h1 strip [128][HH] in 8-B pieces, consecutive lanes along a row; pad columns zero
+  constexpr int HPC = HH / 4, PPC = (KS * 16 - HH) / 4;
+  constexpr int NL = (128 * HPC + 255) / 256;
+  u32x2 hv[NL];  // every load in flight before the LDS stores
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int i0 = 16 * s + 8 * h;
-    uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-    if (row < R) {
-      const bf16_t* src = P.h1 + (int64_t)row * ld_h1 + blk * HH + i0;
-      if (i0 < HH) ld4_guarded<4>(src, HH - i0, a0, a1);
-      if (i0 + 4 < HH) ld4_guarded<4>(src + 4, HH - i0 - 4, b0, b1);
-    }
-    hb[s] = pack8(a0, a1, b0, b1);
+  for (int u = 0; u < NL; ++u) {
+    const int c = tid + 256 * u, row = c / HPC, col = (c % HPC) * 4;
+    hv[u] = u32x2{0u, 0u};
+    if (c < 128 * HPC && r0 + row < R)
+      hv[u] = *reinterpret_cast<const u32x2*>(P.h1 + (int64_t)(r0 + row) * ld_h1 + blk * HH + col);
   }
+#pragma unroll
+  for (int u = 0; u < NL; ++u) {
+    const int c = tid + 256 * u;
+    if (c < 128 * HPC) *reinterpret_cast<u32x2*>(sh + (c / HPC) * SHW + (c % HPC) * 4) = hv[u];
+  }
+  if (PPC > 0)
+    for (int c = tid; c < 128 * PPC; c += 256) {
+      const int row = c / PPC, col = HH + (c % PPC) * 4;
+      *reinterpret_cast<u32x2*>(sh + row * SHW + col) = u32x2{0u, 0u};
+    }
+  const float* w2 = P.w2 + (int64_t)blk * HS * HH;
+  __syncthreads();
+  const int lr = w * 32;
 #pragma unroll
   for (int ot = 0; ot < NOT; ++ot) {
     const int o = ot * 32 + r;
@@ -70,19 +79,26 @@ __global__ __launch_bounds__(256) void qkv2_fwd_mfma(Qkv2Batch batch, int R, int
         const int i = 16 * s + 8 * h + j;
         wa[j] = (__bf16)((o < HS && i < HH) ? w2[o * HH + i] : 0.f);
       }
-      acc = mfma32(wa, hb[s], acc);  // D[o][row]
+      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(sh + (lr + r) * SHW + 16 * s + 8 * h);
+      acc = mfma32(wa, hb, acc);  // D[o][row]
     }
     // lane owns row (r) and o = ot*32 + (e&3) + 8(e>>2) + 4h
-    const int orow = rb * 128 + w * 32 + r;
-    if (orow < R) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int o0 = ot * 32 + 8 * g + 4 * h;
-        if (o0 < HS)
-          *reinterpret_cast<u32x2*>(P.out + (int64_t)orow * ld_out + blk * HS + o0) =
-              u32x2{pack2bf(acc[4 * g], acc[4 * g + 1]), pack2bf(acc[4 * g + 2], acc[4 * g + 3])};
-      }
+    for (int g = 0; g < 4; ++g) {
+      const int o0 = ot * 32 + 8 * g + 4 * h;
+      if (o0 < HS)
+        *reinterpret_cast<u32x2*>(so + (lr + r) * SOW + o0) =
+            u32x2{pack2bf(acc[4 * g], acc[4 * g + 1]), pack2bf(acc[4 * g + 2], acc[4 * g + 3])};
     }
+  }
+  __syncthreads();
+  // out strip [128][HS] in 8-B pieces, consecutive lanes along a row
+  constexpr int OPC = HS / 4;
+  for (int c = tid; c < 128 * OPC; c += 256) {
+    const int row = c / OPC, col = (c % OPC) * 4;
+    if (r0 + row < R)
+      *reinterpret_cast<u32x2*>(P.out + (int64_t)(r0 + row) * ld_out + blk * HS + col) =
+          *reinterpret_cast<const u32x2*>(so + row * SOW + col);
   }
 }
 
