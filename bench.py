@@ -123,8 +123,8 @@ def cpu_baseline(cfg, data, seconds):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200, help="timed steps (SURVEY.md §8d: 200)")
+    ap.add_argument("--warmup", type=int, default=20, help="untimed warm-up steps (SURVEY.md §8d: 20)")
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--dropout", type=float, default=0.1,
