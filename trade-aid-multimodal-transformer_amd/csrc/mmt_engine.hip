@@ -74,7 +74,10 @@ struct Plan {
   size_t xemb[MAXM];
   size_t lnf16[MAXM], meanf[MAXM], rstdf[MAXM], hh[MAXM], dlog[MAXM];
   // backward scratch, per modality
-  size_t dres[MAXM], dres16[MAXM], dln[MAXM], gbig[MAXM], gdo[MAXM], gq[MAXM], gqkv[MAXM], gh1[MAXM], gp[MAXM];
+  size_t dres[MAXM], dln[MAXM], gbig[MAXM], gdo[MAXM], gq[MAXM], gqkv[MAXM], gh1[MAXM], gp[MAXM], gpc[MAXM];
+  // bf16 residual-gradient copies, rotated over 4 buffers (one per LayerNorm-backward / copy launch):
+  // a side-stream weight-gradient GEMM still reading one does not block the next write
+  size_t dres16[4][MAXM];
   size_t dvec[MAXM][MAXM];
   size_t dkv[MAXM][MAXM];
 };
@@ -122,6 +125,7 @@ struct mmt_ctx {
   int side_device = -1;
   std::vector<hipEvent_t> evpool;
   size_t evnext = 0;
+  int d16 = 0;  // rotation index of the current dres16 copy (reset at backward stage 0)
 };
 
 namespace {
@@ -351,10 +355,12 @@ void make_plan(mmt_ctx* c, int B) {
     p.hh[i] = A(R * c->ldvh[i] * b2); p.dlog[i] = A(R * c->ldv[i] * b2);
   }
   for (int i = 0; i < M; ++i) {
-    p.dres[i] = A(R * C * f4); p.dres16[i] = A(R * C * b2); p.dln[i] = A(R * C * f4);
+    p.dres[i] = A(R * C * f4); p.dln[i] = A(R * C * f4);
+    for (int k = 0; k < 4; ++k) p.dres16[k][i] = A(R * C * b2);
     p.gbig[i] = A(R * std::max(4 * C, maxvh) * b2);
     p.gdo[i] = A(R * C * b2); p.gq[i] = A(R * C * b2); p.gqkv[i] = A(R * 3 * C * b2);
     p.gh1[i] = A(R * ldh1 * b2); p.gp[i] = A(R * ldp * b2);
+    p.gpc[i] = (c->any_cross && c->cfg.cross_attention[i]) ? A(R * ldp * b2) : p.gp[i];
     for (int j = 0; j < M; ++j) p.dvec[i][j] = A(bhT * f4);
     if (c->any_cross && c->cfg.cross_attention[i])
       for (int j = 0; j < M - 1; ++j) p.dkv[i][j] = A(R * 2 * C * b2);
@@ -456,15 +462,27 @@ struct Runner {
   }
   // the main stream waits for everything enqueued on the side stream
   void join() {
+    flush();
     if (!c->side) return;
     hipEvent_t e = c->evpool[c->evnext++ % c->evpool.size()];
     ok(hipEventRecord(e, c->side), "event record");
     ok(hipStreamWaitEvent(s, e, 0), "stream wait");
   }
+  // weight-gradient GEMMs go to the side stream in batches: dwgemm() queues one, flush() forks the
+  // side stream once (after everything its queued GEMMs read is enqueued on the main stream) and
+  // launches them. Every fork / join is a barrier packet costing ~10 us of main-stream idle, so
+  // the stage code flushes a few times per layer instead of forking per GEMM.
+  std::vector<std::pair<GemmBatch, const char*>> pend;
+  void flush() {
+    if (pend.empty() || rc != MMT_OK) { pend.clear(); return; }
+    hipStream_t ss = side();
+    for (auto& q : pend) ok(mmt_launch_gemm_wgrad(q.first, W<float>(c->plan.slab), (int64_t)c->plan.slab_bytes, ss), q.second);
+    pend.clear();
+  }
   void dwgemm(const GemmBatch& b, const char* what) {
     if (rc != MMT_OK) return;
     if (c->side && !probing(what)) {
-      ok(mmt_launch_gemm_wgrad(b, W<float>(c->plan.slab), (int64_t)c->plan.slab_bytes, side()), what);
+      pend.emplace_back(b, what);
       return;
     }
     probe_begin(what);
@@ -486,6 +504,29 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   Plan& p = c->plan;
   bf16_t* wpk = r.W<bf16_t>(p.pack);
   r.wpk = wpk;
+  // keep bits of layer ll's self- and cross-attention dropout, one side-stream launch each (the
+  // mask kernel reads nothing the main stream writes: a fork orders it after the previous step)
+  auto gen_masks = [&](int ll) {
+    hipStream_t ss = r.side();
+    const LM* xl = &c->lm[(size_t)ll * M];
+    const ActLM* al = &p.act[(size_t)ll * M];
+    AttnBatch mb{}; mb.count = M;
+    for (int i = 0; i < M; ++i) {
+      r.set_drop(mb.p[i], ll, i, DS_SA_PROB);
+      mb.p[i].nstreams = 1; mb.p[i].dmask[0] = r.W<uint32_t>(al[i].dm);
+    }
+    r.ok(mmt_launch_attn_mask(mb, B, T, H, ss), "attn_mask");
+    if (!c->any_cross) return;
+    AttnBatch mc{}; mc.count = 0;
+    for (int i = 0; i < M; ++i) {
+      if (!xl[i].cross) continue;
+      AttnProblem& q = mc.p[mc.count++];
+      r.set_drop(q, ll, i, DS_CA_PROB);
+      q.nstreams = M - 1;
+      for (int j = 0; j < M - 1; ++j) q.dmask[j] = r.W<uint32_t>(al[i].dmj[j]);
+    }
+    if (mc.count) r.ok(mmt_launch_attn_mask(mc, B, T, H, ss), "ca_attn_mask");
+  };
   if (!r.ok(mmt_launch_pack(c->d_segs, (int)c->segs.size(), (int64_t)c->tasks.size() / 2, c->d_tasks, r.params, wpk,
                             r.s), "pack"))
     return r.rc;
@@ -503,16 +544,9 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   for (int l = 0; l < c->L && r.rc == MMT_OK; ++l) {
     const LM* x = &c->lm[(size_t)l * M];
     const ActLM* a = &p.act[(size_t)l * M];
-    // self-attention dropout keep bits of this layer: made on the side stream while LayerNorm and
-    // the Q/K/V GEMMs run, joined before the attention forward
-    if (r.drop) {
-      AttnBatch mb{}; mb.count = M;
-      for (int i = 0; i < M; ++i) {
-        r.set_drop(mb.p[i], l, i, DS_SA_PROB);
-        mb.p[i].nstreams = 1; mb.p[i].dmask[0] = r.W<uint32_t>(a[i].dm);
-      }
-      r.ok(mmt_launch_attn_mask(mb, B, T, H, r.side()), "attn_mask");
-    }
+    // attention dropout keep bits: layer 0's made on the side stream while the first LayerNorm and
+    // Q/K/V GEMMs run; every later layer's while the previous layer computes (gen_masks below)
+    if (r.drop && l == 0) gen_masks(0);
     LnBatch lb{}; lb.count = M;
     for (int i = 0; i < M; ++i) {
       lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].beta = r.P(x[i].ln1b);
@@ -539,22 +573,13 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       r.set_drop(q, l, i, DS_SA_PROB);
       if (r.drop) q.dmask[0] = r.W<uint32_t>(a[i].dm);
     }
-    if (r.drop) r.join();
+    if (r.drop) {
+      r.join();  // this layer's keep bits (SA and CA) are in
+      if (l + 1 < c->L) gen_masks(l + 1);
+    }
     r.probe_begin("attn_fwd");
     r.ok(mmt_launch_attn_fwd(ab, B, T, H, hs, scale, r.s), "attn_fwd");
     r.probe_end("attn_fwd");
-    // cross-attention keep bits, overlapping the rest of the layer up to the CA forward
-    if (r.drop && c->any_cross) {
-      AttnBatch mc{}; mc.count = 0;
-      for (int i = 0; i < M; ++i) {
-        if (!x[i].cross) continue;
-        AttnProblem& q = mc.p[mc.count++];
-        r.set_drop(q, l, i, DS_CA_PROB);
-        q.nstreams = M - 1;
-        for (int j = 0; j < M - 1; ++j) q.dmask[j] = r.W<uint32_t>(a[i].dmj[j]);
-      }
-      r.ok(mmt_launch_attn_mask(mc, B, T, H, r.side()), "ca_attn_mask");
-    }
     for (int i = 0; i < M; ++i) {
       g.p[i] = gp_fwd(r.W<bf16_t>(a[i].o), C, wpk, x[i].P0, R);
       g.p[i].bias = r.P(x[i].bp0); g.p[i].o16 = r.W<bf16_t>(a[i].p1); g.p[i].ldo16 = ldp;
@@ -628,7 +653,6 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         if (r.drop)
           for (int j = 0; j < M - 1; ++j) q.dmask[j] = r.W<uint32_t>(a[i].dmj[j]);
       }
-      if (r.drop) r.join();
       r.probe_begin("ca_attn_fwd");
       r.ok(mmt_launch_attn_fwd(cb, B, T, H, hs, scale, r.s), "ca_attn_fwd");
       r.probe_end("ca_attn_fwd");
@@ -690,6 +714,10 @@ void colsum_add(Runner& r, ColsumBatch& cb, int u, const bf16_t* x, int ld, floa
 // cross-attention), else its FFN. The copy carries that branch's dropout mask and its column
 // sums are that branch's output-bias gradient. Modalities whose copy is rebuilt later (non-cross
 // modalities of a cross model) and lprev < 0 (embeddings) get no copy.
+// current dres16 copy (the last one written), and the next one in the rotation (for a writer)
+inline bf16_t* d16_cur(mmt_ctx* c, Runner& r, int i) { return r.W<bf16_t>(c->plan.dres16[c->d16 & 3][i]); }
+inline void d16_advance(mmt_ctx* c) { ++c->d16; }
+
 void set_dres16_consumer(mmt_ctx* c, Runner& r, LnProblem& lp, int i, int lprev, float* grads) {
   lp.dx16 = nullptr; lp.dsum = nullptr;
   lp.drop_key = 0; lp.drop_thr = 0; lp.drop_scale = 1.f;
@@ -703,7 +731,7 @@ void set_dres16_consumer(mmt_ctx* c, Runner& r, LnProblem& lp, int i, int lprev,
     r.set_drop(lp, lprev, i, DS_FFN);
     lp.dsum = grads + x.bf2;
   }
-  lp.dx16 = r.W<bf16_t>(c->plan.dres16[i]);
+  lp.dx16 = d16_cur(c, r, i);  // the caller advanced the rotation for this launch
 }
 
 int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads, float* grads) {
@@ -713,6 +741,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   Plan& p = c->plan;
   const bf16_t* wpk = r.W<bf16_t>(p.pack);
   if (stage == 0) {
+    c->d16 = 0;
     HIPCHK(c, hipMemsetAsync(grads, 0, sizeof(float) * c->nparams, r.s));
     const float invR = 1.0f / (float)R;
     GemmBatch dw{}; dw.count = M;
@@ -742,7 +771,9 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     }
     r.dwgemm(dw, "head0_dw");
     r.gemm(dx, true, false, EPI_STORE_F32, 1, "head0_dx");
+    r.flush();
     LnBatch lb{}; lb.count = M;
+    d16_advance(c);
     std::vector<const float*> xfin(M);
     for (int i = 0; i < M; ++i) {
       const ActLM& a = p.act[(size_t)(L - 1) * M + i];
@@ -753,7 +784,6 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       set_dres16_consumer(c, r, lb.p[i], i, L - 1, grads);
       lb.p[i].dgamma = grads + c->post[i].lnw; lb.p[i].dbeta = grads + c->post[i].lnb;
     }
-    r.join();  // lnf_bwd rewrites dres16 (read by side-stream weight-gradient GEMMs)
     r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "lnf_bwd");
     return r.rc;
   }
@@ -778,23 +808,24 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
       // dres16[i] already carries this projection's dropout mask; its bias grad came with it
-      const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
+      const bf16_t* g = d16_cur(c, r, i);
       dw.p[u] = gp_dw(g, C, r.W<bf16_t>(a[i].pc), ldp, grads, x[i].C2, R);
       dx.p[u] = gp_dx(g, C, wpk, x[i].C2, R);
-      dx.p[u].aux = r.W<bf16_t>(a[i].pc); dx.p[u].ldaux = ldp; dx.p[u].o16 = r.W<bf16_t>(p.gp[i]); dx.p[u].ldo16 = ldp;
+      dx.p[u].aux = r.W<bf16_t>(a[i].pc); dx.p[u].ldaux = ldp; dx.p[u].o16 = r.W<bf16_t>(p.gpc[i]); dx.p[u].ldo16 = ldp;
       dx.p[u].dbias = grads + x[i].bc0;
     }
     r.dwgemm(dw, "ca_proj2_dw");
     r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "ca_proj2_dx");
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
-      const bf16_t* g = r.W<bf16_t>(p.gp[i]);
+      const bf16_t* g = r.W<bf16_t>(p.gpc[i]);
       dw.p[u] = gp_dw(g, ldp, r.W<bf16_t>(a[i].oc), C, grads, x[i].C0, R);
       dx.p[u] = gp_dx(g, ldp, wpk, x[i].C0, R);
       dx.p[u].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[u].ldo16 = C;
     }
     r.dwgemm(dw, "ca_proj0_dw");
     r.gemm(dx, true, false, EPI_STORE_BF16, 1, "ca_proj0_dx");
+    r.flush();
     AttnBatch ab{}; ab.count = nc;
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
@@ -855,13 +886,14 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       }
       if (kw.count) { r.dwgemm(kw, "ca_kv_dw"); r.gemm(kx, true, false, EPI_ACC_F32, 1, "ca_kv_dx"); }
     }
+    r.flush();
     // bf16 copy for the FFN backward: FFN dropout mask + FFN output-bias gradient
     DropCopyBatch db{}; db.count = M;
+    d16_advance(c);
     for (int i = 0; i < M; ++i) {
-      db.p[i].src = r.W<float>(p.dres[i]); db.p[i].dst = r.W<bf16_t>(p.dres16[i]); db.p[i].dsum = grads + x[i].bf2;
+      db.p[i].src = r.W<float>(p.dres[i]); db.p[i].dst = d16_cur(c, r, i); db.p[i].dsum = grads + x[i].bf2;
       r.set_drop(db.p[i], l, i, DS_FFN);
     }
-    r.join();
     r.ok(mmt_launch_drop_copy(db, R, C, r.s), "dres16");
   }
   if (r.rc != MMT_OK) return r.rc;
@@ -872,7 +904,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   LnBatch lb{}; lb.count = M;
   for (int i = 0; i < M; ++i) {
     // dres16[i] carries the FFN dropout mask; the FFN output-bias grad was summed with it
-    const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
+    const bf16_t* g = d16_cur(c, r, i);
     dw.p[i] = gp_dw(g, C, r.W<bf16_t>(a[i].f), 4 * C, grads, x[i].F2, R);
     dx.p[i] = gp_dx(g, C, wpk, x[i].F2, R);
     dx.p[i].aux = r.W<bf16_t>(a[i].f); dx.p[i].ldaux = 4 * C; dx.p[i].o16 = r.W<bf16_t>(p.gbig[i]); dx.p[i].ldo16 = 4 * C;
@@ -888,18 +920,19 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   }
   r.dwgemm(dw, "ffn0_dw");
   r.gemm(dx, true, false, EPI_STORE_F32, 1, "ffn0_dx");
+  r.flush();
+  d16_advance(c);
   for (int i = 0; i < M; ++i) {
     lb.p[i].x = r.W<float>(a[i].x1); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].mean = r.W<float>(a[i].mean2);
     lb.p[i].rstd = r.W<float>(a[i].rstd2); lb.p[i].dy = r.W<float>(p.dln[i]); lb.p[i].dx = r.W<float>(p.dres[i]);
-    lb.p[i].dx16 = r.W<bf16_t>(p.dres16[i]); lb.p[i].dgamma = grads + x[i].ln2w; lb.p[i].dbeta = grads + x[i].ln2b;
+    lb.p[i].dx16 = d16_cur(c, r, i); lb.p[i].dgamma = grads + x[i].ln2w; lb.p[i].dbeta = grads + x[i].ln2b;
     r.set_drop(lb.p[i], l, i, DS_SA_PROJ);  // the copy feeds the SA projection backward
     lb.p[i].dsum = grads + x[i].bp2;
   }
-  r.join();
   r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln2_bwd");
   // SA output projection
   for (int i = 0; i < M; ++i) {
-    const bf16_t* g = r.W<bf16_t>(p.dres16[i]);
+    const bf16_t* g = d16_cur(c, r, i);
     dw.p[i] = gp_dw(g, C, r.W<bf16_t>(a[i].p1), ldp, grads, x[i].P2, R);
     dx.p[i] = gp_dx(g, C, wpk, x[i].P2, R);
     dx.p[i].aux = r.W<bf16_t>(a[i].p1); dx.p[i].ldaux = ldp; dx.p[i].o16 = r.W<bf16_t>(p.gp[i]); dx.p[i].ldo16 = ldp;
@@ -915,6 +948,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   }
   r.dwgemm(dw, "proj0_dw");
   r.gemm(dx, true, false, EPI_STORE_BF16, 1, "proj0_dx");
+  r.flush();
   AttnBatch ab{}; ab.count = M;
   for (int i = 0; i < M; ++i) {
     AttnProblem& q = ab.p[i];
@@ -946,13 +980,14 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   r.dwgemm(dw, "qkv1_dw");
   r.ok(mmt_launch_colsum(cs, R, r.s), "qkv1_db");
   r.gemm(dx, true, false, EPI_STORE_F32, 1, "qkv1_dx");
+  r.flush();
+  d16_advance(c);
   for (int i = 0; i < M; ++i) {
     lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].mean = r.W<float>(a[i].mean1);
     lb.p[i].rstd = r.W<float>(a[i].rstd1); lb.p[i].dy = r.W<float>(p.dln[i]); lb.p[i].dx = r.W<float>(p.dres[i]);
     lb.p[i].dgamma = grads + x[i].ln1w; lb.p[i].dbeta = grads + x[i].ln1b;
     set_dres16_consumer(c, r, lb.p[i], i, l - 1, grads);
   }
-  r.join();
   r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln1_bwd");
   return r.rc;
 }
