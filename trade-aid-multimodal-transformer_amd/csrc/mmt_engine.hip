@@ -506,8 +506,9 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   r.wpk = wpk;
   // keep bits of layer ll's self- and cross-attention dropout, one side-stream launch each (the
   // mask kernel reads nothing the main stream writes: a fork orders it after the previous step)
+  hipStream_t ss = r.s;
   auto gen_masks = [&](int ll) {
-    hipStream_t ss = r.side();
+    if (ll <= 1) ss = r.side();  // layer 0: one fork; layers 1..L-1: one fork for all
     const LM* xl = &c->lm[(size_t)ll * M];
     const ActLM* al = &p.act[(size_t)ll * M];
     AttnBatch mb{}; mb.count = M;
@@ -545,7 +546,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
     const LM* x = &c->lm[(size_t)l * M];
     const ActLM* a = &p.act[(size_t)l * M];
     // attention dropout keep bits: layer 0's made on the side stream while the first LayerNorm and
-    // Q/K/V GEMMs run; every later layer's while the previous layer computes (gen_masks below)
+    // Q/K/V GEMMs run, all later layers' while layer 0 computes (two forks, two joins per forward)
     if (r.drop && l == 0) gen_masks(0);
     LnBatch lb{}; lb.count = M;
     for (int i = 0; i < M; ++i) {
@@ -573,9 +574,10 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       r.set_drop(q, l, i, DS_SA_PROB);
       if (r.drop) q.dmask[0] = r.W<uint32_t>(a[i].dm);
     }
-    if (r.drop) {
-      r.join();  // this layer's keep bits (SA and CA) are in
-      if (l + 1 < c->L) gen_masks(l + 1);
+    if (r.drop && l <= 1) {
+      r.join();  // this layer's keep bits (SA and CA) are in (layer 1: every later layer's too)
+      if (l == 0)
+        for (int ll = 1; ll < c->L; ++ll) gen_masks(ll);
     }
     r.probe_begin("attn_fwd");
     r.ok(mmt_launch_attn_fwd(ab, B, T, H, hs, scale, r.s), "attn_fwd");
