@@ -113,6 +113,10 @@ __device__ __forceinline__ bf16x8 tr_rows(const bf16_t* img, int ld, int kb, int
   return join4(lds_tr16(img + kr * ld + col), lds_tr16(img + (kr + 4) * ld + col));
 }
 
+// rows per backward block (a multiple of 256)
+#ifndef QKV2_BWD_ROWS
+#define QKV2_BWD_ROWS 2048
+#endif
 template <int HS>
 __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
   constexpr int HH = HS / 2;
@@ -122,9 +126,9 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
   constexpr int KSD = (HS + 15) / 16;             // k-steps over o for dh1
   const Qkv2Problem& P = batch.p[blockIdx.z];
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int nblk = gridDim.x / ((R + 255) / 256);
+  const int nblk = gridDim.x / ((R + QKV2_BWD_ROWS - 1) / QKV2_BWD_ROWS);
   const int blk = tile % nblk;
-  const int r0 = (tile / nblk) * 256;
+  const int rbase = (tile / nblk) * QKV2_BWD_ROWS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   __shared__ __attribute__((aligned(16))) bf16_t sd[256 * SDW];
@@ -136,6 +140,15 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
     const int i = q / SDW, o = q % SDW;
     w2t[q] = f2bf((i < HH && o < HS) ? w2[o * HH + i] : 0.f);
   }
+  // dW2 partials accumulate over QKV2_BWD_ROWS / 256 chunks: one atomic add per element per block
+  // (blocks of one blk all add into the same [HS][HH] table, so fewer blocks = less contention)
+  f32x16 dw[NOT];
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dw[ot][e] = 0.f;
+  for (int r0 = rbase; r0 < min(R, rbase + QKV2_BWD_ROWS); r0 += 256) {
+  if (r0 > rbase) __syncthreads();  // the previous chunk's LDS reads are done
   // dout chunk and h1 chunk, row per thread, zero padded
   {
     const int rr = r0 + tid;
@@ -188,11 +201,8 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
     }
   }
   // ---- dW2 partial over this wave's 64 rows: D[o][i] = sum_r dout[r][o] h1[r][i] ----
-  f32x16 dw[NOT];
 #pragma unroll
   for (int ot = 0; ot < NOT; ++ot) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) dw[ot][e] = 0.f;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int kb = w * 64 + 16 * s;
@@ -201,6 +211,7 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
       dw[ot] = mfma32(a, b, dw[ot]);
     }
   }
+  }  // chunks
   __syncthreads();
   float* red = reinterpret_cast<float*>(sd);  // reuse: [4 waves][NOT*32 o][32 i] floats
 #pragma unroll
@@ -223,7 +234,8 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
 template <int HS>
 static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_out, bool bwd, hipStream_t s) {
   if (bwd)
-    hipLaunchKernelGGL(qkv2_bwd_mfma<HS>, dim3((R + 255) / 256 * nblk, 1, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
+    hipLaunchKernelGGL(qkv2_bwd_mfma<HS>, dim3((R + QKV2_BWD_ROWS - 1) / QKV2_BWD_ROWS * nblk, 1, b.count), dim3(256), 0, s,
+                       b, R, ld_h1, ld_out);
   else
     hipLaunchKernelGGL(qkv2_fwd_mfma<HS>, dim3((R + 127) / 128 * nblk, 1, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
 }
