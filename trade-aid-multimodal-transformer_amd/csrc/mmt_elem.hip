@@ -237,9 +237,15 @@ __host__ __device__ __forceinline__ int emb_slab(int V, int C) {
   while (p > 4 && (C % p != 0 || (int64_t)V * p > EMB_LDS_FLOATS)) p >>= 1;
   return p;
 }
+#ifndef EMB_CHUNK_MUL
+#define EMB_CHUNK_MUL 4
+#endif
+#ifndef EMB_U
+#define EMB_U 4
+#endif
 __host__ __device__ __forceinline__ int emb_chunk(int V, int R) {
   int ch = 256;
-  while (ch < 4 * V && ch < R) ch <<= 1;
+  while (ch < EMB_CHUNK_MUL * V && ch < R) ch <<= 1;
   return ch;
 }
 __global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int R, int C) {
@@ -262,7 +268,7 @@ __global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int 
   const int s4 = slab >> 2;            // f32x4 per row slab
   const int rows_per_pass = 256 / s4;  // rows covered by the block per pass
   const int lr = threadIdx.x / s4, c4 = threadIdx.x % s4;
-  constexpr int U = 4;  // passes in flight per thread (idx and dx loads issued together)
+  constexpr int U = EMB_U;  // passes in flight per thread (idx and dx loads issued together)
   for (int rb = r0 + lr; lr < rows_per_pass && rb < r1; rb += U * rows_per_pass) {
     int64_t id[U];
     f32x4 d[U];
