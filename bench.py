@@ -189,7 +189,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        # the probe's HIP events are recorded on one step in four (each event record is a queue
+        # barrier, ~0.06 ms/step when every launch is bracketed)
+        L_.mmt_probe_enable(model._ctx, 1 if i % 4 == 0 else 0)
         losses = step()
     torch.cuda.synchronize()
     if world > 1:

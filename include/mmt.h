@@ -112,6 +112,9 @@ int mmt_eval_direction(mmt_ctx* ctx, void* stream, int32_t batch, int32_t T, int
  * the recorded events and returns the summed device time and the number of launches. */
 int mmt_probe_set(mmt_ctx* ctx, const char* label);
 int mmt_probe_read(mmt_ctx* ctx, double* total_ms, int64_t* launches);
+/* Pause (on = 0) / resume (on != 0) the probe's recording without clearing it: the bench samples
+ * one step in four, so the probe's event records stay out of the other steps. */
+int mmt_probe_enable(mmt_ctx* ctx, int32_t on);
 
 /* ---- device-resident batcher: get_batch (training_utils.py:333-384) on HBM token streams ---- */
 /* in-place random walk of one int32 training stream (data_utils.py:342-351 as reached through

@@ -117,6 +117,7 @@ struct mmt_ctx {
   const int64_t* last_idx[MAXM] = {};  // forward token ids, read by the embedding backward stage
   std::string err;
   std::string probe_label;
+  bool probe_on = true;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> probe_events;
   int ldv[MAXM], ldvh[MAXM];
   // backward side stream: the weight-gradient GEMMs (nothing in the data-gradient chain reads
@@ -434,7 +435,7 @@ struct Runner {
     return e == hipSuccess;
   }
   // live kernel timing (mmt_probe_set): HIP events on this stream around launches with a matching label
-  bool probing(const char* what) const { return !c->probe_label.empty() && c->probe_label == what; }
+  bool probing(const char* what) const { return c->probe_on && !c->probe_label.empty() && c->probe_label == what; }
   void probe_begin(const char* what) {
     if (!probing(what)) return;
     hipEvent_t a, b;
@@ -1229,6 +1230,11 @@ extern "C" int mmt_probe_set(mmt_ctx* c, const char* label) {
   return MMT_OK;
 }
 
+extern "C" int mmt_probe_enable(mmt_ctx* c, int32_t on) {
+  if (!c) return MMT_ERR_INVALID;
+  c->probe_on = on != 0;
+  return MMT_OK;
+}
 extern "C" int mmt_probe_read(mmt_ctx* c, double* total_ms, int64_t* launches) {
   if (!c) return MMT_ERR_INVALID;
   double tot = 0.0;

@@ -67,6 +67,7 @@ _SIGS = {
     "mmt_set_dropout_seed": (c_i32, [c_vp, ctypes.c_uint64]),
     "mmt_probe_set": (c_i32, [c_vp, c_cp]),
     "mmt_probe_read": (c_i32, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
+    "mmt_probe_enable": (c_i32, [c_vp, c_i32]),
     "mmt_batch_jitter":(c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64]),
     "mmt_batch_indices": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     "mmt_batch_gather": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), c_vp, c_i32, c_i32, ctypes.POINTER(c_vp),
