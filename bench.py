@@ -9,10 +9,16 @@ loop of reference main.py:641-650 on HBM-resident data: device get_batch (+-1 ra
 900k-row training streams, start indices, window gather), forward, loss, backward, gradient
 all-reduce (N > 1), fused AdamW.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|target|c3] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|target|c3|c4] [--no-cpu-baseline]
 
-Multi-GPU: launched by torch.distributed.run, one rank per GPU, RCCL ("nccl") all-reduce of the
-flat gradient; weak scaling (fixed batch per GPU).
+Multi-GPU: one rank per GPU, RCCL ("nccl") all-reduce of the flat gradient, weak scaling (fixed
+batch per GPU). Launched by torch.distributed.run (the driver's line), or, when `--gpus N > 1` is
+given without it, this process starts that launcher itself (launch_plan) before touching a GPU.
+
+Roofline: the engine times every launch matching the probe patterns (default: all weight-gradient
+GEMMs, attention forward / backward, ffn0, the ffn2 data gradient) with HIP events on the stream it
+runs on, one step in four, and reports each family's algorithmic flops / bytes per launch over
+that time; `roofline` is the family with the largest measured time per step, `kernels` all of them.
 """
 import argparse
 import ctypes
@@ -34,7 +40,12 @@ CONFIGS = {
     "c1": dict(M=4, C=256, H=8, L=6, T=256, B=64),
     "target": dict(M=4, C=512, H=8, L=6, T=512, B=32),
     "c3": dict(M=8, C=512, H=8, L=12, T=1024, B=16),
+    "c4": dict(M=4, C=1024, H=16, L=24, T=4096, B=4),
 }
+WORKLOADS = {"c1": "C1: 4-modality 1M-row synthetic, d256 L6 T256 (BASELINE configs[1])",
+             "target": "north-star target shape: 4-modality 1M-row synthetic, d512 L6 T512",
+             "c3": "C3: 8-modality selective cross-attention stress, d512 L12 T1024 (BASELINE configs[3], per GPU)",
+             "c4": "C4: 4-modality, d1024 L24 T4096 (BASELINE configs[4], per GPU)"}
 PEAK_TFLOPS = 2500.0  # MI355X bf16 dense MFMA (MI355X_MICROARCH.md; no sparsity)
 PEAK_HBM_GBS = 8000.0  # HBM3E
 METRIC = "training tokens/sec/GPU, 4-modality 1M-row synthetic, at 1/2/4/8 MI355X"
@@ -49,31 +60,12 @@ def train_flops_per_row(M, C, H, L, T, V, cross, a=0.5):
     return 6.0 * mac
 
 
-def dominant_kernel_flops(label, M, C, H, T, B, V):
-    """Algorithmic flops of one grouped launch of `label` (all modalities in one launch)."""
-    R = B * T
-    if label == "ffn0":
-        return M * 2.0 * R * C * (4 * C)
-    if label == "ffn0_dw":
-        return M * 2.0 * R * C * (4 * C)
-    if label == "ffn2":
-        return M * 2.0 * R * (4 * C) * C
-    if label == "qkv1":
-        return M * 2.0 * R * C * (1.5 * C)
-    raise ValueError(label)
-
-
-def dominant_kernel_bytes(label, M, C, H, T, B, V):
-    """Algorithmic HBM bytes of one grouped launch of `label`: each operand read once, each
-    output written once (bf16 activations / packed weights, fp32 bias)."""
-    R = B * T
-    if label == "ffn0":
-        return M * (R * C * 2 + 4 * C * C * 2 + 4 * C * 4 + R * 4 * C * 2)
-    if label == "ffn2":
-        return M * (R * 4 * C * 2 + 4 * C * C * 2 + C * 4 + 2 * R * C * 4 + R * C * 2)
-    if label == "qkv1":
-        return M * (R * C * 2 + int(1.5 * C) * C * 2 + int(1.5 * C) * 4 + R * int(1.5 * C) * 2)
-    raise ValueError(label)
+PROBES = ["*_dw", "attn_fwd", "attn_bwd", "ffn0", "ffn2_dx"]  # engine launch labels timed live
+PROBE_NAMES = {"*_dw": "weight-gradient GEMMs (all *_dw launches: split-K 256x256 / 128x128 gemm_kernel)",
+               "attn_fwd": "attn_fwd_kernel (causal self-attention forward)",
+               "attn_bwd": "attn_bwd_dq_kernel + attn_bwd_dkdv1_kernel (self-attention backward)",
+               "ffn0": "gemm_kernel ffn0 (X W0^T + b, ReLU, bf16 out)",
+               "ffn2_dx": "gemm_kernel ffn2 data gradient (dY W2, ReLU' epilogue, bias-grad column sums)"}
 
 
 def pmc_traffic(config, label):
@@ -89,35 +81,92 @@ def pmc_traffic(config, label):
         return None
 
 
+def roofline_entry(label, ms, n, flops, nbytes, sampled_steps, config):
+    """Roofline of one probed launch family: algorithmic flops / bytes per launch (reported by the
+    engine for each launch) over the live HIP-event launch time; the binding roof at the family's
+    arithmetic intensity (ridge = 2500 TFLOP/s / 8 TB/s = 312.5 flop/B)."""
+    sec = ms * 1e-3 / n
+    fl, by = flops / n, nbytes / n
+    if fl / by >= PEAK_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9):
+        r = {"bound": "mfma", "achieved": round(fl / sec / 1e12, 1), "peak": PEAK_TFLOPS, "unit": "TFLOP/s"}
+    else:
+        r = {"bound": "hbm", "achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
+    r["frac"] = round(r["achieved"] / r["peak"], 4)
+    r.update({"traffic": pmc_traffic(config, label), "kernel": PROBE_NAMES.get(label, label), "label": label,
+              "launches_per_step": round(n / sampled_steps, 2), "ms_per_step": round(ms / sampled_steps, 4),
+              "avg_launch_us": round(sec * 1e6, 2), "flops_per_launch": fl, "algorithmic_bytes_per_launch": by,
+              "tflops": round(fl / sec / 1e12, 1), "gbs": round(by / sec / 1e9, 1),
+              "mfma_frac": round(fl / sec / 1e12 / PEAK_TFLOPS, 4)})
+    return r
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg, data, seconds):
-    """The CPU oracle (per-head eager fp32 restatement of the reference structure) on the host
-    cores, a bounded sample of the same workload: C1 shapes at a small batch, fwd+bwd+AdamW."""
+    """The reference's CPU training loop restated by the oracle (oracle/mmt_oracle.py: eager fp32,
+    per-head modules exactly as the reference structures them; get_batch with the reference's
+    per-step list walk, list->tensor conversion and window stack), on the host cores:
+      * model step: C1 at the bench's batch (64), fwd + bwd + AdamW, timed over whole steps;
+      * full loop: that step + one reference get_batch('train', 1) over the 1M-row, 4-modality
+        training lists (report both)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import random
     import mmt_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
     torch.set_num_threads(threads)
     V = data["vocab_sizes"]
     ocfg = O.OracleConfig(cfg["C"], cfg["H"], cfg["L"], cfg["T"], V, [p[8] for p in data["params"]])
     g = torch.Generator().manual_seed(0)
     sd = O.init_params(ocfg, g)
-    B = 2
-    T = cfg["T"]
-    idx = [torch.randint(0, v, (B, T), generator=g) for v in V]
-    tgt = [torch.randint(0, v, (B, T), generator=g) for v in V]
+    B, T = cfg["B"], cfg["T"]
+    # the batcher's share: one reference get_batch (Python-loop walk of the whole training lists)
+    train_lists = [list(map(int, t)) for t in data["train"]]
+    t0 = time.perf_counter()
+    xb, yb = O.get_batch(train_lists, data["val"], [p[2] for p in data["params"]], V, T, B, "train", 1,
+                         data["file_lengths"], data["is_percents"], generator=g, rng=random.Random(0))
+    t_batch = time.perf_counter() - t0
     state = {}
     steps = 0
     t0 = time.perf_counter()
     while True:
-        _, _, grads = O.forward_backward(sd, ocfg, idx, tgt)
+        _, _, grads = O.forward_backward(sd, ocfg, xb, yb)
         steps += 1
         O.adamw_step(sd, grads, state, steps, lr=3e-4)
         if time.perf_counter() - t0 > seconds:
             break
-    dt = time.perf_counter() - t0
-    toks = steps * B * T * len(V)
-    return {"value": toks / dt, "unit": "tokens/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/mmt_oracle.py eager fp32 per-head restatement, C1 shapes at batch {B}, "
-                      f"{steps} fwd+bwd+AdamW steps in {dt:.1f}s on {threads} threads"}
+    t_step = (time.perf_counter() - t0) / steps
+    toks = B * T * len(V)
+    return {"value": round(toks / t_step, 1), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model(),
+            "full_loop_value": round(toks / (t_step + t_batch), 1),
+            "step_s": round(t_step, 3), "get_batch_s": round(t_batch, 3),
+            "sample": f"oracle/mmt_oracle.py eager fp32 per-head restatement of the reference, C1 at batch {B}: "
+                      f"{steps} fwd+bwd+AdamW steps ({t_step:.2f} s/step) on {threads} threads; full loop adds one "
+                      f"reference get_batch('train', 1) over the {len(train_lists[0])}-row x {len(V)} training lists "
+                      f"({t_batch:.2f} s)"}
+
+
+def launch_plan(n, argv, port):
+    """Command the parent runs when `--gpus N > 1` is asked without a torch.distributed launcher:
+    one rank per GPU (the driver's own launch line), started before this process touches a GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
 
 
 def main():
@@ -129,13 +178,22 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--dropout", type=float, default=0.1,
                     help="dropout p; SURVEY.md §8d: 0.1 for throughput runs (0.0 only for parity runs)")
-    ap.add_argument("--probe", default="ffn0", help="engine launch label timed live for the roofline line")
+    ap.add_argument("--probe", default=",".join(PROBES),
+                    help="comma-separated engine launch-label patterns timed live (roofline: the dominant one)")
     ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM pipeline variant (mmt_gemm_set_variant)")
     ap.add_argument("--bucket-mb", type=int, default=32, help="DP gradient all-reduce bucket size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--exact-steps", type=int, default=5,
+                    help="steps timed with the bit-exact host get_batch (reference RNG streams) after the main run")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one rank per GPU, launched before this process makes any GPU call; exit with its status
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        return subprocess.call(launch_plan(args.gpus, sys.argv[1:], _free_port()), env=env)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -143,6 +201,7 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus == world, (dist.get_world_size(), args.gpus, world)
 
     import config_utils
     import mmt_data
@@ -184,15 +243,19 @@ def main():
         losses = step()
     torch.cuda.synchronize()
     L_ = ML.lib()
-    L_.mmt_probe_set(model._ctx, args.probe.encode())
+    probes = [p for p in args.probe.split(",") if p]
+    L_.mmt_probe_set(model._ctx, ",".join(probes).encode())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    sampled = 0
     for i in range(args.steps):
-        # the probe's HIP events are recorded on one step in four (each event record is a queue
+        # the probes' HIP events are recorded on one step in four (each event record is a queue
         # barrier, ~0.06 ms/step when every launch is bracketed)
-        L_.mmt_probe_enable(model._ctx, 1 if i % 4 == 0 else 0)
+        on = i % 4 == 0
+        sampled += on
+        L_.mmt_probe_enable(model._ctx, 1 if on else 0)
         losses = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -203,37 +266,51 @@ def main():
         tt = torch.tensor([dt], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    probe_ms = ctypes.c_double(0)
-    probe_n = ctypes.c_int64(0)
-    L_.mmt_probe_read(model._ctx, ctypes.byref(probe_ms), ctypes.byref(probe_n))
+    kernels = []
+    for pi, label in enumerate(probes):
+        ms, n, fl, by = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_double(0), ctypes.c_double(0)
+        ML.check(L_.mmt_probe_read_at(model._ctx, pi, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl),
+                                      ctypes.byref(by)), model._ctx, "mmt_probe_read_at")
+        if n.value > 0 and by.value > 0:
+            kernels.append(roofline_entry(label, ms.value, n.value, fl.value, by.value, max(1, sampled), args.config))
     L_.mmt_probe_set(model._ctx, None)
     final_loss = float(sum(l.item() for l in losses))
+    nonfinite = int(model.nonfinite_loss_mask(sticky=True).item())
 
     tokens = world * B * T * M * args.steps
     value = tokens / dt
     flops_row = train_flops_per_row(M, C, H, L, T, V, [p[8] for p in data["params"]])
     achieved_step_tflops = flops_row * B * T * args.steps / dt / 1e12  # per GPU
-    roof = None
-    if probe_n.value > 0:
-        per_launch_ms = probe_ms.value / probe_n.value
-        fl = dominant_kernel_flops(args.probe, M, C, H, T, B, V)
-        by = dominant_kernel_bytes(args.probe, M, C, H, T, B, V)
-        sec = per_launch_ms * 1e-3
-        # the binding roof at this kernel's arithmetic intensity (ridge = 2500 TFLOP/s / 8 TB/s)
-        if fl / by >= PEAK_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9):
-            roof = {"bound": "mfma", "achieved": round(fl / sec / 1e12, 1), "peak": PEAK_TFLOPS, "unit": "TFLOP/s"}
-        else:
-            roof = {"bound": "hbm", "achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
-        roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-        roof.update({"traffic": pmc_traffic(args.config, args.probe), "kernel": args.probe, "launches": probe_n.value,
-                     "avg_launch_us": round(per_launch_ms * 1e3, 2), "flops_per_launch": fl,
-                     "algorithmic_bytes_per_launch": by, "tflops": round(fl / sec / 1e12, 1),
-                     "gbs": round(by / sec / 1e9, 1)})
+    # the roofline line prices the DOMINANT probed family by measured time per step
+    roof = max(kernels, key=lambda k: k["ms_per_step"]) if kernels else None
+
+    exact = None
+    if args.exact_steps > 0 and world == 1:
+        # the same loop fed by the bit-exact host get_batch (reference RNG streams, pinned-buffer copies)
+        import random
+        mmt_data.install(TU, data, model)
+        config_utils._config_cache.update({"device": str(dev)})
+        TU.use_device_batcher = False
+        random.seed(0)
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(args.exact_steps):
+            xb, yb = TU.get_batch("train", 1)
+            _, ls = model(xb, yb)
+            opt.zero_grad(set_to_none=True)
+            sum(ls).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        te = time.perf_counter() - te
+        TU.use_device_batcher = True
+        exact = {"tokens_per_s": round(B * T * M * args.exact_steps / te, 1), "ms_per_step": round(te / args.exact_steps * 1e3, 2),
+                 "steps": args.exact_steps}
+
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": f"{args.config}: 4-modality 1M-row synthetic" if M == 4 else f"{args.config}: 8-modality",
+        "config": {"workload": WORKLOADS[args.config],
                    "model": "multimodal-transformer", "global_batch": B * world, "seq_len": T, "n_embd": C,
                    "n_head": H, "n_layer": L, "modalities": M, "vocab_sizes": V, "dropout": args.dropout,
                    "parallelism": f"dp{world}"},
@@ -242,7 +319,10 @@ def main():
         "step_mfma_frac": round(achieved_step_tflops / PEAK_TFLOPS, 4),
         "train_flops_per_row": flops_row,
         "final_loss": round(final_loss, 4),
+        "nonfinite_loss_flags": nonfinite,
         "roofline": roof,
+        "kernels": kernels,
+        "exact_batcher": exact,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -251,7 +331,8 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -80,6 +80,14 @@ int64_t mmt_workspace_bytes(mmt_ctx* ctx, int32_t batch);
 int mmt_forward(mmt_ctx* ctx, void* stream, int32_t batch, const int64_t* const* idx, const int64_t* const* tgt,
                 const float* params, float* const* logits, float* losses, void* workspace, int32_t training);
 
+/* failure detection (the reference's guard is the NaN check on eval losses,
+ * main.py:606): byte offset in the workspace (for this batch size) of two int32 bitmasks. The
+ * loss kernel sets bit i of both when modality i's mean CE is NaN or Inf; word 0 is cleared by
+ * every mmt_forward with targets (the last forward's flags), word 1 only by the caller (sticky
+ * since the caller last cleared it; zero it when the workspace is allocated). Read them when the
+ * host syncs anyway; no kernel ever traps. */
+int64_t mmt_loss_flag_offset(mmt_ctx* ctx, int32_t batch);
+
 /* dropout (model.py:57/69, 87/91, 107/116, 134/151, 171; nn.Dropout(p) in training mode only):
  * masks are a counter hash of (seed, layer, modality, site, row, column) regenerated in the
  * backward, so nothing is stored. Sets the seed of the NEXT training forward (and its backward);
@@ -87,7 +95,8 @@ int mmt_forward(mmt_ctx* ctx, void* stream, int32_t batch, const int64_t* const*
 int mmt_set_dropout_seed(mmt_ctx* ctx, uint64_t seed);
 
 /* backward of sum_i loss_grads[i] * loss_i through the last mmt_forward (same workspace/params).
- * grads: fp32 flat buffer (mmt_param_count elements) — OVERWRITTEN (zeroed then accumulated). */
+ * grads: fp32 flat buffer of the active prefix (mmt_param_active_count elements) — OVERWRITTEN
+ * (zeroed then accumulated); the never-used tail past it has no gradient (reference: .grad None). */
 int mmt_backward(mmt_ctx* ctx, void* stream, const float* loss_grads, const float* params, float* grads,
                  void* workspace);
 /* the same, split into stages (post-block, layer L-1 .. layer 0, embeddings) so a caller can
@@ -107,11 +116,19 @@ int mmt_eval_direction(mmt_ctx* ctx, void* stream, int32_t batch, int32_t T, int
                        const int64_t* xb, const int64_t* yb, const double* vocab, int32_t is_percent,
                        int32_t* wins_losses, double* certainty_sum);
 
-/* live kernel timing: HIP events on the caller's stream around every engine launch labelled
- * `label` (e.g. "ffn0", "ffn0_dw", "attn_fwd"); NULL or "" disables. mmt_probe_read waits for
- * the recorded events and returns the summed device time and the number of launches. */
+/* live kernel timing (no reference counterpart: the reference has no profiler):
+ * HIP events around every engine launch whose label matches one of the comma-separated
+ * patterns of `label` — an exact label ("ffn0", "attn_fwd", "attn_bwd", "qkv1_dw", ...), "*suffix"
+ * ("*_dw": every weight-gradient GEMM) or "prefix*" — recorded on the stream that launch runs on
+ * (the side stream for weight gradients). NULL or "" disables. Each recorded launch carries its
+ * algorithmic flops and HBM bytes (every operand read once, every output written once; attention
+ * causal-useful). mmt_probe_read_at waits for the events of pattern `pattern` (-1: all) and
+ * returns the summed device time, launch count, flops and bytes; mmt_probe_read = all patterns. */
 int mmt_probe_set(mmt_ctx* ctx, const char* label);
+int32_t mmt_probe_count(const mmt_ctx* ctx);
 int mmt_probe_read(mmt_ctx* ctx, double* total_ms, int64_t* launches);
+int mmt_probe_read_at(mmt_ctx* ctx, int32_t pattern, double* total_ms, int64_t* launches, double* flops,
+                      double* bytes);
 /* Pause (on = 0) / resume (on != 0) the probe's recording without clearing it: the bench samples
  * one step in four, so the probe's event records stay out of the other steps. */
 int mmt_probe_enable(mmt_ctx* ctx, int32_t on);

@@ -132,6 +132,11 @@ def run(cfg, data, log=print):
         if it % eval_interval == 0 or it == max_iters - 1:
             losses = estimate_loss(it, max_iters)
             now = datetime.now().strftime("%H:%M:%S")
+            bad = m.nonfinite_loss_mask(sticky=True, clear=True)  # device flag of the loss kernel
+            if bad is not None and int(bad.item()):
+                names = [str(p[9] or f"Modality {i + 1}") for i, p in enumerate(m.all_modality_params)
+                         if int(bad.item()) >> i & 1]
+                log(f"Warning: non-finite loss since the last evaluation in: {', '.join(names)} | {now}")
             history.append((it, losses["train"], losses["val"]))
             if not (np.isnan(losses["train"]) or np.isnan(losses["val"])):
                 log(f"\nLOSS METRICS: Step {it}/{max_iters} | Train: {losses['train']:.4f} | Val: {losses['val']:.4f} "

@@ -27,6 +27,7 @@ Reference anchors (paths relative to the reference repo root):
   training_utils.py:33-181 generate_batch_starting_indices -> batch_starting_indices
   training_utils.py:184-330 _get_direction_sign / calculate_evaluation_metrics -> eval_metrics
   data_utils.py:293-358 add_rand_to_data_points -> jitter_inplace
+  training_utils.py:333-384 get_batch -> get_batch (list walk + list->tensor + stack, as slow as the reference)
 """
 import math
 import numbers
@@ -408,6 +409,23 @@ def jitter_inplace(data, rand_size, vocab_size, rng=random):
         if mx < data[n] < vocab_size - mx:
             data[n] += rng.choice(choices)
     return data
+
+
+def get_batch(train_lists, val_tensors, rand_sizes, vocab_sizes, block_size, batch_size, split, is_training,
+              file_lengths, is_percents, generator=None, rng=random):
+    """training_utils.py:333-384 as the reference runs it, including its per-step costs: the
+    in-place walk of every training list (add_rand_to_data_points through has_header), the
+    conversion of each whole training list to a tensor, the start indices and the window stack."""
+    if is_training == 1:
+        for r, rs in enumerate(rand_sizes):
+            if rs is not None:
+                jitter_inplace(train_lists[r], rs, vocab_sizes[r], rng)
+    tensors = [torch.tensor(t, dtype=torch.long) for t in train_lists]
+    data = tensors if split == "train" else val_tensors
+    ix = batch_starting_indices(len(data[0]), block_size, batch_size, split, file_lengths, is_percents, generator)
+    xb = [torch.stack([d[i:i + block_size] for i in ix]) for d in data]
+    yb = [torch.stack([d[i + 1:i + block_size + 1] for i in ix]) for d in data]
+    return xb, yb
 
 
 def direction_sign(cur, prev, is_pct):

@@ -18,7 +18,20 @@ and params after 1 and 3 AdamW steps (lr=1e-3, torch defaults) on the same batch
 Plus: eval-metric fixtures (calculate_evaluation_metrics) and batch-index fixtures
 (generate_batch_starting_indices) with a seeded torch generator.
 
-Usage:  python tests/golden/gen_golden.py
+Scale fixtures (model-level parity at the BASELINE configs), parameters NOT stored
+(tests/golden_io.recipe_state_dict rebuilds them from the key list and a seed):
+  f_c1     C1 dims: C=256 H=8 L=6 T=256 M=4 V=[900,13,144,5] cross=[T,F,F,F] B=2
+  f_m8     8 modalities (C3's grouping): C=128 H=2 (hs 64) L=2 T=128 V=[900,13,144,5]x2
+           cross=[T,T,F,F,T,T,F,F] B=2 (4 query modalities x 7 KV streams)
+  stored: losses, logits of the last 8 positions, per-tensor gradient L2 norms, sampled gradient
+  entries (every tensor's first and last element + 2048 uniform draws over the concatenation), and
+  the losses after one AdamW step (lr 1e-3) on the same batch.
+Loop fixture (get_batch / estimate_loss as main.py drives them, reference training_utils.py):
+  f_loop   f_small's model + a 3-file synthetic dataset, seeded Python `random` and torch: two
+           get_batch('train', 1), estimate_loss (eval_iters 2), one more get_batch('train', 1);
+           every batch, the estimate_loss result and its printed lines, the walked train sets.
+
+Usage:  python tests/golden/gen_golden.py [fixture names...]   (default: all)
 """
 import json
 import os
@@ -131,6 +144,161 @@ def gen_model_fixture(config_utils, name, cfg, seed=1234):
     print(name, "losses", out["losses"], "params", sum(v.numel() for k, v in sd0.items() if not k.endswith("tril")))
 
 
+SCALE = {
+    "f_c1": dict(n_embd=256, n_head=8, n_layer=6, block_size=256, V=[900, 13, 144, 5],
+                 cross=[True, False, False, False], B=2, param_seed=31),
+    "f_m8": dict(n_embd=128, n_head=2, n_layer=2, block_size=128, V=[900, 13, 144, 5, 900, 13, 144, 5],
+                 cross=[True, True, False, False, True, True, False, False], B=2, param_seed=37),
+}
+
+
+def gen_scale_fixture(config_utils, name, cfg, seed=4321):
+    import importlib
+    import torch
+    sys.path.insert(0, os.path.dirname(HERE))
+    from golden_io import recipe_state_dict
+    config_utils._config_cache = {
+        "n_embd": cfg["n_embd"], "n_head": cfg["n_head"], "n_layer": cfg["n_layer"],
+        "block_size": cfg["block_size"], "dropout": 0.0, "device": "cpu",
+        "batch_size": cfg["B"], "eval_iters": 1,
+    }
+    import model as ref_model
+    importlib.reload(ref_model)
+    torch.manual_seed(seed)
+    torch.set_num_threads(8)
+    M = len(cfg["V"])
+    m = ref_model.MultimodalTransformer(M, list(cfg["V"]), _params_list(cfg))
+    sd0 = m.state_dict()
+    keys = list(sd0.keys())
+    ks = [(k, list(v.shape)) for k, v in sd0.items() if not k.endswith("tril")]
+    rec = recipe_state_dict(ks, cfg["param_seed"])
+    full = dict(rec)
+    for k in keys:
+        if k.endswith("tril"):
+            full[k] = sd0[k]
+    m.load_state_dict(full, strict=True)
+    B, T = cfg["B"], cfg["block_size"]
+    g = torch.Generator().manual_seed(seed + 1)
+    idx = [torch.randint(0, v, (B, T), generator=g) for v in cfg["V"]]
+    tgt = [torch.randint(0, v, (B, T), generator=g) for v in cfg["V"]]
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    logits, losses = m(idx, tgt)
+    opt.zero_grad(set_to_none=True)
+    sum(losses).backward()
+    out = {"losses": np.array([l.item() for l in losses], dtype=np.float32)}
+    for i in range(M):
+        out[f"logits_tail.{i}"] = logits[i][:, -8:, :].detach().numpy()
+        out[f"idx.{i}"] = idx[i].numpy()
+        out[f"tgt.{i}"] = tgt[i].numpy()
+    names = [k for k, p in m.named_parameters() if p.grad is not None]
+    grads = {k: p.grad.detach().flatten() for k, p in m.named_parameters() if p.grad is not None}
+    out["grad_norm"] = np.array([grads[k].norm().item() for k in names], dtype=np.float64)
+    first = np.array([grads[k][0].item() for k in names], dtype=np.float32)
+    last = np.array([grads[k][-1].item() for k in names], dtype=np.float32)
+    out["grad_first"], out["grad_last"] = first, last
+    flat = torch.cat([grads[k] for k in names])
+    gs = torch.Generator().manual_seed(seed + 2)
+    pick = torch.randint(0, flat.numel(), (2048,), generator=gs)
+    out["sample_index"] = pick.numpy().astype(np.int64)
+    out["sample_value"] = flat[pick].numpy()
+    opt.step()
+    with torch.no_grad():
+        _, l1 = m(idx, tgt)
+    out["losses_after1"] = np.array([l.item() for l in l1], dtype=np.float32)
+    meta = dict(cfg)
+    meta["state_dict_keys"] = keys
+    meta["state_dict_shapes"] = {k: list(v.shape) for k, v in sd0.items()}
+    meta["grad_names"] = names
+    meta["grad_none"] = [k for k, p in m.named_parameters() if p.grad is None]
+    meta["seed"] = seed
+    out["meta_json"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, "losses", out["losses"], "after1", out["losses_after1"], "grad tensors", len(names))
+
+
+def gen_loop_fixture(config_utils, seed=11):
+    """get_batch + estimate_loss as main.py drives them (reference training_utils.py:333-520,
+    data_utils.py:293-358), on f_small's model and a 3-file dataset with numeric vocabularies."""
+    import contextlib
+    import importlib
+    import io
+    import torch
+    z = np.load(os.path.join(HERE, "f_small.npz"))
+    meta = json.loads(bytes(z["meta_json"]).decode())
+    B, T = 3, meta["block_size"]
+    config_utils._config_cache = {
+        "n_embd": meta["n_embd"], "n_head": meta["n_head"], "n_layer": meta["n_layer"],
+        "block_size": T, "dropout": 0.0, "device": "cpu", "batch_size": B, "eval_iters": 2,
+        "output_file_name": "", "project_file_path": "",
+    }
+    import model as ref_model
+    import training_utils as tu
+    importlib.reload(ref_model)
+    importlib.reload(tu)
+    torch.set_num_threads(1)
+    V = meta["V"]
+    M = len(V)
+    vocabs = [[round(0.5 * i - 3.0, 1) for i in range(v)] for v in V]  # numeric, sorted (main.py:276-281)
+    file_lengths = [300, 140, 260]
+    n = sum(file_lengths)
+    rs = np.random.RandomState(seed)
+    streams = [rs.randint(0, v, size=n) for v in V]
+    n_train = int(n * 0.8)
+    params = []
+    for i in range(M):
+        p = [None] * 12
+        p[2] = True        # has_header: drives the +-1 walk (reference quirk, training_utils.py:353)
+        p[3] = (i == 1)    # one percent modality (metric sign rule; is_percents skips file starts)
+        p[8] = meta["cross"][i]
+        p[9] = f"mod{i}"
+        params.append(p)
+    params[2][2] = None    # one modality without jitter
+    tu.all_train_sets = [list(map(int, s[:n_train])) for s in streams]
+    tu.all_val_sets = [torch.tensor(s[n_train:], dtype=torch.long) for s in streams]
+    tu.all_vocabularies = vocabs
+    tu.all_modality_params = params
+    tu.all_file_info = None
+    tu.file_lengths = file_lengths
+    tu.num_modalities = M
+    tu.is_percents = True
+    m = ref_model.MultimodalTransformer(M, V, params)
+    sd = {k[len("param."):]: torch.from_numpy(z[k].copy()) for k in z.files if k.startswith("param.")}
+    full = dict(sd)
+    for k in meta["state_dict_keys"]:
+        if k.endswith("tril"):
+            full[k] = torch.tril(torch.ones(T, T))
+    m.load_state_dict(full, strict=True)
+    tu.m = m
+    random.seed(seed)
+    torch.manual_seed(seed)
+    out = {}
+    for i in range(M):
+        out[f"train0.{i}"] = np.array(tu.all_train_sets[i])
+        out[f"val.{i}"] = tu.all_val_sets[i].numpy()
+    calls = []
+    for c in range(2):
+        xb, yb = tu.get_batch("train", 1)
+        calls.append(("train", xb, yb))
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        est = tu.estimate_loss(0, 10)
+    xb, yb = tu.get_batch("train", 1)
+    calls.append(("train", xb, yb))
+    for c, (_, xb, yb) in enumerate(calls):
+        for i in range(M):
+            out[f"x{c}.{i}"] = xb[i].numpy()
+            out[f"y{c}.{i}"] = yb[i].numpy()
+    for i in range(M):
+        out[f"train_end.{i}"] = np.array(tu.all_train_sets[i])
+    out["est"] = np.array([est["train"], est["val"]], dtype=np.float64)
+    printed = [ln for ln in buf.getvalue().splitlines() if not ln.startswith("Evaluation:")]
+    m_ = {"V": V, "B": B, "T": T, "file_lengths": file_lengths, "n_train": n_train, "seed": seed,
+          "vocabs": vocabs, "params": params, "printed": printed, "eval_iters": 2}
+    out["meta_json"] = np.frombuffer(json.dumps(m_).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "f_loop.npz"), **out)
+    print("loop est", est, "\n" + "\n".join(printed))
+
+
 def gen_metric_fixture(seed=77):
     """calculate_evaluation_metrics (reference training_utils.py:215-330)."""
     import torch
@@ -217,9 +385,23 @@ def gen_jitter_fixture(seed=5):
 
 
 if __name__ == "__main__":
+    want = set(sys.argv[1:])
     cu = _import_reference()
+
+    def on(name):
+        return not want or name in want
+
     for name, cfg in CONFIGS.items():
-        gen_model_fixture(cu, name, cfg)
-    gen_metric_fixture()
-    gen_index_fixture()
-    gen_jitter_fixture()
+        if on(name):
+            gen_model_fixture(cu, name, cfg)
+    for name, cfg in SCALE.items():
+        if on(name):
+            gen_scale_fixture(cu, name, cfg)
+    if on("f_loop"):
+        gen_loop_fixture(cu)
+    if on("eval_metrics"):
+        gen_metric_fixture()
+    if on("batch_indices"):
+        gen_index_fixture()
+    if on("jitter"):
+        gen_jitter_fixture()

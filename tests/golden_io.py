@@ -26,3 +26,38 @@ def model_fixture(name):
 
 
 MODEL_FIXTURES = ["f_demo", "f_small", "f_hs32", "f_m1", "f_tiny_v"]
+# BASELINE-config-sized fixtures: parameters are NOT stored (tens of MB); both the generator and
+# the tests rebuild them with recipe_state_dict from the key list + seed kept in the fixture
+SCALE_FIXTURES = ["f_c1", "f_m8"]
+
+
+def recipe_state_dict(keys_shapes, seed):
+    """Deterministic parameters for the scale fixtures, drawn key by key in state_dict order from
+    one seeded torch generator: Linear / Embedding weights and biases N(0, 0.02^2) (the reference
+    init, model.py:372-378, with non-zero biases so their paths are exercised), LayerNorm weights
+    1 + N(0, 0.1^2) and biases N(0, 0.05^2)."""
+    g = torch.Generator().manual_seed(int(seed))
+    out = {}
+    for k, shp in keys_shapes:
+        shp = tuple(int(s) for s in shp)
+        x = torch.randn(shp, generator=g, dtype=torch.float32)
+        is_ln = len(shp) == 1 and any(c.startswith("ln") or "norm" in c for c in k.split("."))
+        if is_ln and k.endswith(".weight"):
+            out[k] = 1.0 + 0.1 * x
+        elif is_ln:
+            out[k] = 0.05 * x
+        else:
+            out[k] = 0.02 * x
+    return out
+
+
+def scale_fixture(name):
+    """(z, meta, cfg, sd, idx, tgt) of a scale fixture, parameters rebuilt by the recipe."""
+    import mmt_oracle as O
+    z, meta = load(name)
+    cfg = O.OracleConfig(meta["n_embd"], meta["n_head"], meta["n_layer"], meta["block_size"], meta["V"], meta["cross"])
+    ks = [(k, meta["state_dict_shapes"][k]) for k in meta["state_dict_keys"] if not k.endswith("tril")]
+    sd = recipe_state_dict(ks, meta["param_seed"])
+    idx = [torch.from_numpy(z[f"idx.{i}"].copy()) for i in range(cfg.M)]
+    tgt = [torch.from_numpy(z[f"tgt.{i}"].copy()) for i in range(cfg.M)]
+    return z, meta, cfg, sd, idx, tgt

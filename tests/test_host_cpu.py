@@ -7,7 +7,7 @@ import pytest
 import torch
 
 import training_utils as TU
-from golden_io import load
+from golden_io import GOLDEN as GOLDEN_DIR, load
 
 
 def test_batch_indices_bit_identical_to_reference():
@@ -33,17 +33,42 @@ def test_batch_indices_validation(args, exc):
         TU.generate_batch_starting_indices(*args)
 
 
-@pytest.mark.parametrize("r", [1, 2, 3])
-def test_host_jitter_law(r):
-    V = 30
-    rng = np.random.default_rng(r)
-    x0 = rng.integers(0, V, size=300_000)
-    x = x0.copy()
-    TU.jitter_(x, r, V, np.random.default_rng(7))
-    d = x - x0
-    elig = (x0 > r) & (x0 < V - r)
-    assert np.all(d[~elig] == 0) and np.all(np.abs(d) <= r)
-    freq = np.bincount(d[elig] + r, minlength=2 * r + 1) / elig.sum()
-    np.testing.assert_allclose(freq, 1.0 / (2 * r + 1), atol=5e-3)
+def test_host_jitter_reproduces_reference_golden():
+    """The reference-held walk (tests/golden/jitter.npz: add_rand_to_data_points(data, True, 12)
+    after random.seed(5), reference data_utils.py:293-358) through the product's vectorised walk."""
+    import random
+    z = np.load(f"{GOLDEN_DIR}/jitter.npz")
+    random.seed(5)
+    a = z["before"].astype(np.int64).copy()
+    TU.jitter_exact_([a], [True], [12])
+    np.testing.assert_array_equal(a, z["after"])
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_host_jitter_bit_exact_with_python_loop(seed):
+    """Several streams with rand sizes {True, None, 2, 3} (edges: values at the walk's bounds, a
+    stream with no eligible element): same result and same Python `random` state afterwards as the
+    reference's per-element random.choice loop (restated by the oracle)."""
+    import random
+    import mmt_oracle as O
+    rng = np.random.default_rng(seed)
+    Vs = [12, 5, 40, 9, 3]
+    rs = [True, None, 2, 3, 1]
+    data = [rng.integers(0, V, size=2000 + 37 * i) for i, V in enumerate(Vs)]
+    random.seed(100 + seed)
+    st0 = random.getstate()
+    ref = [list(map(int, d)) for d in data]
+    for d, r, V in zip(ref, rs, Vs):
+        if r is not None:
+            O.jitter_inplace(d, r, V)
+    nxt = random.random()
+    random.setstate(st0)
+    got = [d.copy() for d in data]
+    TU.jitter_exact_(got, rs, Vs)
+    for g, r_ in zip(got, ref):
+        np.testing.assert_array_equal(g, np.array(r_))
+    assert random.random() == nxt
     with pytest.raises(ValueError):
-        TU.jitter_(x, 4, V, np.random.default_rng(0))
+        TU.jitter_exact_([got[0]], [4], [12])
+    with pytest.raises(ValueError):
+        TU.jitter_exact_([got[0]], [False], [12])  # has_header: false crashes in the reference too

@@ -120,3 +120,50 @@ def test_hash_dropout_mask_law():
     assert int(O.mask_hash(1, 2, 3)) == 1107639200
     assert int(O.mask_hash(0xFFFFFFFF, 0, 7)) == 352430166
     assert O.mask_hash([1, 2], 3, 4).dtype == np.uint32
+
+
+def _scale_compare(z, meta, logits, losses, grads, rel_tol, grad_tol, sample_tol):
+    """Compare a forward/backward against a scale fixture (no stored parameters)."""
+    M = len(meta["V"])
+    got = torch.stack([l.detach().float().cpu() for l in losses])
+    torch.testing.assert_close(got, torch.from_numpy(z["losses"]), rtol=rel_tol, atol=rel_tol)
+    for i in range(M):
+        ref = torch.from_numpy(z[f"logits_tail.{i}"])
+        lg = logits[i][:, -8:, :].detach().float().cpu()
+        assert ((lg - ref).norm() / ref.norm()).item() < 20 * rel_tol, i
+    names = meta["grad_names"]
+    norms = torch.tensor([grads[k].double().norm().item() for k in names])
+    ref_norms = torch.from_numpy(z["grad_norm"])
+    tot = ref_norms.norm().item()
+    err = (norms - ref_norms).abs()
+    bad = [(k, float(n), float(r)) for k, n, r, e in zip(names, norms, ref_norms, err)
+           if not (e <= grad_tol * r or e <= 2e-3 * tot)]
+    assert not bad, bad[:5]
+    flat = torch.cat([grads[k].flatten().float().cpu() for k in names])
+    s = flat[torch.from_numpy(z["sample_index"])]
+    ref = torch.from_numpy(z["sample_value"])
+    assert ((s - ref).norm() / ref.norm()).item() < sample_tol
+    first = torch.stack([grads[k].flatten()[0].float().cpu() for k in names])
+    last = torch.stack([grads[k].flatten()[-1].float().cpu() for k in names])
+    rf, rl = torch.from_numpy(z["grad_first"]), torch.from_numpy(z["grad_last"])
+    assert ((first - rf).norm() / rf.norm()).item() < sample_tol
+    assert ((last - rl).norm() / rl.norm()).item() < sample_tol
+
+
+@pytest.mark.parametrize("name", ["f_c1", "f_m8"])
+def test_scale_fixture_oracle_matches_reference(name):
+    """The oracle at the BASELINE config sizes (C1 dims, 6 layers; 8 modalities with 4 x 7 KV
+    streams) against the reference's own outputs (fp32 restatement tolerances), and one AdamW
+    step against the reference's re-evaluated losses."""
+    from golden_io import scale_fixture
+    torch.set_num_threads(8)
+    z, meta, cfg, sd, idx, tgt = scale_fixture(name)
+    assert sorted(O.param_shapes(cfg).keys()) == sorted(k for k in meta["state_dict_keys"] if not k.endswith("tril"))
+    logits, losses, grads = O.forward_backward(sd, cfg, idx, tgt)
+    assert sorted(k for k, g in grads.items() if g is None) == sorted(meta["grad_none"])
+    _scale_compare(z, meta, logits, losses, grads, rel_tol=1e-5, grad_tol=1e-4, sample_tol=1e-4)
+    params = {k: v.clone() for k, v in sd.items()}
+    O.adamw_step(params, grads, {}, 1, lr=1e-3)
+    _, l1 = O.forward(params, cfg, idx, tgt)
+    torch.testing.assert_close(torch.stack(l1), torch.from_numpy(z["losses_after1"]), rtol=1e-5, atol=1e-5)
+    torch.set_num_threads(1)

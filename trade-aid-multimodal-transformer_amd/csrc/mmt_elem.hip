@@ -415,7 +415,16 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(CeBatch batch, int R) {
   }
   if (lane == 0) part[wave] = contrib;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(P.loss, (part[0] + part[1] + part[2] + part[3]) / (float)R);
+  if (threadIdx.x == 0) {
+    const float blk = (part[0] + part[1] + part[2] + part[3]) / (float)R;
+    atomicAdd(P.loss, blk);
+    // failure detection: a non-finite loss raises this problem's bit in a device
+    // flag word the host reads when it syncs anyway (reference guard: main.py:606)
+    if (P.flag && !__builtin_isfinite(blk)) {
+      atomicOr(P.flag, P.bit);      // this forward's word
+      atomicOr(P.flag + 1, P.bit);  // sticky word (cleared only by the caller)
+    }
+  }
 }
 
 hipError_t mmt_launch_ce_fwd(const CeBatch& b, int R, hipStream_t s) {

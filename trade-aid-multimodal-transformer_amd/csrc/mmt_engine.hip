@@ -70,6 +70,7 @@ struct Plan {
   size_t total = 0;
   size_t pack = 0;
   size_t slab = 0, slab_bytes = 0;  // split-K slabs of the weight-gradient GEMMs
+  size_t flag = 0;                  // int32 non-finite-loss bitmask (bit i: modality i)
   std::vector<ActLM> act;  // [L*M]
   size_t xemb[MAXM];
   size_t lnf16[MAXM], meanf[MAXM], rstdf[MAXM], hh[MAXM], dlog[MAXM];
@@ -116,9 +117,16 @@ struct mmt_ctx {
   bool fwd_drop = false;
   const int64_t* last_idx[MAXM] = {};  // forward token ids, read by the embedding backward stage
   std::string err;
-  std::string probe_label;
+  // live kernel timing (mmt_probe_set): launch-label patterns and the HIP event pairs recorded
+  // around every matching launch, with that launch's algorithmic flops / HBM bytes
+  struct ProbeEv {
+    hipEvent_t a, b;
+    int pat;
+    double flops, bytes;
+  };
+  std::vector<std::string> probe_pats;
   bool probe_on = true;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> probe_events;
+  std::vector<ProbeEv> probe_events;
   int ldv[MAXM], ldvh[MAXM];
   // backward side stream: the weight-gradient GEMMs (nothing in the data-gradient chain reads
   // them) run there, overlapping the latency-bound data-gradient kernels; joined at stage ends
@@ -325,6 +333,7 @@ void make_plan(mmt_ctx* c, int B) {
   const size_t bhT = (size_t)B * H * c->T;
   const size_t mbytes = c->cfg.dropout > 0.f ? (size_t)mmt_attn_mask_dwords(B, H, c->T) * 4 : 0;
   p.pack = A((size_t)c->pack_elems * b2);
+  p.flag = A(256);
   p.act.resize((size_t)c->L * M);
   for (int i = 0; i < M; ++i) p.xemb[i] = A(R * C * f4);
   for (int l = 0; l < c->L; ++l)
@@ -405,6 +414,71 @@ GemmProblem gp_dw(const bf16_t* dY, int ldy, const bf16_t* X, int ldx, float* gr
   return g;
 }
 
+// live-probe pattern match: "label" exact, "*suffix" (e.g. "*_dw": every weight-gradient GEMM),
+// "prefix*"; returns the index of the first matching pattern or -1
+int probe_match(const mmt_ctx* c, const char* what) {
+  const size_t n = std::strlen(what);
+  for (size_t i = 0; i < c->probe_pats.size(); ++i) {
+    const std::string& p = c->probe_pats[i];
+    if (p.empty()) continue;
+    if (p[0] == '*') {
+      const size_t k = p.size() - 1;
+      if (n >= k && std::strcmp(what + n - k, p.c_str() + 1) == 0) return (int)i;
+    } else if (p.back() == '*') {
+      if (std::strncmp(what, p.c_str(), p.size() - 1) == 0) return (int)i;
+    } else if (p == what) {
+      return (int)i;
+    }
+  }
+  return -1;
+}
+
+// algorithmic cost of one grouped GEMM launch: 2MNK flops; every operand read once and every
+// output written once (bf16 activations / packed bf16 weights, fp32 bias / residual / outputs)
+void gemm_cost(const GemmBatch& b, int epi, double* fl, double* by) {
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& P = b.p[g];
+    const double M = P.M, N = P.N, K = P.K;
+    *fl += 2.0 * M * N * K;
+    double x = (M * K + N * K) * 2.0;
+    if (P.bias) x += N * 4.0;
+    const bool f32_out = epi == EPI_BIAS_RESID_F32 || epi == EPI_STORE_F32 || epi == EPI_ACC_F32;
+    x += M * N * (f32_out ? 4.0 : 2.0);
+    if (epi == EPI_BIAS_RESID_F32) x += M * N * 4.0 + (P.o16 ? M * N * 2.0 : 0.0);
+    if (epi == EPI_ACC_F32) x += M * N * 4.0;
+    if (epi == EPI_DTANH_BF16 || epi == EPI_DRELU_BF16) x += M * N * 2.0;
+    *by += x;
+  }
+}
+
+// weight gradient dW[M,N] += dY[K,M]^T X[K,N]: both operands read once, the fp32 gradient written once
+void wgrad_cost(const GemmBatch& b, double* fl, double* by) {
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& P = b.p[g];
+    const double M = P.M, N = P.N, K = P.K;
+    *fl += 2.0 * M * N * K;
+    *by += (M * K + N * K) * 2.0 + M * N * 4.0;
+  }
+}
+
+// causal attention, causal-useful count (a = 1/2): per (batch, head, KV stream)
+// forward 2 T^2 hs (QK^T and PV over the T(T+1)/2 kept scores), backward 2.5x that (S, dP, dV,
+// dQ, dK). Bytes: Q, K, V, O (+ per-stream outputs of a multi-stream problem), log-sum-exp and
+// dropout keep bits read / written once; backward adds dO, the row dot products and dQ, dK, dV.
+void attn_cost(const AttnBatch& ab, int B, int T, int H, int hs, bool bwd, bool drop, double* fl, double* by) {
+  const double C = (double)H * hs, rows = (double)B * T, bhT = (double)B * H * T;
+  const double mask = drop ? (double)mmt_attn_mask_dwords(B, H, T) * 4.0 : 0.0;
+  for (int g = 0; g < ab.count; ++g) {
+    const double ns = ab.p[g].nstreams;
+    const double f = 2.0 * (double)B * H * ns * (double)T * T * hs;
+    *fl += bwd ? 2.5 * f : f;
+    double x = rows * C * 2.0 * (2.0 + 2.0 * ns) + ns * (bhT * 4.0 + mask);  // q, o, k_j, v_j, lse_j, bits
+    if (ns > 1) x += ns * rows * C * 2.0;                                      // per-stream outputs o_j
+    if (bwd) x += rows * C * 2.0 * (2.0 + 2.0 * ns) + ns * bhT * 4.0;         // dO, dQ, dK_j, dV_j, dvec_j
+    *by += x;
+  }
+}
+
 // dropout sites (model.py:69 SA probabilities, :91 SA projection, :151 CA probabilities,
 // :116 CA projection, :171 FFN output); one hash key per (seed, layer, modality, site)
 enum DropSite { DS_SA_PROB = 0, DS_SA_PROJ = 1, DS_FFN = 2, DS_CA_PROB = 3, DS_CA_PROJ = 4 };
@@ -434,24 +508,37 @@ struct Runner {
     if (e != hipSuccess && rc == MMT_OK) rc = fail(c, MMT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
     return e == hipSuccess;
   }
-  // live kernel timing (mmt_probe_set): HIP events on this stream around launches with a matching label
-  bool probing(const char* what) const { return c->probe_on && !c->probe_label.empty() && c->probe_label == what; }
-  void probe_begin(const char* what) {
-    if (!probing(what)) return;
-    hipEvent_t a, b;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
-    hipEventRecord(a, s);
-    c->probe_events.push_back({a, b});
+  // live kernel timing (mmt_probe_set): HIP events around every launch whose label matches one of
+  // the probe patterns, recorded on the stream the launch goes to (the side stream for weight
+  // gradients), each tagged with the launch's algorithmic flops and bytes
+  int probe_begin(const char* what, hipStream_t st) {
+    if (!c->probe_on || c->probe_pats.empty()) return -1;
+    const int pat = probe_match(c, what);
+    if (pat < 0) return -1;
+    mmt_ctx::ProbeEv e{};
+    if (hipEventCreate(&e.a) != hipSuccess) return -1;
+    if (hipEventCreate(&e.b) != hipSuccess) { (void)hipEventDestroy(e.a); return -1; }
+    e.pat = pat;
+    hipEventRecord(e.a, st);
+    c->probe_events.push_back(e);
+    return (int)c->probe_events.size() - 1;
   }
-  void probe_end(const char* what) {
-    if (!probing(what) || c->probe_events.empty()) return;
-    hipEventRecord(c->probe_events.back().second, s);
+  void probe_end(int id, hipStream_t st, double flops, double bytes) {
+    if (id < 0) return;
+    mmt_ctx::ProbeEv& e = c->probe_events[id];
+    e.flops = flops;
+    e.bytes = bytes;
+    hipEventRecord(e.b, st);
   }
   void gemm(const GemmBatch& b, bool akc, bool bkc, int epi, int splits, const char* what) {
     if (rc != MMT_OK) return;
-    probe_begin(what);
+    const int id = probe_begin(what, s);
     ok(mmt_launch_gemm(b, akc, bkc, epi, splits, s), what);
-    probe_end(what);
+    if (id >= 0) {
+      double fl = 0, by = 0;
+      gemm_cost(b, epi, &fl, &by);
+      probe_end(id, s, fl, by);
+    }
   }
   // fork the side stream off the main one (everything enqueued on `s` so far happens first)
   hipStream_t side() {
@@ -477,18 +564,38 @@ struct Runner {
   void flush() {
     if (pend.empty() || rc != MMT_OK) { pend.clear(); return; }
     hipStream_t ss = side();
-    for (auto& q : pend) ok(mmt_launch_gemm_wgrad(q.first, W<float>(c->plan.slab), (int64_t)c->plan.slab_bytes, ss), q.second);
+    for (auto& q : pend) wgrad(q.first, q.second, ss);
     pend.clear();
   }
+  void wgrad(const GemmBatch& b, const char* what, hipStream_t st) {
+    const int id = probe_begin(what, st);
+    ok(mmt_launch_gemm_wgrad(b, W<float>(c->plan.slab), (int64_t)c->plan.slab_bytes, st), what);
+    if (id >= 0) {
+      double fl = 0, by = 0;
+      wgrad_cost(b, &fl, &by);
+      probe_end(id, st, fl, by);
+    }
+  }
+  // weight-gradient GEMMs share one split-K slab region: they run in launch order on ONE stream
+  // (the side stream when there is one), so no two of them ever write the slabs at once
   void dwgemm(const GemmBatch& b, const char* what) {
     if (rc != MMT_OK) return;
-    if (c->side && !probing(what)) {
+    if (c->side) {
       pend.emplace_back(b, what);
       return;
     }
-    probe_begin(what);
-    ok(mmt_launch_gemm_wgrad(b, W<float>(c->plan.slab), (int64_t)c->plan.slab_bytes, s), what);
-    probe_end(what);
+    wgrad(b, what, s);
+  }
+  void attn(const AttnBatch& ab, bool bwd, float scale, const char* what) {
+    if (rc != MMT_OK) return;
+    const int id = probe_begin(what, s);
+    if (bwd) ok(mmt_launch_attn_bwd(ab, B, c->T, c->H, c->hs, scale, s), what);
+    else ok(mmt_launch_attn_fwd(ab, B, c->T, c->H, c->hs, scale, s), what);
+    if (id >= 0) {
+      double fl = 0, by = 0;
+      attn_cost(ab, B, c->T, c->H, c->hs, bwd, drop, &fl, &by);
+      probe_end(id, s, fl, by);
+    }
   }
   template <class T> T* W(size_t off) { return at<T>(ws, off); }
   const float* P(int64_t off) { return params + off; }
@@ -580,9 +687,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       if (l == 0)
         for (int ll = 1; ll < c->L; ++ll) gen_masks(ll);
     }
-    r.probe_begin("attn_fwd");
-    r.ok(mmt_launch_attn_fwd(ab, B, T, H, hs, scale, r.s), "attn_fwd");
-    r.probe_end("attn_fwd");
+    r.attn(ab, false, scale, "attn_fwd");
     for (int i = 0; i < M; ++i) {
       g.p[i] = gp_fwd(r.W<bf16_t>(a[i].o), C, wpk, x[i].P0, R);
       g.p[i].bias = r.P(x[i].bp0); g.p[i].o16 = r.W<bf16_t>(a[i].p1); g.p[i].ldo16 = ldp;
@@ -656,9 +761,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         if (r.drop)
           for (int j = 0; j < M - 1; ++j) q.dmask[j] = r.W<uint32_t>(a[i].dmj[j]);
       }
-      r.probe_begin("ca_attn_fwd");
-      r.ok(mmt_launch_attn_fwd(cb, B, T, H, hs, scale, r.s), "ca_attn_fwd");
-      r.probe_end("ca_attn_fwd");
+      r.attn(cb, false, scale, "ca_attn_fwd");
       GemmBatch g0{}; g0.count = (int)cx.size();
       GemmBatch g2{}; g2.count = (int)cx.size();
       for (size_t u = 0; u < cx.size(); ++u) {
@@ -694,10 +797,12 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   r.gemm(h2, true, true, EPI_STORE_F32, 1, "head2");
   if (tgt && r.rc == MMT_OK) {
     r.ok(hipMemsetAsync(losses, 0, sizeof(float) * M, r.s), "memset losses");
+    r.ok(hipMemsetAsync(r.W<int>(p.flag), 0, sizeof(int), r.s), "memset flag");
     CeBatch cb{}; cb.count = M;
     for (int i = 0; i < M; ++i) {
       cb.p[i].logits = logits[i]; cb.p[i].tgt = tgt[i]; cb.p[i].dlogits = r.W<bf16_t>(p.dlog[i]);
       cb.p[i].loss = losses + i; cb.p[i].V = c->V[i]; cb.p[i].ld_d = c->ldv[i];
+      cb.p[i].flag = r.W<int>(p.flag); cb.p[i].bit = 1 << i;
     }
     r.ok(mmt_launch_ce_fwd(cb, R, r.s), "ce_fwd");
   }
@@ -745,7 +850,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   const bf16_t* wpk = r.W<bf16_t>(p.pack);
   if (stage == 0) {
     c->d16 = 0;
-    HIPCHK(c, hipMemsetAsync(grads, 0, sizeof(float) * c->nparams, r.s));
+    HIPCHK(c, hipMemsetAsync(grads, 0, sizeof(float) * c->nactive, r.s));  // the active prefix only
     const float invR = 1.0f / (float)R;
     GemmBatch dw{}; dw.count = M;
     GemmBatch dx{}; dx.count = M;
@@ -848,9 +953,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       if (r.drop)
         for (int j = 0; j < M - 1; ++j) q.dmask[j] = r.W<uint32_t>(a[i].dmj[j]);
     }
-    r.probe_begin("ca_attn_bwd");
-    r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "ca_attn_bwd");
-    r.probe_end("ca_attn_bwd");
+    r.attn(ab, true, scale, "ca_attn_bwd");
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
       const bf16_t* g = r.W<bf16_t>(p.gq[i]);
@@ -964,9 +1067,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     r.set_drop(q, l, i, DS_SA_PROB);
     if (r.drop) q.dmask[0] = r.W<uint32_t>(a[i].dm);
   }
-  r.probe_begin("attn_bwd");
-  r.ok(mmt_launch_attn_bwd(ab, B, T, H, hs, scale, r.s), "attn_bwd");
-  r.probe_end("attn_bwd");
+  r.attn(ab, true, scale, "attn_bwd");
   Qkv2Batch qb{}; qb.count = M;
   for (int i = 0; i < M; ++i) {
     qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].dout = r.W<bf16_t>(p.gqkv[i]);
@@ -1076,7 +1177,7 @@ void mmt_destroy(mmt_ctx* c) {
   if (!c) return;
   if (c->d_segs) (void)hipFree(c->d_segs);
   if (c->d_tasks) (void)hipFree(c->d_tasks);
-  for (auto& e : c->probe_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  for (auto& e : c->probe_events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
@@ -1100,6 +1201,12 @@ int mmt_tensor_info(const mmt_ctx* c, int32_t i, char* name, int32_t cap, int64_
   if (shape) { shape[0] = t.shape[0]; shape[1] = t.shape[1]; }
   if (kind) *kind = t.kind;
   return MMT_OK;
+}
+
+int64_t mmt_loss_flag_offset(mmt_ctx* c, int32_t batch) {
+  if (!c || batch < 1) return -1;
+  if (c->plan.B != batch) make_plan(c, batch);
+  return (int64_t)c->plan.flag;
 }
 
 int64_t mmt_workspace_bytes(mmt_ctx* c, int32_t batch) {
@@ -1220,13 +1327,26 @@ extern "C" int mmt_set_dropout_seed(mmt_ctx* c, uint64_t seed) {
   return MMT_OK;
 }
 
-// live per-kernel timing: HIP events around every launch labelled `label` (e.g. "ffn0", "ffn0_dw",
-// "attn_fwd"), on the caller's stream, so bench.py can price one kernel inside the timed region.
+// live per-kernel timing: HIP events around every launch whose label matches one of the
+// comma-separated patterns of `label` (e.g. "*_dw,attn_fwd,attn_bwd,ffn0"), recorded on the stream
+// the launch runs on, so bench.py can price kernels inside the timed region.
 extern "C" int mmt_probe_set(mmt_ctx* c, const char* label) {
   if (!c) return MMT_ERR_INVALID;
-  for (auto& e : c->probe_events) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  for (auto& e : c->probe_events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   c->probe_events.clear();
-  c->probe_label = label ? label : "";
+  c->probe_pats.clear();
+  if (label) {
+    std::string cur;
+    for (const char* q = label;; ++q) {
+      if (*q == ',' || *q == 0) {
+        if (!cur.empty()) c->probe_pats.push_back(cur);
+        cur.clear();
+        if (!*q) break;
+      } else if (*q != ' ') {
+        cur += *q;
+      }
+    }
+  }
   return MMT_OK;
 }
 
@@ -1235,16 +1355,31 @@ extern "C" int mmt_probe_enable(mmt_ctx* c, int32_t on) {
   c->probe_on = on != 0;
   return MMT_OK;
 }
-extern "C" int mmt_probe_read(mmt_ctx* c, double* total_ms, int64_t* launches) {
+
+extern "C" int32_t mmt_probe_count(const mmt_ctx* c) { return c ? (int32_t)c->probe_pats.size() : 0; }
+
+extern "C" int mmt_probe_read_at(mmt_ctx* c, int32_t pat, double* total_ms, int64_t* launches, double* flops,
+                                 double* bytes) {
   if (!c) return MMT_ERR_INVALID;
-  double tot = 0.0;
+  double tot = 0.0, fl = 0.0, by = 0.0;
+  int64_t n = 0;
   for (auto& e : c->probe_events) {
+    if (pat >= 0 && e.pat != pat) continue;
     float ms = 0.f;
-    if (hipEventSynchronize(e.second) != hipSuccess) return fail(c, MMT_ERR_HIP, "probe event sync");
-    if (hipEventElapsedTime(&ms, e.first, e.second) != hipSuccess) return fail(c, MMT_ERR_HIP, "probe elapsed");
+    if (hipEventSynchronize(e.b) != hipSuccess) return fail(c, MMT_ERR_HIP, "probe event sync");
+    if (hipEventElapsedTime(&ms, e.a, e.b) != hipSuccess) return fail(c, MMT_ERR_HIP, "probe elapsed");
     tot += ms;
+    fl += e.flops;
+    by += e.bytes;
+    ++n;
   }
   if (total_ms) *total_ms = tot;
-  if (launches) *launches = (int64_t)c->probe_events.size();
+  if (launches) *launches = n;
+  if (flops) *flops = fl;
+  if (bytes) *bytes = by;
   return MMT_OK;
+}
+
+extern "C" int mmt_probe_read(mmt_ctx* c, double* total_ms, int64_t* launches) {
+  return mmt_probe_read_at(c, -1, total_ms, launches, nullptr, nullptr);
 }

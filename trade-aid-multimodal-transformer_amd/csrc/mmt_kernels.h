@@ -174,7 +174,8 @@ struct CeProblem {
   const int64_t* tgt;    // [R]
   bf16_t* dlogits;       // [R, ld_d] = softmax - onehot (pad columns zeroed)
   float* loss;           // scalar, atomic accumulate of mean
-  int V, ld_d;
+  int* flag;             // nullable: flag[0], flag[1] |= bit when this problem's loss is NaN / Inf (no trap)
+  int V, ld_d, bit;
 };
 struct CeBatch { CeProblem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_ce_fwd(const CeBatch& b, int R, hipStream_t s);

@@ -91,6 +91,8 @@ def enable_data_parallel(model, group=None, bucket_bytes=32 << 20, broadcast=Tru
     if broadcast and dist.get_world_size(group) > 1:
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast(model.flat_params.data, src=src, group=group)
+        if model.flat_unused is not None:
+            dist.broadcast(model.flat_unused.data, src=src, group=group)
     sync = GradSync(model.backward_stage_ranges(), group=group, bucket_bytes=bucket_bytes)
     model._grad_sync = sync
     return sync

@@ -56,6 +56,7 @@ _SIGS = {
     "mmt_tensor_info": (c_i32, [c_vp, c_i32, ctypes.c_char_p, c_i32, ctypes.POINTER(c_i64), ctypes.POINTER(c_i32),
                                 ctypes.POINTER(c_i64), ctypes.POINTER(c_i32)]),
     "mmt_workspace_bytes": (c_i64, [c_vp, c_i32]),
+    "mmt_loss_flag_offset": (c_i64, [c_vp, c_i32]),
     "mmt_forward": (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp,
                             ctypes.POINTER(c_vp), c_vp, c_vp, c_i32]),
     "mmt_backward": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -68,6 +69,9 @@ _SIGS = {
     "mmt_probe_set": (c_i32, [c_vp, c_cp]),
     "mmt_probe_read": (c_i32, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
     "mmt_probe_enable": (c_i32, [c_vp, c_i32]),
+    "mmt_probe_count": (c_i32, [c_vp]),
+    "mmt_probe_read_at": (c_i32, [c_vp, c_i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "mmt_batch_jitter":(c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64]),
     "mmt_batch_indices": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     "mmt_batch_gather": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), c_vp, c_i32, c_i32, ctypes.POINTER(c_vp),

@@ -2,10 +2,10 @@
 (reference main.py:464, 648-650).
 
 Semantics follow torch's AdamW defaults: betas (0.9, 0.999), eps 1e-8, weight_decay 0.01,
-decoupled decay, bias correction; parameters whose .grad is None are skipped entirely. For the
-model's flat parameter only the active prefix (`_mmt_active`) is updated: the tail holds
-parameters that never receive a gradient (a CrossAttention with no KV modality), which torch
-would skip because their .grad stays None.
+decoupled decay, bias correction; parameters whose .grad is None are skipped entirely (the
+model's `flat_unused`, the CrossAttention parameters that never get a gradient). The stock
+torch.optim.AdamW gives the same result on the model (tests/test_gpu_model.py); this one runs the
+update as one fused HIP kernel over the flat buffer.
 """
 import torch
 
@@ -42,7 +42,7 @@ class AdamW(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] += 1
-                n = getattr(p, "_mmt_active", p.numel())
+                n = p.numel()
                 rc = L.mmt_adamw_step(None, ML.stream_ptr(p.device), ML.ptr(p), ML.ptr(g), ML.ptr(st["exp_avg"]),
                                       ML.ptr(st["exp_avg_sq"]), n, st["step"], group["lr"], b1, b2, group["eps"],
                                       group["weight_decay"])

@@ -8,9 +8,13 @@ reference (model.py:355-402 of tsnuk/trade-AId-multimodal-transformer):
     sum(losses_list).backward()
 
 Differences that are by design:
-  * all parameters live in ONE flat fp32 `nn.Parameter` (`flat_params`); `state_dict()` /
-    `load_state_dict()` expose and accept exactly the reference's per-head keys (including
-    the `.tril` buffers, emitted as one shared tensor), so reference checkpoints round-trip;
+  * all parameters that receive gradients live in ONE flat fp32 `nn.Parameter` (`flat_params`);
+    the parameters of a CrossAttention with no KV modality (M == 1, reference model.py:198-200,
+    238), which never get a gradient, live in a second one (`flat_unused`) whose `.grad` stays
+    None, so the reference's stock `torch.optim.AdamW(m.parameters(), lr)` (main.py:464) skips
+    them exactly as it does in the reference. `state_dict()` / `load_state_dict()` expose and
+    accept exactly the reference's per-head keys (including the `.tril` buffers, emitted as one
+    shared tensor), so reference checkpoints round-trip;
   * compute runs in bf16 on MFMA with fp32 accumulation, fp32 master weights/residual stream;
   * forward/backward run only on a ROCm device (there is no CPU path: the CPU oracle lives in
     oracle/ and is test infrastructure only);
@@ -100,8 +104,11 @@ class MultimodalTransformer(nn.Module):
         self._tril_keys = self._make_tril_keys()
         flat = torch.zeros(n, dtype=torch.float32)
         self._init_flat(flat)
-        self.flat_params = nn.Parameter(flat)
-        self.flat_params._mmt_active = self._n_active  # AdamW updates only this prefix
+        na = self._n_active
+        self.flat_params = nn.Parameter(flat[:na].clone())
+        # never-used CrossAttention parameters (M == 1): their own Parameter, .grad stays None
+        self.flat_unused = nn.Parameter(flat[na:].clone()) if n > na else None
+        self._dropout_counter = 0
         self._ws = None
         self._ws_batch = -1
         self._ws_bytes = {}
@@ -136,11 +143,18 @@ class MultimodalTransformer(nn.Module):
             else:
                 v.zero_()
 
-    def _view(self, off, shp, base=None):
-        base = self.flat_params if base is None else base
+    def _view(self, off, shp, detach=False):
+        """View of one reference tensor: a slice of flat_params, or of flat_unused past the
+        active prefix."""
         n = 1
         for s in shp:
             n *= s
+        if off >= self._n_active:
+            base, off = self.flat_unused, off - self._n_active
+        else:
+            base = self.flat_params
+        if detach:
+            base = base.detach()
         return base[off:off + n].view(shp)
 
     def named_reference_tensors(self):
@@ -148,10 +162,21 @@ class MultimodalTransformer(nn.Module):
         for name, off, shp, _ in self._tensors:
             yield name, self._view(off, shp)
 
-    def _save_to_state_dict(self, destination, prefix, keep_vars):
-        base = self.flat_params if keep_vars else self.flat_params.detach()
+    def reference_grad_views(self):
+        """(reference key, gradient view) for every parameter; None for the never-used ones."""
+        g = self.flat_params.grad
         for name, off, shp, _ in self._tensors:
-            destination[prefix + name] = self._view(off, shp, base)
+            if off >= self._n_active or g is None:
+                yield name, None
+                continue
+            n = 1
+            for s in shp:
+                n *= s
+            yield name, g[off:off + n].view(shp)
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        for name, off, shp, _ in self._tensors:
+            destination[prefix + name] = self._view(off, shp, detach=not keep_vars)
         if self._tril_keys:
             T = self.block_size
             tril = torch.tril(torch.ones(T, T, device=self.flat_params.device))
@@ -173,7 +198,7 @@ class MultimodalTransformer(nn.Module):
                     error_msgs.append(f"size mismatch for {key}: copying a param with shape {tuple(src.shape)}, "
                                       f"the shape in current model is {tuple(shp)}.")
                     continue
-                self._view(off, shp).copy_(src)
+                self._view(off, shp, detach=True).copy_(src)
         T = self.block_size
         for k in self._tril_keys:
             key = prefix + k
@@ -198,6 +223,8 @@ class MultimodalTransformer(nn.Module):
             self._ws = None
             self._ws = torch.empty(self._ws_bytes[B], dtype=torch.uint8, device=device)
             self._ws_batch = B
+            off = ML.lib().mmt_loss_flag_offset(self._ctx, B)
+            self._ws[off:off + 8].zero_()  # non-finite-loss flags (last forward, sticky)
         return self._ws
 
     def _launch_forward(self, flat, idx, tgt, training):
@@ -210,16 +237,48 @@ class MultimodalTransformer(nn.Module):
         idx_arr = ML.ptr_array(idx)
         tgt_arr = ML.ptr_array(tgt) if tgt is not None else None
         if training:
-            # dropout masks of this step: a counter hash keyed by a seed drawn from torch's
-            # default generator (so torch.manual_seed makes runs repeatable, as with nn.Dropout)
-            self.last_dropout_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            self.last_dropout_seed = self._next_dropout_seed(dev)
             ML.check(L.mmt_set_dropout_seed(self._ctx, self.last_dropout_seed), self._ctx, "mmt_set_dropout_seed")
-        rc = L.mmt_forward(self._ctx, ML.stream_ptr(dev), B, idx_arr, tgt_arr, ML.ptr(flat), ML.ptr_array(logits),
-                           ML.ptr(losses), ML.ptr(ws), 1 if training else 0)
+        with torch.cuda.device(dev):
+            rc = L.mmt_forward(self._ctx, ML.stream_ptr(dev), B, idx_arr, tgt_arr, ML.ptr(flat), ML.ptr_array(logits),
+                               ML.ptr(losses), ML.ptr(ws), 1 if training else 0)
         ML.check(rc, self._ctx, "mmt_forward")
         self._gen += 1
         self._last = (flat, idx, tgt)
         return logits, losses
+
+    def _next_dropout_seed(self, dev):
+        """Seed of this training step's dropout masks. The reference's nn.Dropout on a ROCm device
+        draws from the device generator, never from torch's CPU generator (which get_batch's
+        torch.randint start indices consume): the seed is derived from the device generator's
+        seed and Philox offset, and the offset is advanced as a dropout launch would, so
+        torch.manual_seed makes runs repeatable and the CPU random stream stays the reference's."""
+        self._dropout_counter += 1
+        seed, off = 0, self._dropout_counter
+        try:
+            gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+            seed = int(gen.initial_seed())
+            off = int(gen.get_offset())
+            gen.set_offset(off + 4)
+        except (AttributeError, RuntimeError, IndexError):
+            pass
+        x = (seed * 0x9E3779B97F4A7C15 + off * 0xBF58476D1CE4E5B9 + self._dropout_counter) & (2 ** 64 - 1)
+        x ^= x >> 31
+        x = (x * 0x94D049BB133111EB) & (2 ** 64 - 1)
+        return int(x ^ (x >> 29)) & (2 ** 62 - 1)
+
+    def nonfinite_loss_mask(self, sticky=False, clear=False):
+        """Device int32 bitmask, bit i set when modality i's loss was NaN / Inf (set by the loss
+        kernel): of the last forward with targets, or (sticky=True) of every
+        forward since the sticky word was last cleared (clear=True clears it). A copy, no sync."""
+        if self._ws is None:
+            return None
+        off = ML.lib().mmt_loss_flag_offset(self._ctx, self._ws_batch) + (4 if sticky else 0)
+        w = self._ws[off:off + 4]
+        out = w.view(torch.int32).clone()
+        if clear:
+            w.zero_()
+        return out
 
     def backward_stage_ranges(self):
         """[(begin, end)] of the flat gradient finalised by each backward stage, in execution order
@@ -239,19 +298,20 @@ class MultimodalTransformer(nn.Module):
         g = g_losses.detach().to(dtype=torch.float32).contiguous()
         grad = torch.empty_like(flat)
         sync = self._grad_sync
-        if sync is None:
-            rc = L.mmt_backward(self._ctx, ML.stream_ptr(flat.device), ML.ptr(g), ML.ptr(flat), ML.ptr(grad),
-                                ML.ptr(self._ws))
-            ML.check(rc, self._ctx, "mmt_backward")
-            return grad
-        # data parallel (mmt_dist): stage by stage, each finished bucket all-reduced while the
-        # next stages compute
-        for s in range(L.mmt_backward_stage_count(self._ctx)):
-            rc = L.mmt_backward_stage(self._ctx, ML.stream_ptr(flat.device), s, ML.ptr(g), ML.ptr(flat),
-                                      ML.ptr(grad), ML.ptr(self._ws))
-            ML.check(rc, self._ctx, "mmt_backward_stage")
-            sync.stage_done(s, grad)
-        sync.finish()
+        with torch.cuda.device(flat.device):
+            if sync is None:
+                rc = L.mmt_backward(self._ctx, ML.stream_ptr(flat.device), ML.ptr(g), ML.ptr(flat), ML.ptr(grad),
+                                    ML.ptr(self._ws))
+                ML.check(rc, self._ctx, "mmt_backward")
+                return grad
+            # data parallel (mmt_dist): stage by stage, each finished bucket all-reduced while the
+            # next stages compute
+            for s in range(L.mmt_backward_stage_count(self._ctx)):
+                rc = L.mmt_backward_stage(self._ctx, ML.stream_ptr(flat.device), s, ML.ptr(g), ML.ptr(flat),
+                                          ML.ptr(grad), ML.ptr(self._ws))
+                ML.check(rc, self._ctx, "mmt_backward_stage")
+                sync.stage_done(s, grad)
+            sync.finish()
         return grad
 
     def forward(self, idx_list, targets_list=None):

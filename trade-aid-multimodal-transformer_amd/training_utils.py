@@ -8,8 +8,14 @@ lines and log lines. What changed underneath:
     vectorised searchsorted instead of a per-sample Python loop (training_utils.py:156-178);
   * get_batch keeps the reference's in-place +-1 random walk of the training set, driven by
     all_modality_params[r][2] (`has_header`, the reference quirk at training_utils.py:353; see
-    DESIGN.md), but jitters and slices with numpy over int64 arrays and hands the batch to the
-    GPU through pinned host buffers (non_blocking copies);
+    DESIGN.md). Two modes:
+      - exact (use_device_batcher = False, or MMT_EXACT_BATCHER=1): numpy over the host int64
+        streams, bit-exact with the reference including its consumption of Python's `random`
+        (jitter_exact_) and torch's CPU generator (start indices); the windows go to the GPU
+        through pinned host buffers (non_blocking copies);
+      - fast (default on a GPU): DeviceBatcher, the streams resident in HBM and the walk, the
+        start indices and the gather as HIP kernels driven by a counter hash: the same laws
+        (tested), not the same draws;
   * calculate_evaluation_metrics runs the per-sample argmax / direction / softmax-certainty loop
     (training_utils.py:259-304) as one HIP kernel per modality (mmt_eval_direction) with a single
     device->host copy, instead of B*V `.item()` syncs.
@@ -99,16 +105,76 @@ def _as_array(r):
     return arr
 
 
-def jitter_(arr, rand_size, vocab_size, rng):
-    """Vectorised add_rand_to_data_points: x += uniform choice of {0, +-1 .. +-r} where r < x < V - r."""
-    r = int(rand_size)
-    if r < 1 or r > 3:
-        raise ValueError("rand_size must be an integer between 1 and 3, or null.")
-    elig = (arr > r) & (arr < vocab_size - r)
-    choice = rng.integers(0, 2 * r + 1, size=arr.shape[0])
-    delta = np.where(choice == 0, 0, np.where(choice % 2 == 1, (choice + 1) // 2, -(choice // 2)))
-    arr += np.where(elig, delta, 0)
-    return arr
+_CHOICES = np.array([0, 1, -1, 2, -2, 3, -3], dtype=np.int64)  # rand_list of data_utils.py:342-345
+
+
+def _mt_from_python(state):
+    """numpy MT19937 positioned exactly where Python's `random` is (same key words and index:
+    CPython's Random is MT19937 and getrandbits(k <= 32) is one genrand_uint32() >> (32 - k))."""
+    bg = np.random.MT19937()
+    bg.state = {"bit_generator": "MT19937",
+                "state": {"key": np.asarray(state[1][:624], dtype=np.uint32), "pos": int(state[1][624])}}
+    return bg
+
+
+def jitter_exact_(arrs, rand_sizes, vocab_sizes, pyrandom=random):
+    """add_rand_to_data_points (reference data_utils.py:342-351) over several training streams in
+    the order get_batch calls it (training_utils.py:352-360), bit-exact with the reference's
+    Python loop AND its consumption of Python's global `random` stream, vectorised.
+
+    Reference: every element x with r < x < V - r (r = rand_size, read from the eligibility BEFORE
+    this pass: an element is visited once) gets x += random.choice(rand_list), rand_list =
+    [0, 1, -1, .., r, -r]. random.choice(seq) is seq[_randbelow(len(seq))] and _randbelow(n) draws
+    getrandbits(n.bit_length()) until the value is < n (CPython 3.x). So the eligible elements,
+    stream by stream, take the accepted values of one MT19937 sequence in order. This draws that
+    sequence with numpy's MT19937 from `random.getstate()`, stops exactly at the last draw the loop
+    would make, and writes the advanced state back into `random`."""
+    jobs = []
+    for arr, rs, V in zip(arrs, rand_sizes, vocab_sizes):
+        if rs is None:
+            continue
+        if not isinstance(rs, (int, np.integer)):
+            raise TypeError("rand_size must be an integer or null.")
+        r = int(rs)
+        if r < 1 or r > 3:
+            raise ValueError("rand_size must be an integer between 1 and 3, or null.")
+        if not isinstance(V, (int, np.integer)) or V <= 0:
+            raise TypeError("vocab_size must be a positive integer.")
+        elig = np.flatnonzero((arr > r) & (arr < int(V) - r))
+        jobs.append((arr, elig, 2 * r + 1))
+    need = sum(len(e) for _, e, _ in jobs)
+    if need == 0:
+        return
+    state = pyrandom.getstate()
+    bg = _mt_from_python(state)
+    # every job's n = 2r+1 has the same bit length only when the rand sizes agree; walk per job
+    for arr, elig, n in jobs:
+        m = len(elig)
+        if m == 0:
+            continue
+        k = int(n).bit_length()
+        got = []
+        have = 0
+        chunk = m  # each accepted value needs >= 1 draw
+        while have < m:
+            saved = bg.state
+            raw = bg.random_raw(chunk) >> np.uint64(32 - k)
+            acc = np.flatnonzero(raw < np.uint64(n))
+            if have + len(acc) >= m:
+                take = m - have
+                used = int(acc[take - 1]) + 1  # the loop stops right after the m-th accepted draw
+                bg.state = saved
+                bg.random_raw(used)
+                got.append(raw[acc[:take]])
+                have = m
+            else:
+                got.append(raw[acc])
+                have += len(acc)
+                chunk = max(1024, (m - have) * 3 // 2)
+        vals = np.concatenate(got).astype(np.int64)
+        arr[elig] += _CHOICES[vals]
+    st = bg.state["state"]
+    pyrandom.setstate((state[0], tuple(int(x) for x in st["key"]) + (int(st["pos"]),), state[2]))
 
 
 _RING = 4
@@ -192,7 +258,7 @@ class DeviceBatcher:
 
 
 _device_batcher = [None]
-use_device_batcher = True
+use_device_batcher = os.environ.get("MMT_EXACT_BATCHER", "0") in ("", "0")
 
 
 def _get_device_batcher():
@@ -215,11 +281,10 @@ def get_batch(split, is_training):
     if use_device_batcher and dev != "cpu" and torch.cuda.is_available():
         return _get_device_batcher().next(split, is_training)
     if is_training == 1:
-        for r in range(num_modalities):
-            rs = all_modality_params[r][2]  # reference quirk: has_header, not randomness_size
-            if rs is not None:
-                rng = np.random.default_rng(random.getrandbits(64))
-                jitter_(_as_array(r), rs, len(all_vocabularies[r]), rng)
+        # reference quirk: the jitter size is all_modality_params[r][2] (has_header), not index 7
+        jitter_exact_([_as_array(r) for r in range(num_modalities)],
+                      [all_modality_params[r][2] for r in range(num_modalities)],
+                      [len(all_vocabularies[r]) for r in range(num_modalities)])
     if split == "train":
         data = [_as_array(r) for r in range(num_modalities)]
     else:
