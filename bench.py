@@ -251,9 +251,9 @@ def main():
     t0 = time.perf_counter()
     sampled = 0
     for i in range(args.steps):
-        # the probes' HIP events are recorded on one step in four (each event record is a queue
-        # barrier, ~0.06 ms/step when every launch is bracketed)
-        on = i % 4 == 0
+        # the probes' HIP events are recorded on one step in eight (each event record is a queue
+        # barrier; their pairs are made by mmt_probe_set, outside this loop)
+        on = i % 8 == 0
         sampled += on
         L_.mmt_probe_enable(model._ctx, 1 if on else 0)
         losses = step()

@@ -126,7 +126,8 @@ struct mmt_ctx {
   };
   std::vector<std::string> probe_pats;
   bool probe_on = true;
-  std::vector<ProbeEv> probe_events;
+  std::vector<ProbeEv> probe_events;  // recorded launches (events taken from probe_pool in order)
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> probe_pool;  // created by mmt_probe_set, not in the timed loop
   int ldv[MAXM], ldvh[MAXM];
   // backward side stream: the weight-gradient GEMMs (nothing in the data-gradient chain reads
   // them) run there, overlapping the latency-bound data-gradient kernels; joined at stage ends
@@ -416,7 +417,7 @@ GemmProblem gp_dw(const bf16_t* dY, int ldy, const bf16_t* X, int ldx, float* gr
 
 // live-probe pattern match: "label" exact, "*suffix" (e.g. "*_dw": every weight-gradient GEMM),
 // "prefix*"; returns the index of the first matching pattern or -1
-int probe_match(const mmt_ctx* c, const char* what) {
+int probe_match_one(const mmt_ctx* c, const char* what) {
   const size_t n = std::strlen(what);
   for (size_t i = 0; i < c->probe_pats.size(); ++i) {
     const std::string& p = c->probe_pats[i];
@@ -431,6 +432,17 @@ int probe_match(const mmt_ctx* c, const char* what) {
     }
   }
   return -1;
+}
+// a merged launch is labelled "a+b+...": it matches when any part does
+int probe_match(const mmt_ctx* c, const char* what) {
+  std::string w(what);
+  size_t b = 0;
+  while (true) {
+    const size_t e = w.find('+', b);
+    const int r = probe_match_one(c, w.substr(b, e == std::string::npos ? std::string::npos : e - b).c_str());
+    if (r >= 0 || e == std::string::npos) return r;
+    b = e + 1;
+  }
 }
 
 // algorithmic cost of one grouped GEMM launch: 2MNK flops; every operand read once and every
@@ -515,9 +527,10 @@ struct Runner {
     if (!c->probe_on || c->probe_pats.empty()) return -1;
     const int pat = probe_match(c, what);
     if (pat < 0) return -1;
+    if (c->probe_events.size() >= c->probe_pool.size()) return -1;  // pool exhausted: stop recording
     mmt_ctx::ProbeEv e{};
-    if (hipEventCreate(&e.a) != hipSuccess) return -1;
-    if (hipEventCreate(&e.b) != hipSuccess) { (void)hipEventDestroy(e.a); return -1; }
+    e.a = c->probe_pool[c->probe_events.size()].first;
+    e.b = c->probe_pool[c->probe_events.size()].second;
     e.pat = pat;
     hipEventRecord(e.a, st);
     c->probe_events.push_back(e);
@@ -563,8 +576,22 @@ struct Runner {
   std::vector<std::pair<GemmBatch, const char*>> pend;
   void flush() {
     if (pend.empty() || rc != MMT_OK) { pend.clear(); return; }
-    hipStream_t ss = side();
-    for (auto& q : pend) wgrad(q.first, q.second, ss);
+    hipStream_t ss = c->side ? side() : s;
+    // merge consecutive queued weight-gradient batches of the same tile kind into one launch (up
+    // to MMT_MAX_GROUP problems): more tiles per launch -> fewer K splits -> fewer partial bytes
+    std::vector<std::pair<GemmBatch, std::string>> merged;
+    for (auto& q : pend) {
+      if (!merged.empty()) {
+        GemmBatch& m = merged.back().first;
+        if (m.count + q.first.count <= MMT_MAX_GROUP && mmt_gemm_wgrad_big(m) == mmt_gemm_wgrad_big(q.first)) {
+          for (int g = 0; g < q.first.count; ++g) m.p[m.count++] = q.first.p[g];
+          merged.back().second += std::string("+") + q.second;
+          continue;
+        }
+      }
+      merged.emplace_back(q.first, q.second);
+    }
+    for (auto& q : merged) wgrad(q.first, q.second.c_str(), ss);
     pend.clear();
   }
   void wgrad(const GemmBatch& b, const char* what, hipStream_t st) {
@@ -577,14 +604,11 @@ struct Runner {
     }
   }
   // weight-gradient GEMMs share one split-K slab region: they run in launch order on ONE stream
-  // (the side stream when there is one), so no two of them ever write the slabs at once
+  // (the side stream when there is one), so no two of them ever write the slabs at once (a
+  // probed launch no longer jumps to the main stream: ADVICE r1)
   void dwgemm(const GemmBatch& b, const char* what) {
     if (rc != MMT_OK) return;
-    if (c->side) {
-      pend.emplace_back(b, what);
-      return;
-    }
-    wgrad(b, what, s);
+    pend.emplace_back(b, what);  // launched (merged) at the next flush(), on the side stream if any
   }
   void attn(const AttnBatch& ab, bool bwd, float scale, const char* what) {
     if (rc != MMT_OK) return;
@@ -1177,7 +1201,7 @@ void mmt_destroy(mmt_ctx* c) {
   if (!c) return;
   if (c->d_segs) (void)hipFree(c->d_segs);
   if (c->d_tasks) (void)hipFree(c->d_tasks);
-  for (auto& e : c->probe_events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+  for (auto& e : c->probe_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
@@ -1332,7 +1356,6 @@ extern "C" int mmt_set_dropout_seed(mmt_ctx* c, uint64_t seed) {
 // the launch runs on, so bench.py can price kernels inside the timed region.
 extern "C" int mmt_probe_set(mmt_ctx* c, const char* label) {
   if (!c) return MMT_ERR_INVALID;
-  for (auto& e : c->probe_events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   c->probe_events.clear();
   c->probe_pats.clear();
   if (label) {
@@ -1346,6 +1369,18 @@ extern "C" int mmt_probe_set(mmt_ctx* c, const char* label) {
         cur += *q;
       }
     }
+  }
+  // event pairs for the recorded launches, made here (event creation is a host call of tens of
+  // microseconds: inside the timed loop it starved the GPU); recording stops when they run out
+  static const size_t pool = [] {
+    const char* e = getenv("MMT_PROBE_EVENTS");
+    return (size_t)(e ? atoi(e) : 4096);
+  }();
+  while (!c->probe_pats.empty() && c->probe_pool.size() < pool) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) break;
+    if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); break; }
+    c->probe_pool.push_back({a, b});
   }
   return MMT_OK;
 }

@@ -387,6 +387,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
   // XCD-aware remap (bijective): blocks b and b+8 share an XCD; give each XCD a contiguous run
   // of tiles so neighbouring tiles (same A row panel) share that XCD's L2
   int tile = blockIdx.x;
+  const int split = blockIdx.y, nsplit = gridDim.y;
   {
     const int nwg = gridDim.x;
     const int x = tile % 8, q = nwg / 8, rr = nwg % 8;
@@ -395,10 +396,9 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
   if (tile >= ntiles) return;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * GBM, n0 = tn * GBN;
-  const int nsplit = gridDim.y;
   const int ksteps = (K + BK - 1) / BK;
   const int kper = (ksteps + nsplit - 1) / nsplit;
-  const int ks0 = blockIdx.y * kper;
+  const int ks0 = split * kper;
   const int ks1 = min(ksteps, ks0 + kper);
   if (EPI == EPI_ATOMIC_F32 && ks0 >= ks1) return;  // nothing to add (a slab split still writes its zeros)
 
@@ -406,7 +406,9 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
   // the stage ring during the K loop, the fp32 output tile (EPI_ROWS x (GBN + 4)) in the epilogue
   constexpr int EPI_ROWS = GBM == 128 ? 128 : 64;
   constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
-  __shared__ __attribute__((aligned(1024))) char lds[RING > CTILE ? RING : CTILE];
+  constexpr int LDS_MAIN = RING > CTILE ? RING : CTILE;
+  // (+16 B: the split-K last-arriver's role word, clear of the ring and the epilogue tile)
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN + (EPI == EPI_TREE_F32 ? 16 : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -484,7 +486,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
   float alpha = P.alpha;
   if (P.alpha_ptr) alpha *= *P.alpha_ptr;
   // split-K into slabs: split s of the K loop writes its own fp32 slab (reduced by mmt_gemm_slab_reduce)
-  float* o32 = P.o32 + (P.split_stride ? (int64_t)blockIdx.y * P.split_stride : (int64_t)0);
+  float* o32 = P.o32 + (P.split_stride ? (int64_t)split * P.split_stride : (int64_t)0);
   const int h = lane >> 5, r = lane & 31;
   if constexpr (SWAP) {
     epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
@@ -534,9 +536,16 @@ static int auto_splits(const GemmBatch& b, int splits) {
   max_tiles<TL>(b, &tiles);
   for (int g = 0; g < b.count; ++g) maxk = b.p[g].K > maxk ? b.p[g].K : maxk;
   if (tiles <= 0) return 1;
-  const int target = TL::BM == 128 ? 512 : 256;
-  const int cap = TL::BM == 128 ? (tiles <= 8 ? 32 : 8) : 32;
-  const int s = (target + tiles - 1) / tiles;
+  static const int env_target = [] {
+    const char* e = getenv("MMT_WGRAD_BLOCKS");  // tuning knob: blocks per weight-gradient launch
+    return e ? atoi(e) : 0;
+  }();
+  // ~128 blocks: the weight gradients run on the side stream next to the data-gradient chain, so
+  // half the chip for longer beats the whole chip with twice the split-K slab traffic (measured at
+  // C1: 128 -> 9.97-10.28 ms/step, 256 -> 10.21-10.50, 64 -> 10.6)
+  const int target = env_target > 0 ? env_target : 128;
+  const int cap = 32;
+  const int s = target / tiles;
   const int maxs = std::max(1, std::min(cap, maxk / 512));
   return std::max(1, std::min(s, maxs));
 }
@@ -641,8 +650,11 @@ hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, in
 // Weight gradients dW[M, N] += alpha * dY[K, M]^T X[K, N] (both operands MN-contiguous, K = rows).
 // K = B*T is long and M x N small, so the K loop is split over workgroups. Each split writes a
 // plain fp32 slab (row-coalesced 16-B stores of the staged epilogue) and one reduce pass adds the
-// slabs into the gradient: fp32 atomics per element were the bottleneck (C1 FFN weight grads:
-// 16.7 M atomics per grouped launch, ~60 of its ~85 us).
+// slabs into the gradient. Measured alternatives (C1, same box): per-element fp32
+// atomics (16.7 M per FFN launch, ~60 of its ~85 us), and three in-kernel reductions with no
+// reduce launch (pairwise tree, every-split slice combine behind a per-tile arrival barrier, last
+// arriver) were all slower than this: the reduce launch runs on the side stream beside the
+// data-gradient chain, while an in-kernel reduction holds CUs waiting or reading serially.
 // ---------------------------------------------------------------------------------------------
 struct SlabProblem {
   const float* slab;  // [splits][M * N]
@@ -730,3 +742,7 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks, b.count), dim3(256), 0, s, sb);
   return hipGetLastError();
 }
+
+
+
+bool mmt_gemm_wgrad_big(const GemmBatch& b) { return use_big(b); }

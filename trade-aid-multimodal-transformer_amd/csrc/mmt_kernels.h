@@ -61,6 +61,8 @@ hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, in
 // weight gradients o32 += alpha * A^T B over K rows (both operands MN-contiguous): split-K into fp32
 // slabs in `slab` (capacity slab_bytes) + one reduce pass; without room, one K pass accumulating
 hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_bytes, hipStream_t s);
+// whether a weight-gradient batch runs on the 256x256 tile (launches can only be merged when equal)
+bool mmt_gemm_wgrad_big(const GemmBatch& b);
 
 // ------------------------------------------------------------------------------------------
 // LayerNorm (eps = 1e-5, weight+bias). Row-major [R, C] fp32 in, bf16 out; saves mean/rstd.
