@@ -16,6 +16,8 @@
  *   mmt_backward[_stage]          <- total_loss.backward() of main.py:646-649 (autograd over
  *                                    model.py), gradients into a flat fp32 buffer
  *   mmt_adamw_step                <- torch.optim.AdamW(m.parameters(), lr).step() (main.py:464, 650)
+ *   mmt_decode_step               <- one token of MultimodalTransformer.generate (model.py:404-446),
+ *                                    with a KV cache instead of the reference's full re-forward
  *   mmt_eval_direction            <- the per-sample loop of calculate_evaluation_metrics
  *                                    (training_utils.py:259-304)
  *   mmt_op_*                      primitive kernels, exported for kernel-level parity tests.
@@ -79,6 +81,16 @@ int64_t mmt_workspace_bytes(mmt_ctx* ctx, int32_t batch);
  * losses fp32 [M] (mean CE per modality, written only when tgt != NULL); training != 0 enables dropout */
 int mmt_forward(mmt_ctx* ctx, void* stream, int32_t batch, const int64_t* const* idx, const int64_t* const* tgt,
                 const float* params, float* const* logits, float* losses, void* workspace, int32_t training);
+
+/* KV-cache decode step of generate (reference model.py:404-446, which re-runs the whole forward
+ * per new token): the forward of ONE new position `pos` (1 <= pos < block_size) of every sequence
+ * and modality. idx[i]: int64 [batch] tokens of modality i at position pos; logits[i]: fp32
+ * [batch, V_i], the logits at position pos. Keys / values of positions < pos come from the last
+ * mmt_forward on this workspace (the prefill: prompt right-padded to block_size) and the decode
+ * steps since, which this step extends by position pos. Eval semantics (no dropout); the weights
+ * are the ones packed by that prefill forward. MMT_ERR_STATE without a prefill. */
+int mmt_decode_step(mmt_ctx* ctx, void* stream, int32_t batch, int32_t pos, const int64_t* const* idx,
+                    const float* params, float* const* logits, void* workspace);
 
 /* failure detection (the reference's guard is the NaN check on eval losses,
  * main.py:606): byte offset in the workspace (for this batch size) of two int32 bitmasks. The

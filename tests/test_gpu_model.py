@@ -264,3 +264,51 @@ def test_state_dict_roundtrip_reference_keys():
     for k, v in sd.items():
         assert torch.equal(out[k].cpu(), v), k
         assert list(out[k].shape) == meta["state_dict_shapes"][k]
+
+
+@pytest.mark.parametrize("name", ["f_small", "f_hs32", "f_demo"])
+def test_kv_cache_decode_matches_full_forward(name):
+    """KV-cache decode (mmt_decode_step, used by generate): after a prefill forward over positions
+    < P, one position per step up to block_size - 1; its logits against the full forward of the
+    whole sequence (causal: the same positions) and against the CPU oracle. f_small / f_demo have
+    cross-attention (multi-stream decode attention over the appended cross K/V rows)."""
+    import mmt_oracle as O
+    z, meta, cfg, sd, idx, tgt = model_fixture(name)
+    m = build(meta, sd)
+    m.eval()
+    T = meta["block_size"]
+    P = max(1, T // 2 - 1)
+    seq = [t.cuda() for t in idx]
+    with torch.no_grad():
+        m([s[:, :P] for s in seq])  # prefill
+        dec = [m._decode_step([s[:, t] for s in seq], t) for t in range(P, T)]
+        full, _ = m(seq)
+    ref, _ = O.forward(sd, cfg, idx)
+    for i in range(cfg.M):
+        got = torch.stack([d[i] for d in dec], dim=1).cpu()  # [B, T-P, V]
+        assert rel(got, full[i][:, P:T]) < 1e-2, (i, rel(got, full[i][:, P:T]))
+        assert rel(got, ref[i][:, P:T]) < 2e-2, (i, rel(got, ref[i][:, P:T]))
+    with pytest.raises(Exception):
+        m._decode_step([s[:, 0] for s in seq], T)  # position outside the block
+
+
+def test_generate_kv_cache_greedy_matches_reforward():
+    """generate with the KV cache against the reference's re-forward per token (use_cache=False),
+    greedy sampling on a model with peaked output heads (so argmax is stable to bf16 noise), past
+    the end of the block (the cache path hands over to the re-forward once positions shift)."""
+    z, meta, cfg, sd, idx, tgt = model_fixture("f_small")
+    sd = dict(sd)
+    for k in list(sd):
+        if k.startswith("post_block.soft_score_layers.") and k.endswith(".2.weight"):
+            sd[k] = sd[k] * 60.0
+    m = build(meta, sd)
+    m.eval()
+    T = meta["block_size"]
+    start = [t[:, :5].cuda() for t in idx]
+    greedy = lambda probs: probs.argmax(dim=-1, keepdim=True)  # noqa: E731
+    n_new = T + 3 - 5
+    a = m.generate(start, max_new_tokens=n_new, modality_to_generate=2, use_cache=True, sample_fn=greedy)
+    b = m.generate(start, max_new_tokens=n_new, modality_to_generate=2, use_cache=False, sample_fn=greedy)
+    for i in range(cfg.M):
+        assert tuple(a[i].shape) == (start[0].shape[0], T + 3)
+        assert torch.equal(a[i], b[i]), i

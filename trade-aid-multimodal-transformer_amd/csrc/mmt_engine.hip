@@ -81,6 +81,12 @@ struct Plan {
   size_t dres16[4][MAXM];
   size_t dvec[MAXM][MAXM];
   size_t dkv[MAXM][MAXM];
+  // KV-cache decode (generate): compact [B, *] rows of ONE new position per sequence
+  struct Dec {
+    size_t x0, a16, mean, rstd, h1, qkv, o16, p1, f, x2h, d16, qc, oc, pc, lnf16, hh;
+    size_t kv[MAXM];
+  } dec[MAXM];
+  std::vector<size_t> dec_x;  // [L*M][3]: fp32 residual stream x1, x2, x3 of the new rows
 };
 
 }  // namespace
@@ -108,6 +114,7 @@ struct mmt_ctx {
   Plan plan;
   int last_B = -1;
   bool fwd_ready = false;
+  bool cache_ready = false;  // a forward filled the workspace's Q/K/V (decode may follow)
   bool last_training = false;
   uint64_t step_counter = 0;
   // dropout: seed of the next training forward (mmt_set_dropout_seed) and of the last one
@@ -387,6 +394,17 @@ void make_plan(mmt_ctx* c, int B) {
     p.slab_bytes = (size_t)mx * 16 * f4;
     p.slab = A(p.slab_bytes);
   }
+  // decode scratch (tiny: B rows)
+  p.dec_x.resize((size_t)c->L * M * 3);
+  for (int i = 0; i < M; ++i) {
+    Plan::Dec& d = p.dec[i];
+    d.x0 = A(B * C * f4); d.a16 = A(B * C * b2); d.mean = A(B * f4); d.rstd = A(B * f4);
+    d.h1 = A(B * ldh1 * b2); d.qkv = A(B * 3 * C * b2); d.o16 = A(B * C * b2); d.p1 = A(B * ldp * b2);
+    d.f = A(B * 4 * C * b2); d.x2h = A(B * C * b2); d.d16 = A(B * C * b2); d.qc = A(B * C * b2);
+    d.oc = A(B * C * b2); d.pc = A(B * ldp * b2); d.lnf16 = A(B * C * b2); d.hh = A(B * c->ldvh[i] * b2);
+    for (int j = 0; j < M - 1; ++j) d.kv[j] = A(B * 2 * C * b2);
+  }
+  for (auto& o : p.dec_x) o = A(B * C * f4);
   p.total = cur;
 }
 
@@ -834,6 +852,176 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
 }
 
 // -------------------------------------------------------------------------------------------
+// KV-cache decode (generate, reference model.py:404-446): the forward of ONE new position t per
+// sequence, every layer and modality, on compact [B, *] rows. The self- and cross-attention keys /
+// values of positions < t are the ones the prefill forward (mmt_forward, same workspace) left in
+// its saved Q/K/V and cross-K/V buffers (row b*T + s); this step appends row t to them and runs
+// the decode attention over 0..t. Eval semantics (no dropout). The packed bf16 weights are the
+// ones the prefill forward made.
+// -------------------------------------------------------------------------------------------
+int run_decode(mmt_ctx* c, Runner& r, int t, const int64_t* const* idx, float* const* logits) {
+  const int M = c->M, C = c->C, H = c->H, hs = c->hs, B = r.B, T = c->T;
+  const int R = B;  // compact rows
+  const int ldh1 = r8(3 * H * c->hh), ldp = r8(C / 2);
+  const float scale = 1.0f / std::sqrt((float)hs);
+  Plan& p = c->plan;
+  const bf16_t* wpk = r.W<bf16_t>(p.pack);
+  r.wpk = wpk;
+  auto scatter_rows = [&](bf16_t* cache, int ld, const bf16_t* rows, const char* what) {
+    // compact row b -> cache row b*T + t
+    r.ok(hipMemcpy2DAsync(cache + (size_t)t * ld, (size_t)T * ld * 2, rows, (size_t)ld * 2, (size_t)ld * 2, B,
+                          hipMemcpyDeviceToDevice, r.s), what);
+  };
+  {
+    EmbBatch eb{};
+    eb.count = M;
+    for (int i = 0; i < M; ++i) {
+      eb.p[i].idx = idx[i]; eb.p[i].tok = r.P(c->post[i].tok); eb.p[i].pos = r.P(c->pos_off) + (int64_t)t * C;
+      eb.p[i].x = r.W<float>(p.dec[i].x0); eb.p[i].V = c->V[i];
+    }
+    r.ok(mmt_launch_embed_fwd(eb, B, 1, C, r.s), "dec_embed");
+  }
+  std::vector<const float*> xin(M);
+  for (int i = 0; i < M; ++i) xin[i] = r.W<float>(p.dec[i].x0);
+  for (int l = 0; l < c->L && r.rc == MMT_OK; ++l) {
+    const LM* x = &c->lm[(size_t)l * M];
+    const ActLM* a = &p.act[(size_t)l * M];
+    auto X = [&](int i, int k) { return r.W<float>(p.dec_x[((size_t)l * M + i) * 3 + k]); };
+    LnBatch lb{}; lb.count = M;
+    for (int i = 0; i < M; ++i) {
+      const Plan::Dec& d = p.dec[i];
+      lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].beta = r.P(x[i].ln1b);
+      lb.p[i].y = r.W<bf16_t>(d.a16); lb.p[i].mean = r.W<float>(d.mean); lb.p[i].rstd = r.W<float>(d.rstd);
+    }
+    r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "dec_ln1");
+    GemmBatch g{}; g.count = M;
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(p.dec[i].a16), C, wpk, x[i].W1, R);
+      g.p[i].bias = r.P(x[i].b1); g.p[i].o16 = r.W<bf16_t>(p.dec[i].h1); g.p[i].ldo16 = ldh1;
+    }
+    r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "dec_qkv1");
+    Qkv2Batch qb{}; qb.count = M;
+    for (int i = 0; i < M; ++i) {
+      qb.p[i].h1 = r.W<bf16_t>(p.dec[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].out = r.W<bf16_t>(p.dec[i].qkv);
+    }
+    r.ok(mmt_launch_qkv2_fwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "dec_qkv2");
+    DecodeAttnBatch ab{}; ab.count = M;
+    for (int i = 0; i < M; ++i) {
+      bf16_t* cache = r.W<bf16_t>(a[i].qkv);
+      scatter_rows(cache, 3 * C, r.W<bf16_t>(p.dec[i].qkv), "dec_kv_append");
+      DecodeAttnProblem& q = ab.p[i];
+      q.q = r.W<bf16_t>(p.dec[i].qkv) + C; q.q_ld = 3 * C;
+      q.k[0] = cache; q.v[0] = cache + 2 * C; q.kv_ld = 3 * C; q.kv_hstride = hs;
+      q.o = r.W<bf16_t>(p.dec[i].o16); q.o_ld = C; q.nstreams = 1;
+    }
+    r.ok(mmt_launch_attn_decode(ab, B, t, T, H, hs, scale, r.s), "dec_attn");
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(p.dec[i].o16), C, wpk, x[i].P0, R);
+      g.p[i].bias = r.P(x[i].bp0); g.p[i].o16 = r.W<bf16_t>(p.dec[i].p1); g.p[i].ldo16 = ldp;
+    }
+    r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "dec_proj0");
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(p.dec[i].p1), ldp, wpk, x[i].P2, R);
+      g.p[i].bias = r.P(x[i].bp2); g.p[i].resid = xin[i]; g.p[i].ldres = C;
+      g.p[i].o32 = X(i, 0); g.p[i].ldc = C;
+    }
+    r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "dec_proj2");
+    for (int i = 0; i < M; ++i) {
+      const Plan::Dec& d = p.dec[i];
+      lb.p[i].x = X(i, 0); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].beta = r.P(x[i].ln2b);
+      lb.p[i].y = r.W<bf16_t>(d.a16); lb.p[i].mean = r.W<float>(d.mean); lb.p[i].rstd = r.W<float>(d.rstd);
+    }
+    r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "dec_ln2");
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(p.dec[i].a16), C, wpk, x[i].F0, R);
+      g.p[i].bias = r.P(x[i].bf0); g.p[i].o16 = r.W<bf16_t>(p.dec[i].f); g.p[i].ldo16 = 4 * C;
+    }
+    r.gemm(g, true, true, EPI_BIAS_RELU_BF16, 1, "dec_ffn0");
+    for (int i = 0; i < M; ++i) {
+      g.p[i] = gp_fwd(r.W<bf16_t>(p.dec[i].f), 4 * C, wpk, x[i].F2, R);
+      g.p[i].bias = r.P(x[i].bf2); g.p[i].resid = X(i, 0); g.p[i].ldres = C;
+      g.p[i].o32 = X(i, 1); g.p[i].ldc = C;
+      if (c->any_cross) { g.p[i].o16 = r.W<bf16_t>(p.dec[i].x2h); g.p[i].ldo16 = C; }
+    }
+    r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "dec_ffn2");
+    std::vector<const float*> xout(M);
+    for (int i = 0; i < M; ++i) xout[i] = X(i, 1);
+    if (c->any_cross) {
+      std::vector<int> cx;
+      for (int i = 0; i < M; ++i) if (x[i].cross) cx.push_back(i);
+      LnBatch lc{}; lc.count = (int)cx.size();
+      GemmBatch gq{}; gq.count = (int)cx.size();
+      for (size_t u = 0; u < cx.size(); ++u) {
+        const int i = cx[u];
+        const Plan::Dec& d = p.dec[i];
+        lc.p[u].x = X(i, 1); lc.p[u].gamma = r.P(x[i].lncw); lc.p[u].beta = r.P(x[i].lncb);
+        lc.p[u].y = r.W<bf16_t>(d.d16); lc.p[u].mean = r.W<float>(d.mean); lc.p[u].rstd = r.W<float>(d.rstd);
+        gq.p[u] = gp_fwd(r.W<bf16_t>(d.d16), C, wpk, x[i].Wq, R);
+        gq.p[u].o16 = r.W<bf16_t>(d.qc); gq.p[u].ldo16 = C;
+      }
+      r.ok(mmt_launch_ln_fwd(lc, R, C, r.s), "dec_lnc");
+      r.gemm(gq, true, true, EPI_STORE_BF16, 1, "dec_ca_q");
+      GemmBatch gk{}; gk.count = 0;
+      for (int i : cx) {
+        int jj = 0;
+        for (int j = 0; j < M; ++j) {
+          if (j == i) continue;
+          gk.p[gk.count] = gp_fwd(r.W<bf16_t>(p.dec[j].x2h), C, wpk, x[i].Wkv[jj], R);
+          gk.p[gk.count].o16 = r.W<bf16_t>(p.dec[i].kv[jj]); gk.p[gk.count].ldo16 = 2 * C;
+          ++gk.count; ++jj;
+          if (gk.count == MMT_MAX_GROUP) { r.gemm(gk, true, true, EPI_STORE_BF16, 1, "dec_ca_kv"); gk.count = 0; }
+        }
+      }
+      if (gk.count) r.gemm(gk, true, true, EPI_STORE_BF16, 1, "dec_ca_kv");
+      DecodeAttnBatch cb{}; cb.count = (int)cx.size();
+      for (size_t u = 0; u < cx.size(); ++u) {
+        const int i = cx[u];
+        DecodeAttnProblem& q = cb.p[u];
+        q.q = r.W<bf16_t>(p.dec[i].qc); q.q_ld = C;
+        for (int j = 0; j < M - 1; ++j) {
+          bf16_t* kv = r.W<bf16_t>(a[i].kv[j]);
+          scatter_rows(kv, 2 * C, r.W<bf16_t>(p.dec[i].kv[j]), "dec_cakv_append");
+          q.k[j] = kv; q.v[j] = kv + hs;
+        }
+        q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(p.dec[i].oc); q.o_ld = C; q.nstreams = M - 1;
+      }
+      r.ok(mmt_launch_attn_decode(cb, B, t, T, H, hs, scale, r.s), "dec_ca_attn");
+      GemmBatch g0{}; g0.count = (int)cx.size();
+      GemmBatch g2{}; g2.count = (int)cx.size();
+      for (size_t u = 0; u < cx.size(); ++u) {
+        const int i = cx[u];
+        g0.p[u] = gp_fwd(r.W<bf16_t>(p.dec[i].oc), C, wpk, x[i].C0, R);
+        g0.p[u].bias = r.P(x[i].bc0); g0.p[u].o16 = r.W<bf16_t>(p.dec[i].pc); g0.p[u].ldo16 = ldp;
+        g2.p[u] = gp_fwd(r.W<bf16_t>(p.dec[i].pc), ldp, wpk, x[i].C2, R);
+        g2.p[u].bias = r.P(x[i].bc2); g2.p[u].resid = X(i, 1); g2.p[u].ldres = C;
+        g2.p[u].o32 = X(i, 2); g2.p[u].ldc = C;
+        xout[i] = X(i, 2);
+      }
+      r.gemm(g0, true, true, EPI_BIAS_TANH_BF16, 1, "dec_ca_proj0");
+      r.gemm(g2, true, true, EPI_BIAS_RESID_F32, 1, "dec_ca_proj2");
+    }
+    xin = xout;
+  }
+  if (r.rc != MMT_OK) return r.rc;
+  LnBatch lf{}; lf.count = M;
+  GemmBatch h0{}; h0.count = M;
+  GemmBatch h2{}; h2.count = M;
+  for (int i = 0; i < M; ++i) {
+    const Plan::Dec& d = p.dec[i];
+    lf.p[i].x = xin[i]; lf.p[i].gamma = r.P(c->post[i].lnw); lf.p[i].beta = r.P(c->post[i].lnb);
+    lf.p[i].y = r.W<bf16_t>(d.lnf16); lf.p[i].mean = r.W<float>(d.mean); lf.p[i].rstd = r.W<float>(d.rstd);
+    h0.p[i] = gp_fwd(r.W<bf16_t>(d.lnf16), C, wpk, c->post[i].H0, R);
+    h0.p[i].bias = r.P(c->post[i].b0); h0.p[i].o16 = r.W<bf16_t>(d.hh); h0.p[i].ldo16 = c->ldvh[i];
+    h2.p[i] = gp_fwd(r.W<bf16_t>(d.hh), c->ldvh[i], wpk, c->post[i].H2, R);
+    h2.p[i].bias = r.P(c->post[i].b2); h2.p[i].o32 = logits[i]; h2.p[i].ldc = c->V[i];
+  }
+  r.ok(mmt_launch_ln_fwd(lf, R, C, r.s), "dec_lnf");
+  r.gemm(h0, true, true, EPI_BIAS_TANH_BF16, 1, "dec_head0");
+  r.gemm(h2, true, true, EPI_STORE_F32, 1, "dec_head2");
+  return r.rc;
+}
+
+// -------------------------------------------------------------------------------------------
 // backward stages: 0 = post block, 1..L = layers L-1..0, L+1 = embeddings
 // -------------------------------------------------------------------------------------------
 void colsum_add(Runner& r, ColsumBatch& cb, int u, const bf16_t* x, int ld, float* out, int N, const float* aptr,
@@ -1238,6 +1426,7 @@ int64_t mmt_workspace_bytes(mmt_ctx* c, int32_t batch) {
   make_plan(c, batch);
   c->last_B = batch;
   c->fwd_ready = false;
+  c->cache_ready = false;
   return (int64_t)c->plan.total;
 }
 
@@ -1265,8 +1454,20 @@ int mmt_forward(mmt_ctx* c, void* stream, int32_t batch, const int64_t* const* i
   for (int i = 0; i < c->M; ++i) c->last_idx[i] = idx[i];
   rc = run_forward(c, r, idx, tgt, logits, losses);
   if (rc == MMT_OK && tgt) c->fwd_ready = true;
+  c->cache_ready = rc == MMT_OK;  // the saved Q/K/V of this forward serve mmt_decode_step
   c->last_training = training != 0;
   return rc;
+}
+
+int mmt_decode_step(mmt_ctx* c, void* stream, int32_t batch, int32_t pos, const int64_t* const* idx,
+                    const float* params, float* const* logits, void* workspace) {
+  if (!c) return MMT_ERR_INVALID;
+  if (!idx || !params || !logits || !workspace) return fail(c, MMT_ERR_INVALID, "mmt_decode_step: null argument");
+  if (c->plan.B != batch || !c->cache_ready)
+    return fail(c, MMT_ERR_STATE, "mmt_decode_step: run mmt_forward (prefill) on this batch and workspace first");
+  if (pos < 1 || pos >= c->T) return fail(c, MMT_ERR_INVALID, "mmt_decode_step: position outside 1..block_size-1");
+  Runner r{c, (hipStream_t)stream, workspace, params, nullptr, batch, batch};
+  return run_decode(c, r, pos, idx, logits);
 }
 
 int32_t mmt_backward_stage_count(const mmt_ctx* c) { return c ? c->L + 2 : 0; }

@@ -407,8 +407,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
   constexpr int EPI_ROWS = GBM == 128 ? 128 : 64;
   constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
   constexpr int LDS_MAIN = RING > CTILE ? RING : CTILE;
-  // (+16 B: the split-K last-arriver's role word, clear of the ring and the epilogue tile)
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN + (EPI == EPI_TREE_F32 ? 16 : 0)];
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;

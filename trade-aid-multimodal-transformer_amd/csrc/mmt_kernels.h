@@ -137,6 +137,20 @@ hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, 
 // fill dmask[j] (j < nstreams) of every problem with drop_thr != 0 from its counter hash
 hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStream_t s);
 
+// KV-cache decode attention (generate): the query of position t of sequence b (compact row b)
+// against cached keys / values of positions 0..t (rows b*T + s), per-stream softmax, outputs summed
+struct DecodeAttnProblem {
+  const bf16_t* q; int q_ld;                 // [B, *] compact
+  const bf16_t* k[MMT_MAX_STREAMS];
+  const bf16_t* v[MMT_MAX_STREAMS];          // cache [B*T, kv_ld]
+  int kv_ld, kv_hstride;
+  bf16_t* o; int o_ld;                       // [B, *] compact
+  int nstreams;
+};
+struct DecodeAttnBatch { DecodeAttnProblem p[MMT_MAX_GROUP]; int count; };
+hipError_t mmt_launch_attn_decode(const DecodeAttnBatch& b, int B, int t, int T, int H, int hs, float scale,
+                                  hipStream_t s);
+
 // ------------------------------------------------------------------------------------------
 // Per-head Q/K/V stage 2: block-diagonal [hs/2 -> hs] maps (model.py:39,44,49), nblk = 3*H.
 //   out[r, blk*hs + o] = sum_i W2[blk][o][i] * h1[r, blk*hs/2 + i]

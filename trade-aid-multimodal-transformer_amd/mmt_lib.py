@@ -60,6 +60,7 @@ _SIGS = {
     "mmt_forward": (c_i32, [c_vp, c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp,
                             ctypes.POINTER(c_vp), c_vp, c_vp, c_i32]),
     "mmt_backward": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mmt_decode_step": (c_i32, [c_vp, c_vp, c_i32, c_i32, ctypes.POINTER(c_vp), c_vp, ctypes.POINTER(c_vp), c_vp]),
     "mmt_backward_stage_count": (c_i32, [c_vp]),
     "mmt_backward_stage_range": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     "mmt_backward_stage": (c_i32, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),

@@ -22,7 +22,9 @@ Differences that are by design:
     only the losses; main.py:646-649);
   * training batches are exactly block_size long (as the reference's get_batch makes them); a
     shorter sequence without targets (generate, inference) runs right-padded to block_size: the
-    attention is causal, so the logits of the real positions are exactly those of the short run.
+    attention is causal, so the logits of the real positions are exactly those of the short run;
+  * generate keeps a KV cache (one prefill forward, then one position per token through
+    mmt_decode_step) while the sequence fits the block; the reference re-runs the forward.
 """
 import ctypes
 
@@ -351,28 +353,70 @@ class MultimodalTransformer(nn.Module):
         return logits, [losses[i] for i in range(M)]
 
     @torch.no_grad()
-    def generate(self, idx_list, max_new_tokens=1, modality_to_generate=0):
-        """model.py:404-446: per new token, a forward over the last block_size positions, a sample
-        from the softmax of the target modality's last logits (torch.multinomial, as the
-        reference), appended; the other modalities are padded with their last token or cropped to
-        the same length."""
+    def generate(self, idx_list, max_new_tokens=1, modality_to_generate=0, use_cache=True, sample_fn=None):
+        """model.py:404-446: per new token, the logits of the last position of the (block_size
+        cropped) context, a sample from the softmax of the target modality's last logits
+        (torch.multinomial, as the reference; `sample_fn(probs) -> [B, 1]` overrides it), appended;
+        the other modalities are padded with their last token or cropped to the same length.
+
+        The reference re-runs the whole forward per token. Here, while the sequence still fits the
+        block (positions do not shift), the first step is one forward over the prompt (the prefill,
+        which leaves the keys / values of every position in the workspace) and every later step is
+        ONE position through the KV-cache decode of the engine (mmt_decode_step): the same logits
+        (causal attention, absolute positions) at O(t) instead of O(block_size) attention and no
+        re-run of the prompt's GEMMs. Once the sequence outgrows the block every position shifts
+        and it falls back to the reference's full re-forward. use_cache=False (or training mode
+        with dropout, where the reference's forward samples dropout) always re-runs the forward."""
         seqs = [idx.clone() for idx in idx_list]
         T = self.block_size
+        g = modality_to_generate
+        sample = sample_fn or (lambda probs: torch.multinomial(probs, num_samples=1))
+        cache = (use_cache and not (self.training and self.dropout_p > 0.0)
+                 and len({int(s.shape[1]) for s in seqs}) == 1 and all(s.dim() == 2 for s in seqs))
+        cached_pos = None  # the last position whose keys / values the workspace holds
         for _ in range(max_new_tokens):
-            cond = [s[:, -T:] for s in seqs]
-            logits, _ = self(cond)
-            probs = torch.softmax(logits[modality_to_generate][:, -1, :], dim=-1)
-            nxt = torch.multinomial(probs, num_samples=1).to(seqs[modality_to_generate].dtype)
-            seqs[modality_to_generate] = torch.cat((seqs[modality_to_generate].to(nxt.device), nxt), dim=1)
-            n = seqs[modality_to_generate].shape[1]
+            n = seqs[g].shape[1]
+            if cache and cached_pos is not None and n - 1 == cached_pos + 1 and n <= T:
+                last = self._decode_step([s[:, n - 1] for s in seqs], n - 1)[g]
+                cached_pos = n - 1
+            else:
+                cond = [s[:, -T:] for s in seqs]
+                logits, _ = self(cond)
+                last = logits[g][:, -1, :]
+                cached_pos = n - 1 if (cache and n <= T) else None
+            probs = torch.softmax(last, dim=-1)
+            nxt = sample(probs).to(seqs[g].dtype)
+            seqs[g] = torch.cat((seqs[g].to(nxt.device), nxt), dim=1)
+            n = seqs[g].shape[1]
             for i in range(self.num_modalities):
-                if i == modality_to_generate:
+                if i == g:
                     continue
                 if seqs[i].shape[1] < n:
                     seqs[i] = torch.cat((seqs[i], seqs[i][:, -1:]), dim=1)
                 elif seqs[i].shape[1] > n:
                     seqs[i] = seqs[i][:, :n]
         return seqs
+
+    @torch.no_grad()
+    def _decode_step(self, tokens, pos):
+        """Logits [B, V_i] of every modality at position `pos` (1 <= pos < block_size), given the
+        tokens [B] of that position; the workspace must hold positions < pos (a forward over them,
+        then decode steps; include/mmt.h mmt_decode_step)."""
+        flat = self.flat_params
+        dev = flat.device
+        B = tokens[0].shape[0]
+        if self._ws is None or self._ws_batch != B:
+            raise RuntimeError("_decode_step: no prefill forward at this batch size")
+        idx = [t.to(device=dev, dtype=torch.long).contiguous() for t in tokens]
+        logits = [torch.empty(B, V, dtype=torch.float32, device=dev) for V in self.vocab_sizes]
+        L = ML.lib()
+        with torch.cuda.device(dev):
+            rc = L.mmt_decode_step(self._ctx, ML.stream_ptr(dev), B, int(pos), ML.ptr_array(idx), ML.ptr(flat),
+                                   ML.ptr_array(logits), ML.ptr(self._ws))
+        ML.check(rc, self._ctx, "mmt_decode_step")
+        self._gen += 1
+        self._keep_decode = idx  # alive until the step's kernels have read them
+        return logits
 
     def __del__(self):
         try:
