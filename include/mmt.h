@@ -56,6 +56,9 @@ typedef struct mmt_config {
   int32_t cross_attention[MMT_MAX_MODALITIES];  /* all_modality_params[i][8] */
   float dropout;                                /* nn.Dropout p (model.py:57,87,107,134,171) */
   uint64_t seed;                                /* dropout RNG seed */
+  int32_t precision;                            /* 0: bf16 MFMA; 1: MX-fp8 forward GEMMs (C4;
+                                                   Q/K/V stage 1, FFN, cross-attention query;
+                                                   needs n_embd % 32 == 0) */
 } mmt_config;
 
 typedef struct mmt_ctx mmt_ctx;
@@ -197,6 +200,22 @@ int mmt_op_embedding_fwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t 
                          const float* tok, const float* pos, float* x);
 int mmt_op_embedding_bwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx,
                          const float* dx, float* dtok, float* dpos);
+
+/* ---- MX-fp8 primitives (C4's fp8 path; BASELINE configs[4]) --------------------------------
+ * MX-fp8 = OCP e4m3fn bytes + one E8M0 exponent byte (bias 127) per 32 consecutive K elements of a
+ * row: exponent e = the smallest with amax(block) / 2^e <= 448, value = fp8(x * 2^-e) (RNE). */
+int mmt_op_mx_quant(void* stream, int32_t rows, int32_t cols, const float* src, int32_t ld_src, void* dst8,
+                    int32_t ld8, void* s8, int32_t lds8);
+/* Y = X W^T on MX-fp8 X [M][K] (lda bytes) / W [N][K] (ldb bytes) with exponents sa [M][lds_a],
+ * sb [N][lds_b] (K % 32 == 0, lds % 4 == 0); epi as mmt_op_gemm's forward epilogues; o8 / s8
+ * (nullable): an MX-fp8 copy of a bf16 output (N % 32 == 0) */
+int mmt_op_gemm_f8(void* stream, int32_t epi, int32_t M, int32_t N, int32_t K, const void* A8, int32_t lda,
+                   const void* sa, int32_t lds_a, const void* B8, int32_t ldb, const void* sb, int32_t lds_b,
+                   const float* bias, const float* resid, int32_t ldres, float* o32, int32_t ldc, void* o16,
+                   int32_t ldo16, void* o8, int32_t ld8, void* s8, int32_t lds8);
+/* LayerNorm forward that also writes an MX-fp8 copy of its output (C % 32 == 0) */
+int mmt_op_layernorm_fwd_f8(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
+                            void* y16, float* mean, float* rstd, void* y8, int32_t ld8, void* s8, int32_t lds8);
 
 #ifdef __cplusplus
 }

@@ -42,7 +42,7 @@ import torch.nn.functional as F
 # configuration helpers
 # --------------------------------------------------------------------------------------
 class OracleConfig:
-    def __init__(self, n_embd, n_head, n_layer, block_size, vocab_sizes, cross, dropout=0.0):
+    def __init__(self, n_embd, n_head, n_layer, block_size, vocab_sizes, cross, dropout=0.0, precision="bf16"):
         self.C = int(n_embd)
         self.H = int(n_head)
         self.L = int(n_layer)
@@ -52,6 +52,7 @@ class OracleConfig:
         self.cross = [bool(c) for c in cross]
         self.dropout = float(dropout)
         self.hs = self.C // self.H
+        self.precision = precision  # "fp8": the build's MX-fp8 forward GEMMs (mx_fp8, _lin8)
 
 
 def param_shapes(cfg):
@@ -135,6 +136,17 @@ def _lin(x, w, b=None):
     return y + b if b is not None else y
 
 
+def _lin8(x, w, b=None, fp8=False):
+    """A forward GEMM of the build's fp8 path (precision "fp8": Q/K/V stage 1, FFN, cross query):
+    the VALUE from MX-fp8 operands (mx_fp8 along K of the activation rows and the weight rows),
+    the GRADIENT that of the unquantised product (the build's backward GEMMs read the bf16 copies)."""
+    y = _lin(x, w, b)
+    if not fp8:
+        return y
+    yq = _lin(mx_fp8(x.detach()), mx_fp8(w.detach()), b)
+    return y + (yq - y).detach()
+
+
 def _ln(x, w, b):
     return F.layer_norm(x, (x.shape[-1],), w, b, 1e-5)
 
@@ -207,12 +219,12 @@ def _drop(x, p, training, mask_fn=None):
     return F.dropout(x, p, True)
 
 
-def _head(sd, pre, x, p, training, dm=None):
+def _head(sd, pre, x, p, training, dm=None, fp8=False):
     """model.py:60-73. k/q/v = Linear(C,hs/2)+b -> tanh -> Linear(hs/2,hs, no bias).
     dm: optional () -> mask for the probabilities (HashDropout)."""
     T = x.shape[1]
     def mlp(kind):
-        h = torch.tanh(_lin(x, sd[f"{pre}{kind}.0.weight"], sd[f"{pre}{kind}.0.bias"]))
+        h = torch.tanh(_lin8(x, sd[f"{pre}{kind}.0.weight"], sd[f"{pre}{kind}.0.bias"], fp8))
         return _lin(h, sd[f"{pre}{kind}.2.weight"])
     k = mlp("key")
     q = mlp("query")
@@ -236,7 +248,8 @@ def _mha(sd, pre, x, cfg, training, hd=None, l=0, i=0):
     B, T, C = x.shape
     def pm(h):
         return (lambda: hd.probs(l, i, SITE_SA_PROB, 0, h, cfg.H, B, T)) if hd else None
-    out = torch.cat([_head(sd, f"{pre}heads.{h}.", x, cfg.dropout, training, pm(h)) for h in range(cfg.H)], dim=-1)
+    out = torch.cat([_head(sd, f"{pre}heads.{h}.", x, cfg.dropout, training, pm(h), cfg.precision == "fp8")
+                     for h in range(cfg.H)], dim=-1)
     return _drop(_proj(sd, pre, out), cfg.dropout, training,
                  (lambda: hd.rowcol(l, i, SITE_SA_PROJ, B, T, C)) if hd else None)
 
@@ -249,7 +262,7 @@ def _cross(sd, pre, qx, kv_list, cfg, training, hd=None, l=0, i=0):
     heads = []
     for h in range(cfg.H):
         hp = f"{pre}heads.{h}."
-        q = _lin(qx, sd[f"{hp}query.weight"])
+        q = _lin8(qx, sd[f"{hp}query.weight"], None, cfg.precision == "fp8")
         outs = []
         for j, kvx in enumerate(kv_list):
             kv = _lin(kvx, sd[f"{hp}kv_projections.{j}.weight"])
@@ -269,8 +282,9 @@ def _cross(sd, pre, qx, kv_list, cfg, training, hd=None, l=0, i=0):
 def _ffn(sd, pre, x, cfg, training, hd=None, l=0, i=0):
     """model.py:167-175."""
     B, T, C = x.shape
-    h = torch.relu(_lin(x, sd[f"{pre}net.0.weight"], sd[f"{pre}net.0.bias"]))
-    return _drop(_lin(h, sd[f"{pre}net.2.weight"], sd[f"{pre}net.2.bias"]), cfg.dropout, training,
+    f8 = cfg.precision == "fp8"
+    h = torch.relu(_lin8(x, sd[f"{pre}net.0.weight"], sd[f"{pre}net.0.bias"], f8))
+    return _drop(_lin8(h, sd[f"{pre}net.2.weight"], sd[f"{pre}net.2.bias"], f8), cfg.dropout, training,
                  (lambda: hd.rowcol(l, i, SITE_FFN, B, T, C)) if hd else None)
 
 
@@ -426,6 +440,33 @@ def get_batch(train_lists, val_tensors, rand_sizes, vocab_sizes, block_size, bat
     xb = [torch.stack([d[i:i + block_size] for i in ix]) for d in data]
     yb = [torch.stack([d[i + 1:i + block_size + 1] for i in ix]) for d in data]
     return xb, yb
+
+
+# --------------------------------------------------------------------------------------
+# MX-fp8 (the build's C4 fp8 path; no reference counterpart: BASELINE configs[4] names the
+# precision, the reference computes in fp32). Restates mmt_common.h mx_exp / mx_inv / pack4fp8.
+# --------------------------------------------------------------------------------------
+def mx_fp8_parts(x):
+    """x [..., K] (K % 32 == 0) -> (e4m3fn tensor [..., K], exponent int32 [..., K/32]): per 32
+    consecutive elements e = the smallest with amax / 2^e <= 448 (amax * fp32(1/448), ceil of log2
+    from the float bits, clamped to [-127, 126]; amax == 0 -> -127), values fp8(x * 2^-e)."""
+    xs = x.float().reshape(*x.shape[:-1], x.shape[-1] // 32, 32)
+    amax = xs.abs().amax(dim=-1)
+    t = amax * torch.tensor(1.0 / 448.0, dtype=torch.float32)
+    bits = t.view(torch.int32)
+    e = ((bits >> 23) & 0xFF) - 127 + ((bits & 0x7FFFFF) != 0).to(torch.int32)
+    e = torch.where(amax > 0, e, torch.full_like(e, -127)).clamp(-127, 126)
+    inv = ((127 - e) << 23).view(torch.float32)
+    q = (xs * inv.unsqueeze(-1)).to(torch.float8_e4m3fn)
+    return q.reshape(x.shape), e.to(torch.int32)
+
+
+def mx_fp8(x):
+    """Quantise-dequantise x along its last dim through MX-fp8 (mx_fp8_parts)."""
+    q, e = mx_fp8_parts(x)
+    scale = ((e + 127) << 23).view(torch.float32)  # 2^e
+    qs = q.float().reshape(*x.shape[:-1], x.shape[-1] // 32, 32) * scale.unsqueeze(-1)
+    return qs.reshape(x.shape)
 
 
 def direction_sign(cur, prev, is_pct):

@@ -1,0 +1,205 @@
+"""MX-fp8 primitives of the C4 fp8 path (BASELINE configs[4]) against the oracle's restatement
+(oracle/mmt_oracle.py mx_fp8_parts / mx_fp8):
+  * quantisation (mmt_op_mx_quant): every e4m3fn byte and E8M0 exponent bit-identical (the
+    conversion is v_cvt_pk_fp8_f32 = torch's float8_e4m3fn rounding; the exponent rule is integer);
+  * the fp8 GEMM (mmt_op_gemm_f8, v_mfma_scale_f32_32x32x64_f8f6f4) against fp32 matmul of the
+    dequantised operands: only the fp32 accumulation order differs (rel-L2 <= 5e-5);
+  * the MX-fp8 copies written by the LayerNorm and ReLU epilogues against quantising their fp32
+    results (bytes may differ where the fp32 result itself differs in the last ulp: >= 99.9 % equal,
+    dequantised rel-L2 <= 1e-3).
+"""
+import pytest
+import torch
+
+import mmt_lib as ML
+import mmt_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _s():
+    return ML.stream_ptr(torch.device(DEV))
+
+
+def quant(x):
+    rows, cols = x.shape
+    lds = (cols // 32 + 3) // 4 * 4
+    q = torch.empty(rows, cols, dtype=torch.uint8, device=DEV)
+    sc = torch.empty(rows, lds, dtype=torch.uint8, device=DEV)
+    xc = x.contiguous()
+    assert ML.lib().mmt_op_mx_quant(_s(), rows, cols, ML.ptr(xc), cols, ML.ptr(q), cols, ML.ptr(sc), lds) == 0
+    torch.cuda.synchronize()
+    return q, sc, lds
+
+
+@pytest.mark.parametrize("rows,cols", [(7, 32), (130, 96), (64, 1024)])
+def test_mx_quant_bit_exact(rows, cols):
+    torch.manual_seed(rows + cols)
+    x = torch.randn(rows, cols) * torch.exp(torch.randn(rows, 1) * 4)  # magnitudes over ~2^-12..2^12
+    x[0, :32] = 0.0                      # all-zero block
+    x[1, 32 % cols: 32 % cols + 1] = 1e30  # huge element
+    x[2, :] = 1e-30                      # denormal-scale row
+    q, sc, lds = quant(x.to(DEV))
+    rq, re = O.mx_fp8_parts(x)
+    assert torch.equal(q.cpu(), rq.view(torch.uint8))
+    assert torch.equal(sc[:, :cols // 32].cpu().to(torch.int32) - 127, re)
+    if lds * 32 > cols:
+        assert int(sc[:, cols // 32:].min()) == 127 == int(sc[:, cols // 32:].max())
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 384, 256), (300, 200, 96), (128, 1024, 1024), (33, 64, 32)])
+def test_gemm_f8_matches_dequantised_fp32(M, N, K):
+    torch.manual_seed(M + N + K)
+    X = torch.randn(M, K)
+    W = torch.randn(N, K) * 0.05
+    bias = torch.randn(N)
+    xq, xs, ldsx = quant(X.to(DEV))
+    wq, ws, ldsw = quant(W.to(DEV))
+    ref = O.mx_fp8(X).double() @ O.mx_fp8(W).double().t() + bias.double()
+    out = torch.empty(M, N, device=DEV)
+    b_d = bias.to(DEV)
+    rc = ML.lib().mmt_op_gemm_f8(_s(), ML.EPI["store_f32"], M, N, K, ML.ptr(xq), K, ML.ptr(xs), ldsx, ML.ptr(wq), K,
+                                 ML.ptr(ws), ldsw, ML.ptr(b_d), None, 0, ML.ptr(out), N, None, 0, None, 0, None, 0)
+    assert rc == 0
+    torch.cuda.synchronize()
+    err = ((out.cpu().double() - ref).norm() / ref.norm()).item()
+    assert err < 5e-5, err  # fp32 accumulation order over K (measured 1.3e-5 at K = 1024)
+
+
+def test_gemm_f8_relu_epilogue_mx_copy():
+    """ffn0's fp8 form: bias + ReLU, bf16 output for the backward and an MX-fp8 copy for ffn2."""
+    torch.manual_seed(5)
+    M, N, K = 512, 1024, 256
+    X = torch.randn(M, K)
+    W = torch.randn(N, K) * 0.06
+    bias = torch.randn(N) * 0.1
+    xq, xs, ldsx = quant(X.to(DEV))
+    wq, ws, ldsw = quant(W.to(DEV))
+    o16 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    lds8 = N // 32
+    o8 = torch.empty(M, N, dtype=torch.uint8, device=DEV)
+    s8 = torch.empty(M, lds8, dtype=torch.uint8, device=DEV)
+    b_d = bias.to(DEV)
+    rc = ML.lib().mmt_op_gemm_f8(_s(), ML.EPI["bias_relu_bf16"], M, N, K, ML.ptr(xq), K, ML.ptr(xs), ldsx, ML.ptr(wq),
+                                 K, ML.ptr(ws), ldsw, ML.ptr(b_d), None, 0, None, 0, ML.ptr(o16), N, ML.ptr(o8), N,
+                                 ML.ptr(s8), lds8)
+    assert rc == 0
+    torch.cuda.synchronize()
+    y = torch.relu(O.mx_fp8(X) @ O.mx_fp8(W).t() + bias)
+    assert ((o16.float().cpu() - y).norm() / y.norm()).item() < 1e-2
+    rq, re = O.mx_fp8_parts(y)
+    same = (o8.cpu() == rq.view(torch.uint8)).float().mean().item()
+    assert same > 0.999, same
+    deq = O.mx_fp8(y)
+    got = o8.cpu().view(torch.float8_e4m3fn).float().reshape(M, N // 32, 32) * \
+        ((s8.cpu().to(torch.int32)) << 23).view(torch.float32).unsqueeze(-1)
+    assert ((got.reshape(M, N) - deq).norm() / deq.norm()).item() < 1e-3
+
+
+def test_layernorm_mx_copy():
+    torch.manual_seed(9)
+    R, C = 333, 256
+    x = torch.randn(R, C) * 3 + 1
+    g = 1 + 0.1 * torch.randn(C)
+    b = 0.05 * torch.randn(C)
+    xd, gd, bd = x.to(DEV), g.to(DEV), b.to(DEV)
+    y16 = torch.empty(R, C, dtype=torch.bfloat16, device=DEV)
+    mean = torch.empty(R, device=DEV)
+    rstd = torch.empty(R, device=DEV)
+    y8 = torch.empty(R, C, dtype=torch.uint8, device=DEV)
+    s8 = torch.empty(R, C // 32, dtype=torch.uint8, device=DEV)
+    rc = ML.lib().mmt_op_layernorm_fwd_f8(_s(), R, C, ML.ptr(xd), ML.ptr(gd), ML.ptr(bd), ML.ptr(y16), ML.ptr(mean),
+                                          ML.ptr(rstd), ML.ptr(y8), C, ML.ptr(s8), C // 32)
+    assert rc == 0
+    torch.cuda.synchronize()
+    y = torch.nn.functional.layer_norm(x, (C,), g, b, eps=1e-5)
+    rq, re = O.mx_fp8_parts(y)
+    assert (y8.cpu() == rq.view(torch.uint8)).float().mean().item() > 0.999
+    assert (s8.cpu().to(torch.int32) - 127 == re).float().mean().item() > 0.999
+
+
+# ------------------------------------------------------------------------------------------------
+# model level (precision "fp8": MX-fp8 Q/K/V stage 1, FFN and cross-attention query GEMMs)
+# ------------------------------------------------------------------------------------------------
+import config_utils  # noqa: E402
+from golden_io import model_fixture, scale_fixture  # noqa: E402
+
+
+def _build(meta, sd, precision, dropout=0.0, B=None):
+    config_utils._config_cache = {"n_embd": meta["n_embd"], "n_head": meta["n_head"], "n_layer": meta["n_layer"],
+                                  "block_size": meta["block_size"], "dropout": dropout, "device": "cuda",
+                                  "batch_size": B or meta["B"], "eval_iters": 1, "precision": precision}
+    import model as mmt_model
+    params = [[None] * 8 + [c] + [None] * 3 for c in meta["cross"]]
+    m = mmt_model.MultimodalTransformer(len(meta["V"]), meta["V"], params).to("cuda")
+    full = dict(sd)
+    T = meta["block_size"]
+    for k in meta["state_dict_keys"]:
+        if k.endswith("tril"):
+            full[k] = torch.tril(torch.ones(T, T))
+    m.load_state_dict(full, strict=True)
+    assert m.precision == precision
+    return m
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("name", ["f_demo", "f_small", "f_m8"])
+def test_fp8_step_matches_fp8_oracle_and_reference(name):
+    """The fp8 training step against (1) the oracle's fp8 emulation (same MX quantisation, bf16
+    tolerances: losses rel 5e-3, logits rel-L2 2e-2, gradients rel-L2 3e-2) and (2) the reference's
+    fp32 result (SURVEY.md §8c fp8 bar: loss rel <= 2e-2)."""
+    z, meta, cfg, sd, idx, tgt = (scale_fixture if name == "f_m8" else model_fixture)(name)
+    m = _build(meta, sd, "fp8")
+    logits, losses = m([t.cuda() for t in idx], [t.cuda() for t in tgt])
+    sum(losses).backward()
+    torch.cuda.synchronize()
+    got = torch.stack([l.detach().cpu() for l in losses])
+    assert torch.allclose(got, torch.from_numpy(z["losses"]), rtol=2e-2, atol=2e-2), (got, z["losses"])
+    cfg.precision = "fp8"
+    r_logits, r_losses, r_grads = O.forward_backward(sd, cfg, idx, tgt)
+    assert torch.allclose(got, torch.stack(r_losses), rtol=5e-3, atol=5e-3), (got, r_losses)
+    for i in range(cfg.M):
+        assert _rel(logits[i], r_logits[i]) < 2e-2, i
+    pairs = [(g.flatten().cpu(), r_grads[k].flatten()) for k, g in m.reference_grad_views()
+             if g is not None and r_grads.get(k) is not None]
+    a = torch.cat([p for p, _ in pairs])
+    b = torch.cat([q for _, q in pairs])
+    assert _rel(a, b) < 4e-2
+
+
+def test_fp8_loss_curve_tracks_bf16():
+    """SURVEY.md §8c fp8 bar: a 100-step training loss curve within 3 % of the bf16 curve (same
+    init, same batches, AdamW lr 1e-3, f_small dims at batch 16)."""
+    import mmt_optim
+    z, meta, cfg, sd, idx, tgt = model_fixture("f_small")
+    T, V = meta["block_size"], meta["V"]
+    g = torch.Generator().manual_seed(11)
+    # learnable streams: each modality repeats a random 40-token pattern (the next token follows
+    # from the context)
+    streams = [torch.randint(0, v, (40,), generator=g).repeat(500) for v in V]
+    starts = torch.randint(0, 20000 - T - 1, (100, 16), generator=g)
+    curves = {}
+    for prec in ("bf16", "fp8"):
+        m = _build(meta, sd, prec, B=16)
+        opt = mmt_optim.AdamW(m.parameters(), lr=1e-3)
+        out = []
+        for st in range(100):
+            ix = starts[st]
+            xb = [torch.stack([s[i:i + T] for i in ix]).cuda() for s in streams]
+            yb = [torch.stack([s[i + 1:i + T + 1] for i in ix]).cuda() for s in streams]
+            _, losses = m(xb, yb)
+            loss = sum(losses)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            out.append(loss.item())
+        curves[prec] = torch.tensor(out)
+    a, b = curves["fp8"], curves["bf16"]
+    assert b[-1] < 0.8 * b[0]  # it learns
+    dev = ((a - b).abs() / b).max().item()
+    assert dev < 0.03, dev

@@ -16,7 +16,9 @@ _DEFAULTS = {
     "training_parameters": {"batch_size": 32, "block_size": 64, "max_iters": 5000, "eval_interval": 500,
                             "eval_iters": 40, "learning_rate": 3e-4},
     "model_architecture": {"n_embd": 384, "n_head": 6, "n_layer": 6, "dropout": 0.2,
-                           "fixed_values": [-0.5, -0.2, -0.1, 0, 0.1, 0.2, 0.5]},
+                           "fixed_values": [-0.5, -0.2, -0.1, 0, 0.1, 0.2, 0.5],
+                           # build-only key (the reference ignores unknown keys): "bf16" | "fp8"
+                           "precision": "bf16"},
 }
 
 
@@ -81,3 +83,12 @@ def _get_dropout():
 
 def _get_fixed_values():
     return _get_config()["fixed_values"]
+
+
+def _get_precision():
+    """Build-only knob (no reference counterpart): "bf16" (default) or "fp8" (MX-fp8 forward
+    GEMMs, BASELINE configs[4]); the MMT_PRECISION environment variable overrides the config."""
+    p = os.environ.get("MMT_PRECISION") or _get_config().get("precision", "bf16")
+    if p not in ("bf16", "fp8"):
+        raise ValueError(f"precision must be 'bf16' or 'fp8', got {p!r}")
+    return p

@@ -101,3 +101,29 @@ __host__ __device__ __forceinline__ uint32_t mmt_hash(uint32_t a, uint32_t b, ui
   h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
   return h;
 }
+
+// ---------------------------------------------------------------------------------------------
+// MX-fp8 (OCP e4m3fn values, E8M0 block exponents over 32 consecutive K elements): the operand
+// format of v_mfma_scale_f32_32x32x64_f8f6f4 (C4's fp8 path). A 32-element block with absolute
+// max `amax` gets the smallest exponent e with amax / 2^e <= 448 (no clipping: every value stays
+// finite in e4m3fn, whose conversion does not saturate), stored as the byte e + 127; its values
+// are fp8(x * 2^-e) (round to nearest even, v_cvt_pk_fp8_f32). The oracle restates this exactly
+// (oracle/mmt_oracle.py mx_fp8).
+// ---------------------------------------------------------------------------------------------
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ int mx_exp(float amax) {
+  if (!(amax > 0.f)) return -127;
+  const uint32_t u = __float_as_uint(amax * (1.0f / 448.0f));
+  int e = (int)((u >> 23) & 0xff) - 127;
+  if (u & 0x7fffffu) ++e;  // ceil(log2) unless a power of two (denormal quotients: e = -127 or -126)
+  return e < -127 ? -127 : (e > 126 ? 126 : e);
+}
+// 2^-e for e in [-127, 126]
+__device__ __forceinline__ float mx_inv(int e) { return __uint_as_float((uint32_t)(127 - e) << 23); }
+// four floats (already multiplied by 2^-e) -> four e4m3fn bytes, element 0 in the low byte
+__device__ __forceinline__ uint32_t pack4fp8(float a, float b, float c, float d) {
+  uint32_t w = 0;
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return w;
+}

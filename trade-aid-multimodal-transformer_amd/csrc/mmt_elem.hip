@@ -63,6 +63,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnBatch batch, int R, int C
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = (v[u][i][e] - mean) * rstd * g[i][e] + b[i][e];
         reinterpret_cast<u32x2*>(y)[c4] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+        if (P.y8) {  // MX-fp8 copy: a 32-column block is 8 consecutive lanes
+          float am = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+          am = fmaxf(am, __shfl_xor(am, 1, 64));
+          am = fmaxf(am, __shfl_xor(am, 2, 64));
+          am = fmaxf(am, __shfl_xor(am, 4, 64));
+          const int ex = mx_exp(am);
+          const float inv = mx_inv(ex);
+          reinterpret_cast<uint32_t*>(P.y8 + (int64_t)row * P.ld8)[c4] = pack4fp8(o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv);
+          if ((c4 & 7) == 0) P.s8[(int64_t)row * P.lds8 + (c4 >> 3)] = (uint8_t)(ex + 127);
+        }
       }
     }
     if (lane == 0) { P.mean[row] = mean; P.rstd[row] = rstd; }
@@ -698,5 +708,55 @@ hipError_t mmt_launch_eval_direction(const float* logits, const int64_t* xb, con
   if (B == 0) return hipSuccess;
   hipLaunchKernelGGL(eval_dir_kernel, dim3(B), dim3(64), 0, s, logits, xb, yb, vocab, T, V, is_pct, wins_losses,
                      certainty);
+  return hipGetLastError();
+}
+
+// ============================================================================================
+// MX-fp8 quantisation (mmt_common.h): one thread per (row, 32-column block) of each segment
+// ============================================================================================
+__device__ __forceinline__ void mx_quant_unit(const MxSeg& S, int64_t u, const float* base, uint8_t* dst) {
+  const int nb = S.lds8;  // blocks per row including the padding exponents
+  if (u >= (int64_t)S.rows * nb) return;
+  const int row = (int)(u / nb), kb = (int)(u % nb);
+  uint8_t* sp = dst + S.sdst + (int64_t)row * S.lds8 + kb;
+  if (kb * 32 >= S.cols) { *sp = 127; return; }
+  const float* src = base + S.src + (int64_t)row * S.ld_src + kb * 32;
+  f32x4 v[8];
+  float am = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    v[q] = reinterpret_cast<const f32x4*>(src)[q];
+    am = fmaxf(am, fmaxf(fmaxf(fabsf(v[q][0]), fabsf(v[q][1])), fmaxf(fabsf(v[q][2]), fabsf(v[q][3]))));
+  }
+  const int ex = mx_exp(am);
+  const float inv = mx_inv(ex);
+  u32x4 w[2];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    w[q >> 2][q & 3] = pack4fp8(v[q][0] * inv, v[q][1] * inv, v[q][2] * inv, v[q][3] * inv);
+  uint8_t* dp = dst + S.dst + (int64_t)row * S.ld8 + kb * 32;
+  reinterpret_cast<u32x4*>(dp)[0] = w[0];
+  reinterpret_cast<u32x4*>(dp)[1] = w[1];
+  *sp = (uint8_t)(ex + 127);
+}
+
+__global__ __launch_bounds__(256) void mx_quant_kernel(const MxSeg* segs, const float* base, uint8_t* dst) {
+  mx_quant_unit(segs[blockIdx.y], (int64_t)blockIdx.x * 256 + threadIdx.x, base, dst);
+}
+__global__ __launch_bounds__(256) void mx_quant1_kernel(MxSeg S, const float* base, uint8_t* dst) {
+  mx_quant_unit(S, (int64_t)blockIdx.x * 256 + threadIdx.x, base, dst);
+}
+
+hipError_t mmt_launch_mx_quant1(const MxSeg& S, const float* base, uint8_t* dst, hipStream_t s) {
+  const int64_t units = (int64_t)S.rows * S.lds8;
+  if (units == 0) return hipSuccess;
+  hipLaunchKernelGGL(mx_quant1_kernel, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, s, S, base, dst);
+  return hipGetLastError();
+}
+
+hipError_t mmt_launch_mx_quant(const MxSeg* segs_dev, int nseg, int max_units, const float* base, uint8_t* dst,
+                               hipStream_t s) {
+  if (nseg == 0 || max_units == 0) return hipSuccess;
+  hipLaunchKernelGGL(mx_quant_kernel, dim3((max_units + 255) / 256, nseg), dim3(256), 0, s, segs_dev, base, dst);
   return hipGetLastError();
 }

@@ -33,6 +33,10 @@ struct Mat {
   int rows = 0, cols = 0;
   int64_t pk = 0;    // bf16 element offset in the packed-weight region
   int ld = 0;        // packed leading dimension (multiple of 8)
+  // MX-fp8 copy (precision fp8): byte offsets of the e4m3fn rows and E8M0 exponents in the fp8
+  // pack region, row strides in bytes; pk8 < 0: no fp8 copy
+  int64_t pk8 = -1, ps8 = -1;
+  int ld8 = 0, lds8 = 0;
 };
 
 struct TensorInfo {
@@ -63,6 +67,9 @@ struct ActLM {  // byte offsets of one (layer, modality)'s saved activations in 
   size_t a, mean1, rstd1, h1, qkv, o, lse, p1, x1, c, mean2, rstd2, f, x2, x2h;
   size_t d, meanc, rstdc, qc, kv[MAXM], oc, ocj[MAXM], lsej[MAXM], pc, x3;
   size_t dm, dmj[MAXM];  // attention dropout keep bits (SA; CA per KV stream), dropout > 0 only
+  // MX-fp8 copies of the fp8 GEMMs' A operands (precision fp8): LN1 / LN2 / LNc outputs and the
+  // FFN hidden, e4m3fn bytes + E8M0 exponents
+  size_t a8 = 0, as8 = 0, c8 = 0, cs8 = 0, f8 = 0, fs8 = 0, d8 = 0, ds8 = 0;
 };
 
 struct Plan {
@@ -71,6 +78,7 @@ struct Plan {
   size_t pack = 0;
   size_t slab = 0, slab_bytes = 0;  // split-K slabs of the weight-gradient GEMMs
   size_t flag = 0;                  // int32 non-finite-loss bitmask (bit i: modality i)
+  size_t pack8 = 0;                 // MX-fp8 weight copies (precision fp8)
   std::vector<ActLM> act;  // [L*M]
   size_t xemb[MAXM];
   size_t lnf16[MAXM], meanf[MAXM], rstdf[MAXM], hh[MAXM], dlog[MAXM];
@@ -107,6 +115,13 @@ struct mmt_ctx {
   // weight packing
   std::vector<PackSeg> segs;
   std::vector<int> tasks;
+  // MX-fp8 weight copies (precision fp8): quantisation segments and the fp8 pack region size
+  std::vector<MxSeg> mxsegs;
+  int64_t pack8_bytes = 0;
+  int mx_units = 0;
+  MxSeg* d_mxsegs = nullptr;
+  int tables_device = -1;
+  bool fp8 = false;
   int64_t pack_elems = 0;
   PackSeg* d_segs = nullptr;
   int* d_tasks = nullptr;
@@ -319,6 +334,29 @@ void build_layout(mmt_ctx* c) {
   }
   for (int i = 0; i < M; ++i) { add(c->post[i].H0); add(c->post[i].H2); }
   c->pack_elems = pk;
+  if (c->fp8) {
+    // MX-fp8 copies of the weights of the fp8 forward GEMMs (Q/K/V stage 1, FFN, cross query)
+    int64_t b8 = 0;
+    auto add8 = [&](Mat& m) {
+      if (m.off < 0 || m.rows == 0) return;
+      m.ld8 = (int)rup(m.cols, 16);
+      m.lds8 = (int)rup((m.cols + 31) / 32, 4);
+      m.pk8 = b8;
+      b8 += rup((int64_t)m.rows * m.ld8, 256);
+      m.ps8 = b8;
+      b8 += rup((int64_t)m.rows * m.lds8, 256);
+      MxSeg sg{};
+      sg.src = m.off; sg.dst = m.pk8; sg.sdst = m.ps8; sg.rows = m.rows; sg.cols = m.cols; sg.ld_src = m.cols;
+      sg.ld8 = m.ld8; sg.lds8 = m.lds8;
+      c->mxsegs.push_back(sg);
+      c->mx_units = std::max(c->mx_units, m.rows * m.lds8);
+    };
+    for (auto& x : c->lm) {
+      add8(x.W1); add8(x.F0); add8(x.F2);
+      if (x.cross) add8(x.Wq);
+    }
+    c->pack8_bytes = b8;
+  }
   for (int i = 0; i < M; ++i) {
     c->ldv[i] = r8(c->V[i]);
     c->ldvh[i] = r8(c->V[i] / 2);
@@ -342,6 +380,7 @@ void make_plan(mmt_ctx* c, int B) {
   const size_t mbytes = c->cfg.dropout > 0.f ? (size_t)mmt_attn_mask_dwords(B, H, c->T) * 4 : 0;
   p.pack = A((size_t)c->pack_elems * b2);
   p.flag = A(256);
+  p.pack8 = c->fp8 ? A((size_t)c->pack8_bytes) : 0;
   p.act.resize((size_t)c->L * M);
   for (int i = 0; i < M; ++i) p.xemb[i] = A(R * C * f4);
   for (int l = 0; l < c->L; ++l)
@@ -355,6 +394,13 @@ void make_plan(mmt_ctx* c, int B) {
       a.f = A(R * 4 * C * b2); a.x2 = A(R * C * f4);
       a.x2h = c->any_cross ? A(R * C * b2) : 0;
       a.dm = mbytes ? A(mbytes) : 0;
+      if (c->fp8) {
+        const int ldsC = (int)rup(C / 32, 4), ldsF = (int)rup(4 * C / 32, 4);
+        a.a8 = A(R * C); a.c8 = A(R * C); a.f8 = A(R * 4 * C);
+        if (x.cross) a.d8 = A(R * C);
+        a.as8 = A(R * ldsC); a.cs8 = A(R * ldsC); a.fs8 = A(R * ldsF);
+        if (x.cross) a.ds8 = A(R * ldsC);
+      }
       if (x.cross) {
         a.d = A(R * C * b2); a.meanc = A(R * f4); a.rstdc = A(R * f4); a.qc = A(R * C * b2);
         for (int j = 0; j < M - 1; ++j) {
@@ -509,6 +555,16 @@ void attn_cost(const AttnBatch& ab, int B, int T, int H, int hs, bool bwd, bool 
   }
 }
 
+// MX-fp8 forward linear: A = e4m3fn activations [R, K] (lda bytes) + exponents, B = the weight's
+// MX-fp8 copy in the fp8 pack region
+GemmProblem gp_f8(const uint8_t* X8, int ldx, const uint8_t* Xs, int ldxs, const uint8_t* w8, const Mat& W, int R) {
+  GemmProblem g{};
+  g.A = reinterpret_cast<const bf16_t*>(X8); g.lda = ldx; g.sa = Xs; g.lds_a = ldxs;
+  g.B = reinterpret_cast<const bf16_t*>(w8 + W.pk8); g.ldb = W.ld8; g.sb = w8 + W.ps8; g.lds_b = W.lds8;
+  g.M = R; g.N = W.rows; g.K = W.cols; g.alpha = 1.f;
+  return g;
+}
+
 // dropout sites (model.py:69 SA probabilities, :91 SA projection, :151 CA probabilities,
 // :116 CA projection, :171 FFN output); one hash key per (seed, layer, modality, site)
 enum DropSite { DS_SA_PROB = 0, DS_SA_PROJ = 1, DS_FFN = 2, DS_CA_PROB = 3, DS_CA_PROJ = 4 };
@@ -560,6 +616,18 @@ struct Runner {
     e.flops = flops;
     e.bytes = bytes;
     hipEventRecord(e.b, st);
+  }
+  // MX-fp8 forward GEMM (precision fp8): A / B e4m3fn + E8M0 (mmt_launch_gemm_f8)
+  void gemm8(const GemmBatch& b, int epi, const char* what) {
+    if (rc != MMT_OK) return;
+    const int id = probe_begin(what, s);
+    ok(mmt_launch_gemm_f8(b, epi, s), what);
+    if (id >= 0) {
+      double fl = 0, by = 0;
+      gemm_cost(b, epi, &fl, &by);
+      for (int g = 0; g < b.count; ++g) by -= ((double)b.p[g].M + b.p[g].N) * b.p[g].K;  // 1-byte operands
+      probe_end(id, s, fl, by);
+    }
   }
   void gemm(const GemmBatch& b, bool akc, bool bkc, int epi, int splits, const char* what) {
     if (rc != MMT_OK) return;
@@ -681,6 +749,25 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   if (!r.ok(mmt_launch_pack(c->d_segs, (int)c->segs.size(), (int64_t)c->tasks.size() / 2, c->d_tasks, r.params, wpk,
                             r.s), "pack"))
     return r.rc;
+  const bool f8 = c->fp8;
+  uint8_t* w8 = f8 ? r.W<uint8_t>(p.pack8) : nullptr;
+  const int ldsC = (int)rup(C / 32, 4), ldsF = (int)rup(4 * C / 32, 4);
+  if (f8) {
+    r.ok(mmt_launch_mx_quant(c->d_mxsegs, (int)c->mxsegs.size(), c->mx_units, r.params, w8, r.s), "mx_quant");
+    if ((C / 32) % 4) {  // exponent bytes past C/32 of a row: finite (127) for the K-step that straddles C
+      for (int l = 0; l < c->L; ++l)
+        for (int i = 0; i < M; ++i) {
+          const ActLM& a = p.act[(size_t)l * M + i];
+          r.ok(hipMemsetAsync(r.W<uint8_t>(a.as8), 127, (size_t)R * ldsC, r.s), "memset exps");
+          r.ok(hipMemsetAsync(r.W<uint8_t>(a.cs8), 127, (size_t)R * ldsC, r.s), "memset exps");
+          if (c->lm[(size_t)l * M + i].cross) r.ok(hipMemsetAsync(r.W<uint8_t>(a.ds8), 127, (size_t)R * ldsC, r.s), "memset exps");
+        }
+    }
+  }
+  auto ln8 = [&](LnProblem& q, size_t y8, size_t s8) {
+    if (!f8) return;
+    q.y8 = r.W<uint8_t>(y8); q.s8 = r.W<uint8_t>(s8); q.ld8 = C; q.lds8 = ldsC;
+  };
   {
     EmbBatch eb{};
     eb.count = M;
@@ -702,14 +789,17 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
     for (int i = 0; i < M; ++i) {
       lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].beta = r.P(x[i].ln1b);
       lb.p[i].y = r.W<bf16_t>(a[i].a); lb.p[i].mean = r.W<float>(a[i].mean1); lb.p[i].rstd = r.W<float>(a[i].rstd1);
+      ln8(lb.p[i], a[i].a8, a[i].as8);
     }
     r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "ln1_fwd");
     GemmBatch g{}; g.count = M;
     for (int i = 0; i < M; ++i) {
-      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].a), C, wpk, x[i].W1, R);
+      g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].a8), C, r.W<uint8_t>(a[i].as8), ldsC, w8, x[i].W1, R)
+                  : gp_fwd(r.W<bf16_t>(a[i].a), C, wpk, x[i].W1, R);
       g.p[i].bias = r.P(x[i].b1); g.p[i].o16 = r.W<bf16_t>(a[i].h1); g.p[i].ldo16 = ldh1;
     }
-    r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "qkv1");
+    if (f8) r.gemm8(g, EPI_BIAS_TANH_BF16, "qkv1");
+    else r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "qkv1");
     Qkv2Batch qb{}; qb.count = M;
     for (int i = 0; i < M; ++i) {
       qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].out = r.W<bf16_t>(a[i].qkv);
@@ -745,21 +835,27 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
     for (int i = 0; i < M; ++i) {
       lb.p[i].x = r.W<float>(a[i].x1); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].beta = r.P(x[i].ln2b);
       lb.p[i].y = r.W<bf16_t>(a[i].c); lb.p[i].mean = r.W<float>(a[i].mean2); lb.p[i].rstd = r.W<float>(a[i].rstd2);
+      ln8(lb.p[i], a[i].c8, a[i].cs8);
     }
     r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "ln2_fwd");
     for (int i = 0; i < M; ++i) {
-      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].c), C, wpk, x[i].F0, R);
+      g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].c8), C, r.W<uint8_t>(a[i].cs8), ldsC, w8, x[i].F0, R)
+                  : gp_fwd(r.W<bf16_t>(a[i].c), C, wpk, x[i].F0, R);
       g.p[i].bias = r.P(x[i].bf0); g.p[i].o16 = r.W<bf16_t>(a[i].f); g.p[i].ldo16 = 4 * C;
+      if (f8) { g.p[i].o8 = r.W<uint8_t>(a[i].f8); g.p[i].ld8 = 4 * C; g.p[i].s8 = r.W<uint8_t>(a[i].fs8); g.p[i].lds8 = ldsF; }
     }
-    r.gemm(g, true, true, EPI_BIAS_RELU_BF16, 1, "ffn0");
+    if (f8) r.gemm8(g, EPI_BIAS_RELU_BF16, "ffn0");
+    else r.gemm(g, true, true, EPI_BIAS_RELU_BF16, 1, "ffn0");
     for (int i = 0; i < M; ++i) {
-      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].f), 4 * C, wpk, x[i].F2, R);
+      g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].f8), 4 * C, r.W<uint8_t>(a[i].fs8), ldsF, w8, x[i].F2, R)
+                  : gp_fwd(r.W<bf16_t>(a[i].f), 4 * C, wpk, x[i].F2, R);
       g.p[i].bias = r.P(x[i].bf2); g.p[i].resid = r.W<float>(a[i].x1); g.p[i].ldres = C;
       g.p[i].o32 = r.W<float>(a[i].x2); g.p[i].ldc = C;
       if (c->any_cross) { g.p[i].o16 = r.W<bf16_t>(a[i].x2h); g.p[i].ldo16 = C; }
       r.set_drop(g.p[i], l, i, DS_FFN);
     }
-    r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "ffn2");
+    if (f8) r.gemm8(g, EPI_BIAS_RESID_F32, "ffn2");
+    else r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "ffn2");
     std::vector<const float*> xout(M);
     for (int i = 0; i < M; ++i) xout[i] = r.W<float>(a[i].x2);
     if (c->any_cross) {
@@ -771,11 +867,14 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         const int i = cx[u];
         lc.p[u].x = r.W<float>(a[i].x2); lc.p[u].gamma = r.P(x[i].lncw); lc.p[u].beta = r.P(x[i].lncb);
         lc.p[u].y = r.W<bf16_t>(a[i].d); lc.p[u].mean = r.W<float>(a[i].meanc); lc.p[u].rstd = r.W<float>(a[i].rstdc);
-        gq.p[u] = gp_fwd(r.W<bf16_t>(a[i].d), C, wpk, x[i].Wq, R);
+        ln8(lc.p[u], a[i].d8, a[i].ds8);
+        gq.p[u] = f8 ? gp_f8(r.W<uint8_t>(a[i].d8), C, r.W<uint8_t>(a[i].ds8), ldsC, w8, x[i].Wq, R)
+                     : gp_fwd(r.W<bf16_t>(a[i].d), C, wpk, x[i].Wq, R);
         gq.p[u].o16 = r.W<bf16_t>(a[i].qc); gq.p[u].ldo16 = C;
       }
       r.ok(mmt_launch_ln_fwd(lc, R, C, r.s), "lnc_fwd");
-      r.gemm(gq, true, true, EPI_STORE_BF16, 1, "ca_q");
+      if (f8) r.gemm8(gq, EPI_STORE_BF16, "ca_q");
+      else r.gemm(gq, true, true, EPI_STORE_BF16, 1, "ca_q");
       // KV projections of the other modalities' post-FFN states, grouped up to 8 per launch
       GemmBatch gk{}; gk.count = 0;
       for (int i : cx) {
@@ -1325,15 +1424,32 @@ int check_cfg(const mmt_config* cfg, std::string& msg) {
   for (int i = 0; i < M; ++i)
     if (cfg->vocab_sizes[i] < 1) { msg = "vocab sizes must be >= 1"; return MMT_ERR_INVALID; }
   if (cfg->dropout < 0.f || cfg->dropout >= 1.f) { msg = "dropout must be in [0, 1)"; return MMT_ERR_INVALID; }
+  if (cfg->precision != 0 && cfg->precision != 1) { msg = "precision must be 0 (bf16) or 1 (fp8)"; return MMT_ERR_INVALID; }
+  if (cfg->precision == 1 && cfg->n_embd % 32) {
+    msg = "precision fp8 needs n_embd % 32 == 0 (MX blocks of 32 along every fp8 GEMM's K)"; return MMT_ERR_UNSUPPORTED;
+  }
   return MMT_OK;
 }
 
 int ensure_device_tables(mmt_ctx* c) {
-  if (c->d_segs || c->segs.empty()) return MMT_OK;
+  // the pack tables live on the device of the caller's current stream (rebuilt when the
+  // model moves to another device)
+  int dev = -1;
+  HIPCHK(c, hipGetDevice(&dev));
+  if (c->d_segs && c->tables_device == dev) return MMT_OK;
+  if (c->d_segs) { (void)hipFree(c->d_segs); c->d_segs = nullptr; }
+  if (c->d_tasks) { (void)hipFree(c->d_tasks); c->d_tasks = nullptr; }
+  if (c->d_mxsegs) { (void)hipFree(c->d_mxsegs); c->d_mxsegs = nullptr; }
+  if (c->segs.empty()) return MMT_OK;
   HIPCHK(c, hipMalloc(&c->d_segs, sizeof(PackSeg) * c->segs.size()));
   HIPCHK(c, hipMalloc(&c->d_tasks, sizeof(int) * c->tasks.size()));
   HIPCHK(c, hipMemcpy(c->d_segs, c->segs.data(), sizeof(PackSeg) * c->segs.size(), hipMemcpyHostToDevice));
   HIPCHK(c, hipMemcpy(c->d_tasks, c->tasks.data(), sizeof(int) * c->tasks.size(), hipMemcpyHostToDevice));
+  if (!c->mxsegs.empty()) {
+    HIPCHK(c, hipMalloc(&c->d_mxsegs, sizeof(MxSeg) * c->mxsegs.size()));
+    HIPCHK(c, hipMemcpy(c->d_mxsegs, c->mxsegs.data(), sizeof(MxSeg) * c->mxsegs.size(), hipMemcpyHostToDevice));
+  }
+  c->tables_device = dev;
   return MMT_OK;
 }
 
@@ -1347,6 +1463,8 @@ void ensure_side(mmt_ctx* c) {
   int dev = -1;
   if (!use_side || hipGetDevice(&dev) != hipSuccess || (c->side && c->side_device == dev)) return;
   if (c->side) (void)hipStreamDestroy(c->side);
+  for (auto& e : c->evpool) (void)hipEventDestroy(e);  // events of the previous device
+  c->evpool.clear();
   c->side = nullptr;
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
   c->side_device = dev;
@@ -1381,6 +1499,7 @@ mmt_ctx* mmt_create(const mmt_config* cfg) {
     if (cfg->cross_attention[i] && c->M > 1) { c->any_cross = true; ++c->ncross; }
   }
   if (c->M - 1 > MMT_MAX_STREAMS) { g_create_err = "too many KV streams"; delete c; return nullptr; }
+  c->fp8 = cfg->precision == 1;
   build_layout(c);
   return c;
 }
@@ -1389,6 +1508,7 @@ void mmt_destroy(mmt_ctx* c) {
   if (!c) return;
   if (c->d_segs) (void)hipFree(c->d_segs);
   if (c->d_tasks) (void)hipFree(c->d_tasks);
+  if (c->d_mxsegs) (void)hipFree(c->d_mxsegs);
   for (auto& e : c->probe_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);

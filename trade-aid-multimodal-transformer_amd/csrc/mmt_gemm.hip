@@ -220,6 +220,8 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
                             EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16;
   // fused bias gradient (bf16-output epilogues): column sums of the stored values
   constexpr bool CAN_DB = EPI == EPI_STORE_BF16 || EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
+  // MX-fp8 copy of a forward activation (P.o8; needs N % 32 == 0 and the vector path)
+  constexpr bool MX_OUT = EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_STORE_BF16;
   const bool want_db = CAN_DB && P.dbias != nullptr;
   // 16-B vector accesses need bf16 leading dimensions % 8 and fp32 ones % 4 (bias pointers are
   // 64-B aligned by the parameter layout)
@@ -327,6 +329,20 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
         } else {
           *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
               u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+          if (MX_OUT && P.o8) {
+            // MX-fp8 copy: the 32-column block of this row is 4 consecutive threads (c8 & ~3)
+            float am = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(r[e]));
+            am = fmaxf(am, __shfl_xor(am, 1, 64));
+            am = fmaxf(am, __shfl_xor(am, 2, 64));
+            const int ex = mx_exp(am);
+            const float inv = mx_inv(ex);
+            *reinterpret_cast<u32x2*>(P.o8 + (int64_t)m * P.ld8 + n) =
+                u32x2{pack4fp8(r[0] * inv, r[1] * inv, r[2] * inv, r[3] * inv),
+                      pack4fp8(r[4] * inv, r[5] * inv, r[6] * inv, r[7] * inv)};
+            if ((c8 & 3) == 0) P.s8[(int64_t)m * P.lds8 + (n >> 5)] = (uint8_t)(ex + 127);
+          }
           if (CAN_DB) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) cs[e] += r[e];
@@ -504,6 +520,135 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
         }
       }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MX-fp8 forward GEMM (C4's fp8 path): Y = X W^T with X [M][K], W [N][K] e4m3fn bytes and E8M0
+// block exponents per 32 K elements, on v_mfma_scale_f32_32x32x64_f8f6f4 (2x the bf16 MFMA rate).
+// Same structure as gemm_kernel (SWAP layout, LDS-DMA ring, XCD tile order, fused epilogues); a
+// K-step is 128 fp8 = the 128-B image rows of the bf16 kernel's 64-element step, so the image
+// geometry and swizzle are unchanged. Operand lane map (probed on gfx950: tools/probe/probe_mx.py):
+// lane r + 32h of a 64-deep MFMA holds K elements [16h, 16h+16) and [32+16h, 48+16h) of row r in
+// its 32 bytes, and its scale byte is the exponent of block h (K elements [32h, 32h+32)) of row r
+// -> image chunks 4s + h and 4s + 2 + h, scale byte 2s + h of the row's K-step dword.
+// ---------------------------------------------------------------------------------------------
+template <int ROWS, int NW>
+__device__ __forceinline__ void issue_tile_f8(const i32x4& rsrc, char* img, int ld, int rows_total, int K, int r0,
+                                              int k0, int wave, int lane) {
+  constexpr int PPW = ROWS * 128 / 1024 / NW;  // 1-KiB pieces per wave: 8 rows of 128 B
+#pragma unroll
+  for (int u = 0; u < PPW; ++u) {
+    const int i = wave * PPW + u;
+    const int row = 8 * i + lane / 8;
+    const int chunk = kc_swz<64>(lane % 8, row);
+    const int grow = r0 + row, gk = k0 + chunk * 16;
+    const int voff = (grow < rows_total && gk < K) ? grow * ld + gk : 0x7fffffff;
+    dma16(rsrc, __builtin_amdgcn_readfirstlane(lds_u32(img + i * 1024)), voff);
+  }
+}
+
+__device__ __forceinline__ i32x8 frag_f8(const char* img, int sb, int s, int lane) {
+  const int row = sb + (lane & 31), h = lane >> 5;
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(img + row * 128 + kc_swz<64>(4 * s + h, row) * 16);
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(img + row * 128 + kc_swz<64>(4 * s + 2 + h, row) * 16);
+  return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+
+template <class TL, int EPI>
+__global__ __launch_bounds__(TL::NT) void gemm_f8_kernel(GemmBatch batch) {
+  constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
+  constexpr int ST = 2, KS = 128;                           // stages, K elements per step
+  constexpr int IMG_A = GBM * 128, IMG_B = GBN * 128, STAGE_BYTES = IMG_A + IMG_B;
+  const GemmProblem& P = batch.p[blockIdx.z];
+  const int M = P.M, N = P.N, K = P.K;
+  const int tiles_n = (N + GBN - 1) / GBN, tiles_m = (M + GBM - 1) / GBM;
+  int tile = blockIdx.x;
+  {
+    const int nwg = gridDim.x;
+    const int x = tile % 8, q = nwg / 8, rr = nwg % 8;
+    tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + tile / 8;
+  }
+  if (tile >= tiles_m * tiles_n) return;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int nk = (K + KS - 1) / KS;
+  constexpr int EPI_ROWS = GBM == 128 ? 128 : 64;
+  constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
+  __shared__ __attribute__((aligned(1024))) char lds[RING > CTILE ? RING : CTILE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int h = lane >> 5, r = lane & 31;
+  f32x16 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+  const i32x4 ra = make_rsrc(P.A, (int64_t)M * P.lda);
+  const i32x4 rb = make_rsrc(P.B, (int64_t)N * P.ldb);
+  // E8M0 dwords (4 blocks = one K-step) of this lane's rows of the A / B sub-tiles: buffer loads
+  // from one SGPR descriptor per operand, one 32-bit row offset each (rows past M / N read the
+  // descriptor's zero fill: exponent byte 0 = 2^-127 on zero-filled values)
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(P.sa), (short)0, (int)std::min<int64_t>((int64_t)M * P.lds_a, 0x7ffffff0), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(P.sb), (short)0, (int)std::min<int64_t>((int64_t)N * P.lds_b, 0x7ffffff0), 0x00020000);
+  const int sa_row = (m0 + wm * TM * 32 + r) * P.lds_a, sb_row = (n0 + wn * TN * 32 + r) * P.lds_b;
+  uint32_t sa_cur[TM], sb_cur[TN];
+  auto load_scales = [&](int t, uint32_t (&sa)[TM], uint32_t (&sb)[TN]) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+      sa[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsa, sa_row + 32 * j * P.lds_a, 4 * t, 0);
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+      sb[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsb, sb_row + 32 * i * P.lds_b, 4 * t, 0);
+  };
+  load_scales(0, sa_cur, sb_cur);
+  issue_tile_f8<GBM, NW>(ra, lds, P.lda, M, K, m0, 0, wave, lane);
+  issue_tile_f8<GBN, NW>(rb, lds + IMG_A, P.ldb, N, K, n0, 0, wave, lane);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage t landed for every wave; stage t-1's reads are done
+    uint32_t sa_nxt[TM], sb_nxt[TN];
+    if (t + 1 < nk) {
+      load_scales(t + 1, sa_nxt, sb_nxt);
+      char* st = lds + ((t + 1) & 1) * STAGE_BYTES;
+      issue_tile_f8<GBM, NW>(ra, st, P.lda, M, K, m0, (t + 1) * KS, wave, lane);
+      issue_tile_f8<GBN, NW>(rb, st + IMG_A, P.ldb, N, K, n0, (t + 1) * KS, wave, lane);
+    }
+    const char* imgA = lds + (t & 1) * STAGE_BYTES;
+    const char* imgB = imgA + IMG_A;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      // B fragments for the sub-step, A fragments one at a time (32-byte fragments: all TM + TN
+      // of them live at once spill the 256-register budget of the 256x256 tile)
+      i32x8 fb[TN];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[i] = frag_f8(imgB, wn * TN * 32 + 32 * i, s, lane);
+      const int sh = 8 * (2 * s + h);
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const i32x8 fa = frag_f8(imgA, wm * TM * 32 + 32 * j, s, lane);
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[i], fa, acc[i][j], 0, 0, 0,
+                                                                       (int)(sb_cur[i] >> sh), 0,
+                                                                       (int)(sa_cur[j] >> sh));
+      }
+    }
+    if (t + 1 < nk) {
+#pragma unroll
+      for (int j = 0; j < TM; ++j) sa_cur[j] = sa_nxt[j];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) sb_cur[i] = sb_nxt[i];
+    }
+  }
+  float alpha = P.alpha;
+  if (P.alpha_ptr) alpha *= *P.alpha_ptr;
+  epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, P.o32, alpha, m0, n0, tid, lane, wave);
 }
 
 template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
@@ -745,3 +890,40 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
 
 
 bool mmt_gemm_wgrad_big(const GemmBatch& b) { return use_big(b); }
+
+template <class TL, int EPI>
+static hipError_t launch_f8(const GemmBatch& b, hipStream_t s) {
+  int mt = 0;
+  for (int g = 0; g < b.count; ++g)
+    mt = std::max(mt, ((b.p[g].M + TL::BM - 1) / TL::BM) * ((b.p[g].N + TL::BN - 1) / TL::BN));
+  if (mt == 0) return hipSuccess;
+  hipLaunchKernelGGL((gemm_f8_kernel<TL, EPI>), dim3(mt, 1, b.count), dim3(TL::NT), 0, s, b);
+  return hipGetLastError();
+}
+
+template <int EPI>
+static hipError_t launch_f8_tile(const GemmBatch& b, hipStream_t s) {
+  // 128x128 tiles only: the 256x256 form's 32-byte fragments + E8M0 dwords spill (hipcc, 256
+  // registers at 2 waves per SIMD)
+  return launch_f8<TileS, EPI>(b, s);
+}
+
+hipError_t mmt_launch_gemm_f8(const GemmBatch& b, int epi, hipStream_t s) {
+  if (b.count == 0) return hipSuccess;
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& P = b.p[g];
+    if ((P.K & 31) || (P.lda & 15) || (P.ldb & 15) || (((uintptr_t)P.A | (uintptr_t)P.B) & 15) || (P.lds_a & 3) ||
+        (P.lds_b & 3) || (((uintptr_t)P.sa | (uintptr_t)P.sb) & 3) || P.lds_a * 32 < P.K || P.lds_b * 32 < P.K)
+      return hipErrorInvalidValue;
+    if (P.o8 && ((P.N & 31) || (P.ld8 & 7) || ((uintptr_t)P.o8 & 7))) return hipErrorInvalidValue;
+  }
+  switch (epi) {
+    case EPI_STORE_BF16: return launch_f8_tile<EPI_STORE_BF16>(b, s);
+    case EPI_BIAS_TANH_BF16: return launch_f8_tile<EPI_BIAS_TANH_BF16>(b, s);
+    case EPI_BIAS_RELU_BF16: return launch_f8_tile<EPI_BIAS_RELU_BF16>(b, s);
+    case EPI_BIAS_RESID_F32: return launch_f8_tile<EPI_BIAS_RESID_F32>(b, s);
+    case EPI_STORE_F32: return launch_f8_tile<EPI_STORE_F32>(b, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+

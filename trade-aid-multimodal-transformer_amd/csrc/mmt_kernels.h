@@ -50,6 +50,16 @@ struct GemmProblem {
   float* dbias;
   // split-K slabs: split s writes o32 + s * split_stride (elements); 0 = one output
   int64_t split_stride;
+  // MX-fp8 (mmt_launch_gemm_f8): A and B hold e4m3fn bytes (lda / ldb in bytes = elements) and
+  // these their E8M0 block exponents, one byte per 32 K elements (row stride in bytes, % 4 == 0)
+  const uint8_t* sa;
+  const uint8_t* sb;
+  int lds_a, lds_b;
+  // optional MX-fp8 copy of a bf16-output epilogue (the next fp8 GEMM's A operand): e4m3fn bytes
+  // [M][ld8] and block exponents [M][lds8] over 32 consecutive output columns
+  uint8_t* o8;
+  uint8_t* s8;
+  int ld8, lds8;
 };
 
 struct GemmBatch {
@@ -61,6 +71,10 @@ hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, in
 // weight gradients o32 += alpha * A^T B over K rows (both operands MN-contiguous): split-K into fp32
 // slabs in `slab` (capacity slab_bytes) + one reduce pass; without room, one K pass accumulating
 hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_bytes, hipStream_t s);
+// forward linear Y = X W^T on MX-fp8 operands (A = X [M][K], B = W [N][K], both K-contiguous e4m3fn
+// with E8M0 exponents per 32 K elements; K % 32 == 0) via v_mfma_scale_f32_32x32x64_f8f6f4, any
+// of the bf16 GEMM's forward epilogues; fp32 accumulation
+hipError_t mmt_launch_gemm_f8(const GemmBatch& b, int epi, hipStream_t s);
 // whether a weight-gradient batch runs on the 256x256 tile (launches can only be merged when equal)
 bool mmt_gemm_wgrad_big(const GemmBatch& b);
 
@@ -74,6 +88,11 @@ struct LnProblem {
   bf16_t* y;            // [R, C] (ld = C)
   float* mean;          // [R]
   float* rstd;          // [R]
+  // optional MX-fp8 copy of y (an fp8 GEMM's A operand): e4m3fn [R][ld8], E8M0 [R][lds8] per 32
+  // columns (C % 32 == 0)
+  uint8_t* y8;
+  uint8_t* s8;
+  int ld8, lds8;
   // backward
   const float* dy;      // [R, C] fp32
   float* dx;            // [R, C] fp32, ACCUMULATED (dx += ...)
@@ -212,6 +231,19 @@ struct PackSeg { int64_t src_off; int64_t dst_off; int rows; int cols; int dld; 
 hipError_t mmt_launch_pack(const PackSeg* segs_dev, int nseg, int64_t ntasks, const int* task_dev, const float* src,
                            bf16_t* dst, hipStream_t s);
 hipError_t mmt_launch_f32_to_bf16(const float* src, bf16_t* dst, int64_t n, hipStream_t s);
+
+// MX-fp8 quantisation of fp32 matrices [rows][cols] (row stride ld_src, cols % 32 == 0): e4m3fn
+// bytes [rows][ld8] and E8M0 exponents [rows][lds8] per 32 columns; exponent bytes past cols/32 up
+// to lds8 are written as 127 (2^0) so a K-step that straddles the end reads finite scales
+struct MxSeg {
+  int64_t src;   // fp32 element offset of the matrix in `base`
+  int64_t dst;   // byte offset of the e4m3fn matrix
+  int64_t sdst;  // byte offset of the exponent matrix
+  int rows, cols, ld_src, ld8, lds8;
+};
+hipError_t mmt_launch_mx_quant(const MxSeg* segs_dev, int nseg, int max_units, const float* base, uint8_t* dst,
+                               hipStream_t s);
+hipError_t mmt_launch_mx_quant1(const MxSeg& S, const float* base, uint8_t* dst, hipStream_t s);
 // dst = bf16(mask * src) over row-major [R, C] (mask as in LnProblem), dsum[c] += column sums
 struct DropCopyProblem {
   const float* src;

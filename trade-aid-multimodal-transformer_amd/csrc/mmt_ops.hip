@@ -158,3 +158,43 @@ int mmt_op_embedding_bwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t 
 }
 
 }  // extern "C"
+
+// ---- MX-fp8 (C4's fp8 path) -------------------------------------------------------------------
+int mmt_op_mx_quant(void* stream, int32_t rows, int32_t cols, const float* src, int32_t ld_src, void* dst8,
+                    int32_t ld8, void* s8, int32_t lds8) {
+  if (rows < 0 || cols < 0 || (cols & 31) || (ld_src & 3) || (ld8 & 15) || lds8 * 32 < cols || !src || !dst8 || !s8)
+    return MMT_ERR_INVALID;
+  // one "base" for source and destinations: offsets relative to the source / destination pointers
+  MxSeg S{};
+  S.src = 0; S.dst = 0; S.sdst = (const uint8_t*)s8 - (const uint8_t*)dst8;
+  S.rows = rows; S.cols = cols; S.ld_src = ld_src; S.ld8 = ld8; S.lds8 = lds8;
+  return st(mmt_launch_mx_quant1(S, src, (uint8_t*)dst8, (hipStream_t)stream));
+}
+
+int mmt_op_gemm_f8(void* stream, int32_t epi, int32_t M, int32_t N, int32_t K, const void* A8, int32_t lda,
+                   const void* sa, int32_t lds_a, const void* B8, int32_t ldb, const void* sb, int32_t lds_b,
+                   const float* bias, const float* resid, int32_t ldres, float* o32, int32_t ldc, void* o16,
+                   int32_t ldo16, void* o8, int32_t ld8, void* s8, int32_t lds8) {
+  GemmBatch b{};
+  b.count = 1;
+  GemmProblem& p = b.p[0];
+  p.A = (const bf16_t*)A8; p.lda = lda; p.B = (const bf16_t*)B8; p.ldb = ldb;
+  p.sa = (const uint8_t*)sa; p.lds_a = lds_a; p.sb = (const uint8_t*)sb; p.lds_b = lds_b;
+  p.bias = bias; p.resid = resid; p.ldres = ldres; p.o32 = o32; p.ldc = ldc; p.o16 = (bf16_t*)o16; p.ldo16 = ldo16;
+  p.o8 = (uint8_t*)o8; p.ld8 = ld8; p.s8 = (uint8_t*)s8; p.lds8 = lds8;
+  p.M = M; p.N = N; p.K = K; p.alpha = 1.f;
+  const hipError_t e = mmt_launch_gemm_f8(b, epi, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return MMT_ERR_UNSUPPORTED;
+  return st(e);
+}
+
+int mmt_op_layernorm_fwd_f8(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
+                            void* y16, float* mean, float* rstd, void* y8, int32_t ld8, void* s8, int32_t lds8) {
+  if (C & 31) return MMT_ERR_UNSUPPORTED;
+  LnBatch b{};
+  b.count = 1;
+  LnProblem& p = b.p[0];
+  p.x = x; p.gamma = gamma; p.beta = beta; p.y = (bf16_t*)y16; p.mean = mean; p.rstd = rstd;
+  p.y8 = (uint8_t*)y8; p.ld8 = ld8; p.s8 = (uint8_t*)s8; p.lds8 = lds8;
+  return st(mmt_launch_ln_fwd(b, R, C, (hipStream_t)stream));
+}

@@ -36,6 +36,7 @@ class MmtConfig(ctypes.Structure):
         ("cross_attention", c_i32 * MAX_MOD),
         ("dropout", c_f32),
         ("seed", ctypes.c_uint64),
+        ("precision", c_i32),
     ]
 
 
@@ -96,6 +97,11 @@ _SIGS = {
     "mmt_op_cross_entropy": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "mmt_op_embedding_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mmt_op_embedding_bwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "mmt_op_mx_quant": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32]),
+    "mmt_op_gemm_f8": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32,
+                               c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32]),
+    "mmt_op_layernorm_fwd_f8": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp,
+                                        c_i32]),
 }
 
 EXPORTED = sorted(_SIGS)

@@ -32,7 +32,7 @@ import torch
 import torch.nn as nn
 
 import mmt_lib as ML
-from config_utils import _get_block_size, _get_dropout, _get_n_embd, _get_n_head, _get_n_layer
+from config_utils import _get_block_size, _get_dropout, _get_n_embd, _get_n_head, _get_n_layer, _get_precision
 
 
 class _MmtStep(torch.autograd.Function):
@@ -88,6 +88,8 @@ class MultimodalTransformer(nn.Module):
             cfg.cross_attention[i] = 1 if all_modality_params[i][8] else 0  # model.py:196
         cfg.dropout = self.dropout_p
         cfg.seed = 0
+        self.precision = _get_precision()
+        cfg.precision = 1 if self.precision == "fp8" else 0
         L = ML.lib()
         ctx = L.mmt_create(ctypes.byref(cfg))
         if not ctx:
@@ -366,12 +368,13 @@ class MultimodalTransformer(nn.Module):
         (causal attention, absolute positions) at O(t) instead of O(block_size) attention and no
         re-run of the prompt's GEMMs. Once the sequence outgrows the block every position shifts
         and it falls back to the reference's full re-forward. use_cache=False (or training mode
-        with dropout, where the reference's forward samples dropout) always re-runs the forward."""
+        with dropout, where the reference's forward samples dropout, or the fp8 precision, whose
+        forward GEMMs the bf16 decode would not reproduce) always re-runs the forward."""
         seqs = [idx.clone() for idx in idx_list]
         T = self.block_size
         g = modality_to_generate
         sample = sample_fn or (lambda probs: torch.multinomial(probs, num_samples=1))
-        cache = (use_cache and not (self.training and self.dropout_p > 0.0)
+        cache = (use_cache and not (self.training and self.dropout_p > 0.0) and self.precision == "bf16"
                  and len({int(s.shape[1]) for s in seqs}) == 1 and all(s.dim() == 2 for s in seqs))
         cached_pos = None  # the last position whose keys / values the workspace holds
         for _ in range(max_new_tokens):
