@@ -182,6 +182,8 @@ def main():
                     help="comma-separated engine launch-label patterns timed live (roofline: the dominant one)")
     ap.add_argument("--gemm-variant", type=int, default=-1, help="GEMM pipeline variant (mmt_gemm_set_variant)")
     ap.add_argument("--bucket-mb", type=int, default=32, help="DP gradient all-reduce bucket size")
+    ap.add_argument("--precision", default=None, choices=["bf16", "fp8"],
+                    help="compute precision (default: fp8 for c4 as BASELINE configs[4] names it, else bf16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--exact-steps", type=int, default=5,
@@ -217,8 +219,10 @@ def main():
     if args.batch:
         cfg["B"] = args.batch
     M, C, H, L, T, B = cfg["M"], cfg["C"], cfg["H"], cfg["L"], cfg["T"], cfg["B"]
+    precision = args.precision or ("fp8" if args.config == "c4" else "bf16")
     config_utils._config_cache = {"n_embd": C, "n_head": H, "n_layer": L, "block_size": T, "dropout": args.dropout,
-                                  "device": str(dev), "batch_size": B, "eval_iters": 1, "learning_rate": 3e-4}
+                                  "device": str(dev), "batch_size": B, "eval_iters": 1, "learning_rate": 3e-4,
+                                  "precision": precision}
     data = mmt_data.make_synthetic(n_modalities=M)
     V = data["vocab_sizes"]
     torch.manual_seed(1234)
@@ -309,7 +313,9 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16" if precision == "bf16" else "fp8 (MX e4m3: Q/K/V stage 1, FFN, cross query) + bf16",
+        "data": "synthetic",
         "config": {"workload": WORKLOADS[args.config],
                    "model": "multimodal-transformer", "global_batch": B * world, "seq_len": T, "n_embd": C,
                    "n_head": H, "n_layer": L, "modalities": M, "vocab_sizes": V, "dropout": args.dropout,

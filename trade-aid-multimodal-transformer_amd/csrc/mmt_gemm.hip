@@ -554,11 +554,23 @@ __device__ __forceinline__ i32x8 frag_f8(const char* img, int sb, int s, int lan
   return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
 }
 
+// one 4-B-per-lane LDS-DMA (buffer_load_dword ... lds): LDS[lds_addr + 4*lane] = buffer[voff]
+__device__ __forceinline__ void dma4(const i32x4& rsrc, uint32_t lds_addr, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :
+               : "s"(lds_addr), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
 template <class TL, int EPI>
 __global__ __launch_bounds__(TL::NT) void gemm_f8_kernel(GemmBatch batch) {
   constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
   constexpr int ST = 2, KS = 128;                           // stages, K elements per step
-  constexpr int IMG_A = GBM * 128, IMG_B = GBN * 128, STAGE_BYTES = IMG_A + IMG_B;
+  constexpr int IMG_A = GBM * 128, IMG_B = GBN * 128;       // e4m3 tiles
+  constexpr int SC_A = GBM * 4, SC_B = GBN * 4;             // E8M0 dwords of the step, one per row
+  constexpr int STAGE_BYTES = IMG_A + IMG_B + SC_A + SC_B;
+  constexpr int SCDMA = (GBM + GBN) / 64;                   // dword LDS-DMAs of the exponents per stage
+  static_assert(SCDMA <= NW, "one exponent DMA per wave at most");
   const GemmProblem& P = batch.p[blockIdx.z];
   const int M = P.M, N = P.N, K = P.K;
   const int tiles_n = (N + GBN - 1) / GBN, tiles_m = (M + GBM - 1) / GBM;
@@ -588,62 +600,55 @@ __global__ __launch_bounds__(TL::NT) void gemm_f8_kernel(GemmBatch batch) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
   const i32x4 ra = make_rsrc(P.A, (int64_t)M * P.lda);
   const i32x4 rb = make_rsrc(P.B, (int64_t)N * P.ldb);
-  // E8M0 dwords (4 blocks = one K-step) of this lane's rows of the A / B sub-tiles: buffer loads
-  // from one SGPR descriptor per operand, one 32-bit row offset each (rows past M / N read the
-  // descriptor's zero fill: exponent byte 0 = 2^-127 on zero-filled values)
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(P.sa), (short)0, (int)std::min<int64_t>((int64_t)M * P.lds_a, 0x7ffffff0), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(P.sb), (short)0, (int)std::min<int64_t>((int64_t)N * P.lds_b, 0x7ffffff0), 0x00020000);
-  const int sa_row = (m0 + wm * TM * 32 + r) * P.lds_a, sb_row = (n0 + wn * TN * 32 + r) * P.lds_b;
-  uint32_t sa_cur[TM], sb_cur[TN];
-  auto load_scales = [&](int t, uint32_t (&sa)[TM], uint32_t (&sb)[TN]) {
-#pragma unroll
-    for (int j = 0; j < TM; ++j)
-      sa[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsa, sa_row + 32 * j * P.lds_a, 4 * t, 0);
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-      sb[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsb, sb_row + 32 * i * P.lds_b, 4 * t, 0);
+  const i32x4 rsa = make_rsrc(P.sa, (int64_t)M * P.lds_a);
+  const i32x4 rsb = make_rsrc(P.sb, (int64_t)N * P.lds_b);
+  // the E8M0 dwords of a K-step ride the ring next to the tiles: wave w < SCDMA brings 64 rows' dwords
+  // (rows past M / N land as zeros: exponent 2^-127 on zero-filled values)
+  auto issue_scales = [&](char* st, int t) {
+    if (wave >= SCDMA) return;
+    const bool isa = wave < GBM / 64;
+    const int row = (isa ? wave : wave - GBM / 64) * 64 + lane;
+    const int grow = (isa ? m0 : n0) + row;
+    const int voff = grow < (isa ? M : N) ? grow * (isa ? P.lds_a : P.lds_b) + 4 * t : 0x7fffffff;
+    char* dst = st + IMG_A + IMG_B + (isa ? 0 : SC_A) + (isa ? wave : wave - GBM / 64) * 256;
+    dma4(isa ? rsa : rsb, __builtin_amdgcn_readfirstlane(lds_u32(dst)), voff);
   };
-  load_scales(0, sa_cur, sb_cur);
   issue_tile_f8<GBM, NW>(ra, lds, P.lda, M, K, m0, 0, wave, lane);
   issue_tile_f8<GBN, NW>(rb, lds + IMG_A, P.ldb, N, K, n0, 0, wave, lane);
+  issue_scales(lds, 0);
   for (int t = 0; t < nk; ++t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage t landed for every wave; stage t-1's reads are done
-    uint32_t sa_nxt[TM], sb_nxt[TN];
     if (t + 1 < nk) {
-      load_scales(t + 1, sa_nxt, sb_nxt);
       char* st = lds + ((t + 1) & 1) * STAGE_BYTES;
       issue_tile_f8<GBM, NW>(ra, st, P.lda, M, K, m0, (t + 1) * KS, wave, lane);
       issue_tile_f8<GBN, NW>(rb, st + IMG_A, P.ldb, N, K, n0, (t + 1) * KS, wave, lane);
+      issue_scales(st, t + 1);
     }
     const char* imgA = lds + (t & 1) * STAGE_BYTES;
     const char* imgB = imgA + IMG_A;
+    const uint32_t* scA = reinterpret_cast<const uint32_t*>(imgB + IMG_B);
+    const uint32_t* scB = scA + GBM;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      // B fragments for the sub-step, A fragments one at a time (32-byte fragments: all TM + TN
-      // of them live at once spill the 256-register budget of the 256x256 tile)
+      // B fragments for the sub-step, A fragments one at a time (32-byte fragments)
       i32x8 fb[TN];
+      uint32_t sb[TN];
 #pragma unroll
-      for (int i = 0; i < TN; ++i) fb[i] = frag_f8(imgB, wn * TN * 32 + 32 * i, s, lane);
-      const int sh = 8 * (2 * s + h);
+      for (int i = 0; i < TN; ++i) {
+        fb[i] = frag_f8(imgB, wn * TN * 32 + 32 * i, s, lane);
+        sb[i] = scB[wn * TN * 32 + 32 * i + r] >> (8 * (2 * s + h));
+      }
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
         const i32x8 fa = frag_f8(imgA, wm * TM * 32 + 32 * j, s, lane);
+        const uint32_t sa = scA[wm * TM * 32 + 32 * j + r] >> (8 * (2 * s + h));
 #pragma unroll
         for (int i = 0; i < TN; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[i], fa, acc[i][j], 0, 0, 0,
-                                                                       (int)(sb_cur[i] >> sh), 0,
-                                                                       (int)(sa_cur[j] >> sh));
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[i], fa, acc[i][j], 0, 0, 0, (int)sb[i], 0,
+                                                                       (int)sa);
       }
-    }
-    if (t + 1 < nk) {
-#pragma unroll
-      for (int j = 0; j < TM; ++j) sa_cur[j] = sa_nxt[j];
-#pragma unroll
-      for (int i = 0; i < TN; ++i) sb_cur[i] = sb_nxt[i];
     }
   }
   float alpha = P.alpha;
@@ -903,9 +908,11 @@ static hipError_t launch_f8(const GemmBatch& b, hipStream_t s) {
 
 template <int EPI>
 static hipError_t launch_f8_tile(const GemmBatch& b, hipStream_t s) {
-  // 128x128 tiles only: the 256x256 form's 32-byte fragments + E8M0 dwords spill (hipcc, 256
-  // registers at 2 waves per SIMD)
-  return launch_f8<TileS, EPI>(b, s);
+  // the 256x256 tile where every problem fills it and K is long (as the bf16 policy), else 128x128
+  bool big = g_big_mode != 0;
+  for (int g = 0; g < b.count; ++g)
+    if (b.p[g].M < TileL::BM || b.p[g].N < TileL::BN || b.p[g].K < 2 * g_big_kmin) big = false;
+  return big ? launch_f8<TileL, EPI>(b, s) : launch_f8<TileS, EPI>(b, s);
 }
 
 hipError_t mmt_launch_gemm_f8(const GemmBatch& b, int epi, hipStream_t s) {
