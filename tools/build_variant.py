@@ -22,7 +22,7 @@ def main():
 
     def comp(src):
         o = os.path.join(out, src.replace(".hip", ".o"))
-        r = subprocess.run([B.HIPCC] + B.FLAGS + extra + ["-c", os.path.join(B.CSRC, src), "-o", o],
+        r = subprocess.run([B.HIPCC] + B.FLAGS + B.FILE_FLAGS.get(src, []) + extra + ["-c", os.path.join(B.CSRC, src), "-o", o],
                            capture_output=True, text=True)
         if r.returncode:
             raise RuntimeError(r.stderr)

@@ -83,8 +83,6 @@ __device__ __forceinline__ void zero16(f32x16& a) {
   for (int e = 0; e < 16; ++e) a[e] = 0.f;
 }
 
-// all ones iff bit b of w is set (keep-bit select for float bit patterns: v_bfe_i32)
-__device__ __forceinline__ int bit_mask(uint32_t w, int b) { return (int)(w << (31 - b)) >> 31; }
 __device__ __forceinline__ float keep_f(float v, int m) { return __int_as_float(__float_as_int(v) & m); }
 
 // dword of an S^T mask tile that holds key r's keep bits over the tile's 32 queries
@@ -174,9 +172,9 @@ struct MaskStager {
 
 __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// packed fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth per instruction)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+// Softmax / dS arithmetic is scalar fp32 on purpose: v_pk_*_f32 beside MFMAs costs more issue
+// cycles than the two scalar instructions it replaces (MI355X_MICROARCH.md, constants table), and
+// this file is compiled with -fno-slp-vectorize so the compiler does not re-pack them.
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
@@ -196,72 +194,131 @@ constexpr float kTau = 8.0f;  // lazy-rescale threshold of the forward's running
 #define MMT_DKDV1_MINB(hs) ((hs) <= 32 ? 1 : 2)
 #endif
 
-// forward: one 32x32 (keys x queries) tile of S^T, online softmax, O^T += V^T P^T
-template <int HS, bool diag, bool DROP>
-__device__ __forceinline__ void fwd_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq,
-                                         const bf16x8 (&qf)[Geo<HS>::NKS], float& m, float& l,
-                                         f32x16 (&oacc)[Geo<HS>::ND], float c2, const uint32_t* mt, int lane) {
+// cross-half reductions (lanes l and l ^ 32) in one v_permlane32_swap: no LDS round trip
+__device__ __forceinline__ float xhalf_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  float m;
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(__uint_as_float(r[0])), "v"(__uint_as_float(r[1])));
+  return m;
+}
+__device__ __forceinline__ float xhalf_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Lane word of an S^T keep tile (attn_mask_kernel): bit i = element 2i, bit 8 + i = element 2i + 1
+// of the lane's 16 accumulator elements. keep_spread moves the odd byte to bits 16..23 (one
+// v_perm_b32); pair_keep then turns pair i (the two elements one v_cvt_pk_bf16_f32 packs) into a
+// 0x0000 / 0xFFFF half mask with one shift and one packed arithmetic shift: 1.5 VALU per element
+// including the AND on the packed bf16 pair.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t keep_spread(uint32_t w16) { return __builtin_amdgcn_perm(0u, w16, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t pair_keep(uint32_t w32, int i) {
+  s16x2 v = __builtin_bit_cast(s16x2, w32 << (15 - i));
+  v = v >> (s16x2){15, 15};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// keep mask (all ones / zero) of element e of a lane word (fp32 selects in the dQ pass)
+__device__ __forceinline__ int elem_keep(uint32_t w16, int e) {
+  return __builtin_amdgcn_sbfe((int)w16, (e & 1) * 8 + (e >> 1), 1);
+}
+
+// accumulator registers 8s..8s+7 -> bf16 operand fragment, dropped elements zeroed
+__device__ __forceinline__ bf16x8 acc_frag_keep(const f32x16& a, int s, uint32_t w32) {
+  const u32x4 v = {pack2bf(a[8 * s], a[8 * s + 1]) & pair_keep(w32, 4 * s),
+                   pack2bf(a[8 * s + 2], a[8 * s + 3]) & pair_keep(w32, 4 * s + 1),
+                   pack2bf(a[8 * s + 4], a[8 * s + 5]) & pair_keep(w32, 4 * s + 2),
+                   pack2bf(a[8 * s + 6], a[8 * s + 7]) & pair_keep(w32, 4 * s + 3)};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// per query tile state of the forward walk: Q fragments, running max / sum, O^T accumulators.
+// l is this lane's HALF of the row sum (keys 4h + ..., combined across halves at the end): the
+// two halves always share m (the max is reduced across them every tile)
+template <int HS>
+struct FwdQ {
+  bf16x8 qf[Geo<HS>::NKS];
+  f32x16 o[Geo<HS>::ND];
+  float m, l;
+  int tq;
+};
+
+// online softmax of one S^T tile for one query tile (log2 domain, lazy rescale)
+template <int HS, bool diag>
+__device__ __forceinline__ void fwd_softmax(f32x16& sacc, FwdQ<HS>& q, int k0, float c2, int h) {
   using G = Geo<HS>;
-  const int r = lane & 31, h = lane >> 5;
-  const uint32_t mw = DROP ? reinterpret_cast<const uint16_t*>(mt)[lane] : 0u;  // this lane's keep bits (LDS)
-  f32x16 sacc;
-  zero16(sacc);
-#pragma unroll
-  for (int s = 0; s < G::NKS; ++s) {
-    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
-    sacc = mfma32(kf, qf[s], sacc);
-  }
   // row max on the raw scores (c2 > 0 commutes with max), then into the log2 domain
   float tmax = -INFINITY;
   if (diag) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (key > tq) sacc[e] = -INFINITY;
-      tmax = fmaxf(tmax, sacc[e]);
+      if (key > q.tq) sacc[e] = -INFINITY;
     }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) tmax = fmaxf(tmax, sacc[e]);
   }
-  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) tmax = fmaxf(tmax, sacc[e]);
+  tmax = xhalf_max(tmax) * c2;
   // lazy rescale: the running max m moves only when a tile's max exceeds it by more than kTau
   // (log2 units; always on the first tile, m = -inf). Until then exp2(s - m) <= 2^kTau keeps P, l
-  // and O comfortably in fp32/bf16 range, and the O accumulators (AGPRs at hs = 64: a read,
-  // multiply and write back per element) are not touched on the common path. l and O share m,
-  // so the normalised output and the LSE m + log2(l) are unchanged.
-  const bool up = tmax > m + kTau;
+  // and O comfortably in fp32/bf16 range and the O accumulators are not touched on the common
+  // path. l and O share m, so the normalised output and the LSE m + log2(l) are unchanged.
+  const bool up = tmax > q.m + kTau;
   if (__builtin_amdgcn_ballot_w64(up)) {  // wave-uniform
-    const float alpha = up ? ex2(m - tmax) : 1.f;
-    m = up ? tmax : m;
-    l *= alpha;
+    const float alpha = up ? ex2(q.m - tmax) : 1.f;
+    q.m = up ? tmax : q.m;
+    q.l *= alpha;
 #pragma unroll
     for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) oacc[dt][e] *= alpha;
+      for (int e = 0; e < 16; ++e) q.o[dt][e] *= alpha;
   }
-  f32x2 rs2 = {0.f, 0.f};
-  const f32x2 c2v = {c2, c2}, nm = {-m, -m};
+  const float nm = -q.m;
 #pragma unroll
-  for (int e = 0; e < 16; e += 2) {
-    const f32x2 a = pk_fma(f32x2{sacc[e], sacc[e + 1]}, c2v, nm);
-    const f32x2 pv = {ex2(a.x), ex2(a.y)};
-    sacc[e] = pv.x;
-    sacc[e + 1] = pv.y;
-    rs2 += pv;
-  }
-  float rs = rs2.x + rs2.y;
-  rs += __shfl_xor(rs, 32, 64);
-  l += rs;
-  if (DROP) {  // dropout on the probabilities (the normaliser l keeps every term; 1/(1-p) at the end)
+  for (int e = 0; e < 16; ++e) sacc[e] = ex2(__builtin_fmaf(sacc[e], c2, nm));
+  // the row sum keeps every term (dropout acts on the normalised probabilities); four partial
+  // chains, no cross-half reduction per tile
+  float r0 = sacc[0] + sacc[1], r1 = sacc[2] + sacc[3], r2 = sacc[4] + sacc[5], r3 = sacc[6] + sacc[7];
+  r0 += sacc[8] + sacc[9]; r1 += sacc[10] + sacc[11]; r2 += sacc[12] + sacc[13]; r3 += sacc[14] + sacc[15];
+  q.l += (r0 + r1) + (r2 + r3);
+}
+
+// forward step over one 32-key tile for one or two query tiles (NQ): the K fragments and the
+// transposed V fragments are read from LDS once and feed both tiles' MFMAs; the V reads are
+// issued before the softmax so their latency hides under it
+template <int HS, int NQ, bool DA, bool DB, bool DROP>
+__device__ __forceinline__ void fwd_step(const bf16_t* ks, const bf16_t* vs, int kl, int k0, FwdQ<HS>& a, FwdQ<HS>& b,
+                                         const uint32_t* mta, const uint32_t* mtb, float c2, int lane) {
+  using G = Geo<HS>;
+  const int r = lane & 31, h = lane >> 5;
+  const uint32_t wa = DROP ? keep_spread(reinterpret_cast<const uint16_t*>(mta)[lane]) : 0u;
+  const uint32_t wb = (DROP && NQ == 2) ? keep_spread(reinterpret_cast<const uint16_t*>(mtb)[lane]) : 0u;
+  f32x16 sa, sb;
+  zero16(sa);
+  if (NQ == 2) zero16(sb);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) sacc[e] = keep_f(sacc[e], bit_mask(mw, e));
+  for (int s = 0; s < G::NKS; ++s) {
+    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
+    sa = mfma32(kf, a.qf[s], sa);
+    if (NQ == 2) sb = mfma32(kf, b.qf[s], sb);
   }
+  bf16x8 vf[2][G::ND];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) vf[s][dt] = tr_frag(vs + kl * G::TW, G::TW, dt, s, lane);
+  fwd_softmax<HS, DA>(sa, a, k0, c2, h);
+  if (NQ == 2) fwd_softmax<HS, DB>(sb, b, k0, c2, h);
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const bf16x8 pf = acc_frag(sacc, s);
+    const bf16x8 pa = DROP ? acc_frag_keep(sa, s, wa) : acc_frag(sa, s);
 #pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt) oacc[dt] = mfma32(tr_frag(vs + kl * G::TW, G::TW, dt, s, lane), pf, oacc[dt]);
+    for (int dt = 0; dt < G::ND; ++dt) a.o[dt] = mfma32(vf[s][dt], pa, a.o[dt]);
+    if (NQ == 2) {
+      const bf16x8 pb = DROP ? acc_frag_keep(sb, s, wb) : acc_frag(sb, s);
+#pragma unroll
+      for (int dt = 0; dt < G::ND; ++dt) b.o[dt] = mfma32(vf[s][dt], pb, b.o[dt]);
+    }
   }
 }
 
@@ -295,8 +352,10 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::TW];
   using MS = MaskStager<HS>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // keep-bit lane words
-  for (int q = tid; q < ROWS * G::RW; q += 256) if (q % G::RW >= HS) ks[q] = 0;
-  for (int q = tid; q < ROWS * G::TW; q += 256) if (q % G::TW >= HS) vs[q] = 0;
+  if (HS % 32 != 0) {  // pad columns are read only when HS is not a multiple of 32
+    for (int q = tid; q < ROWS * G::RW; q += 256) if (q % G::RW >= HS) ks[q] = 0;
+    for (int q = tid; q < ROWS * G::TW; q += 256) if (q % G::TW >= HS) vs[q] = 0;
+  }
   Stager<HS> st;
   MS mst;
   // lane-word record of the keep bits (AttnProblem::dmask): after the key-major one
@@ -309,56 +368,56 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb
   const bool la = qa < nt, lb = qb < nt;     // lb implies la
-  const int tqa = qa * 32 + r, tqb = qb * 32 + r;
   const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
   const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
-  bf16x8 qfa[G::NKS], qfb[G::NKS];
+  FwdQ<HS> A, Bq;
+  A.tq = qa * 32 + r;
+  Bq.tq = qb * 32 + r;
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
     const int d0 = 16 * s + 8 * h;
-    qfa[s] = ld8(P.q + (rowbase + tqa) * P.q_ld + head * HS + d0, la && tqa < T && d0 < HS);
-    qfb[s] = ld8(P.q + (rowbase + tqb) * P.q_ld + head * HS + d0, lb && tqb < T && d0 < HS);
+    A.qf[s] = ld8(P.q + (rowbase + A.tq) * P.q_ld + head * HS + d0, la && A.tq < T && d0 < HS);
+    Bq.qf[s] = ld8(P.q + (rowbase + Bq.tq) * P.q_ld + head * HS + d0, lb && Bq.tq < T && d0 < HS);
   }
   for (int j = 0; j < P.nstreams; ++j) {
-    float ma = -INFINITY, lsa = 0.f, mb = -INFINITY, lsb = 0.f;
-    f32x16 oa[G::ND], ob[G::ND];
+    A.m = -INFINITY; A.l = 0.f; Bq.m = -INFINITY; Bq.l = 0.f;
 #pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt) { zero16(oa[dt]); zero16(ob[dt]); }
+    for (int dt = 0; dt < G::ND; ++dt) { zero16(A.o[dt]); zero16(Bq.o[dt]); }
     for (int c = 0; c < nch; ++c) {
       const int kt_lo = c * (ROWS / 32);
       const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
+#define FWD_STEP(NQ, DA, DB, KT) \
+  fwd_step<HS, NQ, DA, DB, DROP>(ks, vs, ((KT) - kt_lo) * 32, (KT) * 32, A, Bq, mska + ((KT) - kt_lo) * 32, \
+                                 mskb + ((KT) - kt_lo) * 32, c2, lane)
+#define FWD_STEP_B(DB, KT) \
+  fwd_step<HS, 1, DB, false, DROP>(ks, vs, ((KT) - kt_lo) * 32, (KT) * 32, Bq, A, mskb + ((KT) - kt_lo) * 32, \
+                                   mska, c2, lane)
       if (lb) {
         int kt = kt_lo;
 #pragma unroll 1
-        for (; kt <= min(qa - 1, kt_hi); ++kt) {  // both tiles, off the diagonal
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mska + (kt - kt_lo) * 32, lane);
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (kt - kt_lo) * 32, lane);
-        }
-        if (qa >= kt_lo && qa <= kt_hi) {  // tile a's diagonal, tile b off it
-          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mska + (qa - kt_lo) * 32, lane);
-          fwd_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (qa - kt_lo) * 32, lane);
-        }
+        for (; kt <= min(qa - 1, kt_hi); ++kt) FWD_STEP(2, false, false, kt);  // both tiles, off the diagonal
+        if (qa >= kt_lo && qa <= kt_hi) FWD_STEP(2, true, false, qa);        // tile a's diagonal
 #pragma unroll 1
-        for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (kt - kt_lo) * 32, lane);
-        if (qb >= kt_lo && qb <= kt_hi)
-          fwd_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, mb, lsb, ob, c2, mskb + (qb - kt_lo) * 32, lane);
+        for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt) FWD_STEP_B(false, kt);
+        if (qb >= kt_lo && qb <= kt_hi) FWD_STEP_B(true, qb);
       } else if (la) {
 #pragma unroll 1
-        for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
-          fwd_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, ma, lsa, oa, c2, mska + (kt - kt_lo) * 32, lane);
-        if (qa >= kt_lo && qa <= kt_hi)
-          fwd_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, ma, lsa, oa, c2, mska + (qa - kt_lo) * 32, lane);
+        for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt) FWD_STEP(1, false, false, kt);
+        if (qa >= kt_lo && qa <= kt_hi) FWD_STEP(1, true, false, qa);
       }
+#undef FWD_STEP
+#undef FWD_STEP_B
       // next (stream, chunk) resident for the whole block
       int nj = j, nc = c + 1;
       if (nc == nch) { nc = 0; ++nj; }
       if (nj < P.nstreams && (nj != j || nc != c)) {
         __syncthreads();
+#ifndef MMT_EXP_NORELOAD
         st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
                 T, tid);
         if (DROP) mst.load(P.dmask[nj] + lw_off, bh, nt, qt0, nc * (ROWS / 32), true, tid);
         st.store(ks, G::RW, vs, G::TW, tid);
+#endif
         if (DROP) mst.store(msk, tid);
         __syncthreads();
       }
@@ -368,21 +427,20 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const bool live = u == 0 ? la : lb;
-      const int tq = u == 0 ? tqa : tqb;
-      f32x16* o = u == 0 ? oa : ob;
-      const float m = u == 0 ? ma : mb, l = u == 0 ? lsa : lsb;
+      FwdQ<HS>& q = u == 0 ? A : Bq;
+      const float l = xhalf_sum(q.l);
       const float inv = (l > 0.f) ? (DROP ? P.drop_scale : 1.f) / l : 0.f;
-      if (live && tq < T) {
-        if (h == 0) P.lse[j][(int64_t)bh * T + tq] = (m + __log2f(l)) * kLn2;
-        bf16_t* dst = (P.nstreams > 1 ? P.oj[j] : P.o) + (rowbase + tq) * P.o_ld + head * HS;
+      if (live && q.tq < T) {
+        if (h == 0) P.lse[j][(int64_t)bh * T + q.tq] = (q.m + __log2f(l)) * kLn2;
+        bf16_t* dst = (P.nstreams > 1 ? P.oj[j] : P.o) + (rowbase + q.tq) * P.o_ld + head * HS;
 #pragma unroll
         for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int d0 = dt * 32 + 8 * g + 4 * h;
             if (d0 < HS)
-              *reinterpret_cast<u32x2*>(dst + d0) = u32x2{pack2bf(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv),
-                                                          pack2bf(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv)};
+              *reinterpret_cast<u32x2*>(dst + d0) = u32x2{pack2bf(q.o[dt][4 * g] * inv, q.o[dt][4 * g + 1] * inv),
+                                                          pack2bf(q.o[dt][4 * g + 2] * inv, q.o[dt][4 * g + 3] * inv)};
           }
       }
     }
@@ -393,7 +451,7 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const bool live = u == 0 ? la : lb;
-      const int tq = u == 0 ? tqa : tqb;
+      const int tq = u == 0 ? A.tq : Bq.tq;
       if (!(live && tq < T)) continue;
       const int64_t off = (rowbase + tq) * P.o_ld + head * HS;
 #pragma unroll
@@ -433,23 +491,18 @@ __device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int 
     sacc = mfma32(kf, qf[s], sacc);
     dpacc = mfma32(vf, dof[s], dpacc);
   }
-  const f32x2 c2v = {c2, c2}, nl = {-lse2, -lse2}, nd = {-dsum, -dsum};
-  const f32x2 dsc = {DROP ? P.drop_scale : 1.f, DROP ? P.drop_scale : 1.f};
+  const float nl = -lse2, nd = -dsum;
+  const float dsc = DROP ? P.drop_scale : 1.f;
 #pragma unroll
-  for (int e = 0; e < 16; e += 2) {
-    const f32x2 a = pk_fma(f32x2{sacc[e], sacc[e + 1]}, c2v, nl);
-    f32x2 pv = {ex2(a.x), ex2(a.y)};
+  for (int e = 0; e < 16; ++e) {
+    float pv = ex2(__builtin_fmaf(sacc[e], c2, nl));
     if (diag) {
-      const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;  // keys key, key + 1
-      if (key > tq) pv.x = 0.f;
-      if (key + 1 > tq) pv.y = 0.f;
+      const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (key > tq) pv = 0.f;
     }
-    f32x2 dp = {dpacc[e], dpacc[e + 1]};
-    if (DROP) dp = f32x2{keep_f(dp.x, bit_mask(mw, e)), keep_f(dp.y, bit_mask(mw, e + 1))};
-    const f32x2 t = pk_fma(dp, dsc, nd);  // Z.dP - D (dropped: -D)
-    const f32x2 ds = pv * t;  // dS^T
-    sacc[e] = ds.x;
-    sacc[e + 1] = ds.y;
+    float dp = dpacc[e];
+    if (DROP) dp = keep_f(dp, elem_keep(mw, e));
+    sacc[e] = pv * __builtin_fmaf(dp, dsc, nd);  // dS^T = P (Z.dP - D) (dropped: -P D)
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -485,8 +538,9 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::RW];  // V chunk: row reads
   using MS = MaskStager<HS>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // keep-bit lane words
-  for (int q = tid; q < ROWS * G::RW; q += 256)
-    if (q % G::RW >= HS) { ks[q] = 0; vs[q] = 0; }
+  if (HS % 32 != 0)  // pad columns are read only when HS is not a multiple of 32
+    for (int q = tid; q < ROWS * G::RW; q += 256)
+      if (q % G::RW >= HS) { ks[q] = 0; vs[q] = 0; }
   Stager<HS> st;
   MS mst;
   // lane-word record of the keep bits (AttnProblem::dmask): after the key-major one
@@ -633,30 +687,23 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
     const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsl + ql + 8 * g + 4 * h);
     const f32x4 d4 = *reinterpret_cast<const f32x4*>(dsl + ql + 8 * g + 4 * h);
 #pragma unroll
-    for (int e4 = 0; e4 < 4; e4 += 2) {  // element pairs in packed fp32
+    for (int e4 = 0; e4 < 4; ++e4) {
       const int e = 4 * g + e4;
-      const f32x2 a = pk_fma(f32x2{sacc[e], sacc[e + 1]}, f32x2{c2, c2}, f32x2{l4[e4], l4[e4 + 1]});
-      f32x2 pv = {ex2(a.x), ex2(a.y)};
+      float pv = ex2(__builtin_fmaf(sacc[e], c2, l4[e4]));
       if (MASKED) {
         const int tq = q0 + 8 * g + 4 * h + e4;
-        if (!(tk <= tq && tq < T)) pv.x = 0.f;
-        if (!(tk <= tq + 1 && tq + 1 < T)) pv.y = 0.f;
+        if (!(tk <= tq && tq < T)) pv = 0.f;
       }
-      f32x2 dp = {dpacc[e], dpacc[e + 1]};
+      float dp = dpacc[e];
       if (DROP) {  // pm = Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
-        const int k0 = (int)(mw << (31 - (8 * g + e4))) >> 31;  // all ones iff kept
-        const int k1 = (int)(mw << (30 - (8 * g + e4))) >> 31;
-        pm[e] = __int_as_float(__float_as_int(pv.x) & k0);
-        pm[e + 1] = __int_as_float(__float_as_int(pv.y) & k1);
-        dp = f32x2{__int_as_float(__float_as_int(dp.x) & k0), __int_as_float(__float_as_int(dp.y) & k1)};
+        const int kb = __builtin_amdgcn_sbfe((int)mw, 8 * g + e4, 1);  // all ones iff kept
+        pm[e] = keep_f(pv, kb);
+        dp = keep_f(dp, kb);
       } else {
-        pm[e] = pv.x;
-        pm[e + 1] = pv.y;
+        pm[e] = pv;
       }
       const float sc = DROP ? P.drop_scale : 1.f;
-      const f32x2 ds = pv * pk_fma(dp, f32x2{sc, sc}, f32x2{d4[e4], d4[e4 + 1]});  // dS[q][key]
-      sacc[e] = ds.x;
-      sacc[e + 1] = ds.y;
+      sacc[e] = pv * __builtin_fmaf(dp, sc, d4[e4]);  // dS[q][key]
     }
   }
 #pragma unroll
@@ -705,8 +752,9 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
   __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // -log2-domain LSE, -D of the chunk rows
   using MS = MaskStager<HS>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // [key tile][chunk q tile]
-  for (int q = tid; q < ROWS * G::RW; q += 256)
-    if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
+  if (HS % 32 != 0)  // pad columns are read only when HS is not a multiple of 32
+    for (int q = tid; q < ROWS * G::RW; q += 256)
+      if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
 
   const bf16_t* kp = P.k[j] + head * P.kv_hstride;
   const bf16_t* vp = P.v[j] + head * P.kv_hstride;
@@ -869,8 +917,9 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
   __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // -log2-domain LSE, -D of the chunk rows
   using MS = MaskStager<HS>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // [key tile][chunk q tile]
-  for (int q = tid; q < ROWS * G::RW; q += 256)
-    if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
+  if (HS % 32 != 0)  // pad columns are read only when HS is not a multiple of 32
+    for (int q = tid; q < ROWS * G::RW; q += 256)
+      if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
 
   const bf16_t* kp = P.k[j] + head * P.kv_hstride;
   const bf16_t* vp = P.v[j] + head * P.kv_hstride;
@@ -1064,7 +1113,7 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH,
   const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
   const uint32_t drow = (uint32_t)(bh * T + qt * 32 + r);
   uint32_t out = 0;   // lane L < 32 collects key-major dword L = half (L & 1) of element (L >> 1)'s ballot
-  uint32_t word = 0;  // this lane's own 16 bits
+  uint32_t word = 0;  // this lane's own 16 bits: element 2i at bit i, element 2i + 1 at bit 8 + i
 #pragma unroll
   for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
     const uint32_t key = (uint32_t)(kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h);
@@ -1075,7 +1124,7 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH,
     const uint32_t w0 = (lane & 1) ? (uint32_t)(b0 >> 32) : (uint32_t)b0;
     const uint32_t w1 = (lane & 1) ? (uint32_t)(b1 >> 32) : (uint32_t)b1;
     out = ((lane >> 1) == e) ? w0 : ((lane >> 1) == e + 1) ? w1 : out;
-    word |= ((uint32_t)k0 << e) | ((uint32_t)k1 << (e + 1));
+    word |= ((uint32_t)k0 << (e >> 1)) | ((uint32_t)k1 << (8 + (e >> 1)));  // (keep_spread, elem_keep)
   }
   if (lane < 32) P.dmask[j][tt * 32 + lane] = out;
   reinterpret_cast<uint16_t*>(P.dmask[j] + (per + tt) * 32)[lane] = (uint16_t)word;
