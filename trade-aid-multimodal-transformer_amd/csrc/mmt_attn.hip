@@ -472,43 +472,96 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
   }
 }
 
-// dQ: one 32x32 tile; S^T, dP^T recomputed, dQ^T += K^T dS^T
+// per query tile state of the dQ walk: Q / dO fragments, the row's log2-domain LSE and D, dQ^T
+template <int HS>
+struct DqQ {
+  bf16x8 qf[Geo<HS>::NKS], dof[Geo<HS>::NKS];
+  f32x16 dq[Geo<HS>::ND];
+  float lse2, dsum;
+  int tq;
+};
+
+// dS^T of one tile for one query tile (in place in sacc), packed to the two bf16 operand fragments
 template <int HS, bool diag, bool DROP>
-__device__ __forceinline__ void dq_tile(const bf16_t* ks, const bf16_t* vs, int kl, int k0, int tq,
-                                        const bf16x8 (&qf)[Geo<HS>::NKS], const bf16x8 (&dof)[Geo<HS>::NKS],
-                                        float lse2, float dsum, f32x16 (&dq)[Geo<HS>::ND], float c2,
-                                        const AttnProblem& P, const uint32_t* mt, int lane) {
-  using G = Geo<HS>;
-  const int r = lane & 31, h = lane >> 5;
-  const uint32_t mw = DROP ? reinterpret_cast<const uint16_t*>(mt)[lane] : 0u;  // this lane's keep bits (LDS)
-  f32x16 sacc, dpacc;
-  zero16(sacc);
-  zero16(dpacc);
-#pragma unroll
-  for (int s = 0; s < G::NKS; ++s) {
-    const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
-    const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vs + (kl + r) * G::RW + 16 * s + 8 * h);
-    sacc = mfma32(kf, qf[s], sacc);
-    dpacc = mfma32(vf, dof[s], dpacc);
-  }
-  const float nl = -lse2, nd = -dsum;
-  const float dsc = DROP ? P.drop_scale : 1.f;
+__device__ __forceinline__ void dq_ds(f32x16& sacc, const f32x16& dpacc, const DqQ<HS>& q, int k0, float c2,
+                                      float dsc, uint32_t mw, int h, bf16x8 (&df)[2]) {
+  const float nl = -q.lse2, nd = -q.dsum;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     float pv = ex2(__builtin_fmaf(sacc[e], c2, nl));
     if (diag) {
       const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (key > tq) pv = 0.f;
+      if (key > q.tq) pv = 0.f;
     }
     float dp = dpacc[e];
     if (DROP) dp = keep_f(dp, elem_keep(mw, e));
     sacc[e] = pv * __builtin_fmaf(dp, dsc, nd);  // dS^T = P (Z.dP - D) (dropped: -P D)
   }
+  df[0] = acc_frag(sacc, 0);
+  df[1] = acc_frag(sacc, 1);
+}
+
+// dQ step over one 32-key tile for one or two query tiles: S^T, dP^T recomputed, dQ^T += K^T dS^T.
+// The K / V row fragments and the transposed K fragments are read once for both tiles and issued
+// up front (the transposed ones land behind the dS arithmetic)
+template <int HS, int NQ, bool DA, bool DB, bool DROP>
+__device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, int kl, int k0, DqQ<HS>& a, DqQ<HS>& b,
+                                        const uint32_t* mta, const uint32_t* mtb, float c2, const AttnProblem& P,
+                                        int lane) {
+  using G = Geo<HS>;
+  const int r = lane & 31, h = lane >> 5;
+  const uint32_t wa = DROP ? reinterpret_cast<const uint16_t*>(mta)[lane] : 0u;  // keep bits (LDS)
+  const uint32_t wb = (DROP && NQ == 2) ? reinterpret_cast<const uint16_t*>(mtb)[lane] : 0u;
+  f32x16 sa, pa, sb, pb;
+  zero16(sa);
+  zero16(pa);
+  if (NQ == 2) { zero16(sb); zero16(pb); }
+  if (NQ == 2) {
+    bf16x8 kf[G::NKS], vf[G::NKS];
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const bf16x8 df = acc_frag(sacc, s);
+    for (int s = 0; s < G::NKS; ++s) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
+      vf[s] = *reinterpret_cast<const bf16x8*>(vs + (kl + r) * G::RW + 16 * s + 8 * h);
+    }
 #pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt) dq[dt] = mfma32(tr_frag(ks + kl * G::RW, G::RW, dt, s, lane), df, dq[dt]);
+    for (int s = 0; s < G::NKS; ++s) {
+      sa = mfma32(kf[s], a.qf[s], sa);
+      pa = mfma32(vf[s], a.dof[s], pa);
+      sb = mfma32(kf[s], b.qf[s], sb);
+      pb = mfma32(vf[s], b.dof[s], pb);
+    }
+  } else {  // register-lean order (hs >= 48)
+#pragma unroll
+    for (int s = 0; s < G::NKS; ++s) {
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
+      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vs + (kl + r) * G::RW + 16 * s + 8 * h);
+      sa = mfma32(kf, a.qf[s], sa);
+      pa = mfma32(vf, a.dof[s], pa);
+    }
+  }
+  const float dsc = DROP ? P.drop_scale : 1.f;
+  bf16x8 dfa[2], dfb[2];
+  if (NQ == 2) {
+    bf16x8 kt[2][G::ND];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < G::ND; ++dt) kt[s][dt] = tr_frag(ks + kl * G::RW, G::RW, dt, s, lane);
+    dq_ds<HS, DA, DROP>(sa, pa, a, k0, c2, dsc, wa, h, dfa);
+    dq_ds<HS, DB, DROP>(sb, pb, b, k0, c2, dsc, wb, h, dfb);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < G::ND; ++dt) {
+        a.dq[dt] = mfma32(kt[s][dt], dfa[s], a.dq[dt]);
+        b.dq[dt] = mfma32(kt[s][dt], dfb[s], b.dq[dt]);
+      }
+  } else {
+    dq_ds<HS, DA, DROP>(sa, pa, a, k0, c2, dsc, wa, h, dfa);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < G::ND; ++dt) a.dq[dt] = mfma32(tr_frag(ks + kl * G::RW, G::RW, dt, s, lane), dfa[s], a.dq[dt]);
   }
 }
 
@@ -553,78 +606,79 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb; lb implies la
   const bool la = qa < nt, lb = qb < nt;
-  const int tqa = qa * 32 + r, tqb = qb * 32 + r;
   const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of qa, qb
   const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile kt - kt_lo)
-  const bool oka = la && tqa < T, okb = lb && tqb < T;
-  bf16x8 qfa[G::NKS], dofa[G::NKS], qfb[G::NKS], dofb[G::NKS];
-  f32x16 dqa[G::ND], dqb[G::ND];
+  DqQ<HS> A, Bq;
+  A.tq = qa * 32 + r;
+  Bq.tq = qb * 32 + r;
+  const bool oka = la && A.tq < T, okb = lb && Bq.tq < T;
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
     const int d0 = 16 * s + 8 * h;
-    qfa[s] = ld8(P.q + (rowbase + tqa) * P.q_ld + head * HS + d0, oka && d0 < HS);
-    dofa[s] = ld8(P.dout + (rowbase + tqa) * P.dout_ld + head * HS + d0, oka && d0 < HS);
-    qfb[s] = ld8(P.q + (rowbase + tqb) * P.q_ld + head * HS + d0, okb && d0 < HS);
-    dofb[s] = ld8(P.dout + (rowbase + tqb) * P.dout_ld + head * HS + d0, okb && d0 < HS);
+    A.qf[s] = ld8(P.q + (rowbase + A.tq) * P.q_ld + head * HS + d0, oka && d0 < HS);
+    A.dof[s] = ld8(P.dout + (rowbase + A.tq) * P.dout_ld + head * HS + d0, oka && d0 < HS);
+    Bq.qf[s] = ld8(P.q + (rowbase + Bq.tq) * P.q_ld + head * HS + d0, okb && d0 < HS);
+    Bq.dof[s] = ld8(P.dout + (rowbase + Bq.tq) * P.dout_ld + head * HS + d0, okb && d0 < HS);
   }
 #pragma unroll
-  for (int dt = 0; dt < G::ND; ++dt) { zero16(dqa[dt]); zero16(dqb[dt]); }
+  for (int dt = 0; dt < G::ND; ++dt) { zero16(A.dq[dt]); zero16(Bq.dq[dt]); }
   for (int j = 0; j < P.nstreams; ++j) {
     const bf16_t* oj = (P.nstreams > 1) ? P.oj[j] : P.o;
     float dsa = 0.f, dsb = 0.f;
 #pragma unroll
     for (int s = 0; s < G::NKS; ++s) {
       const int d0 = 16 * s + 8 * h;
-      const bf16x8 ova = ld8(oj + (rowbase + tqa) * P.o_ld + head * HS + d0, oka && d0 < HS);
-      const bf16x8 ovb = ld8(oj + (rowbase + tqb) * P.o_ld + head * HS + d0, okb && d0 < HS);
+      const bf16x8 ova = ld8(oj + (rowbase + A.tq) * P.o_ld + head * HS + d0, oka && d0 < HS);
+      const bf16x8 ovb = ld8(oj + (rowbase + Bq.tq) * P.o_ld + head * HS + d0, okb && d0 < HS);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        dsa += (float)ova[e] * (float)dofa[s][e];
-        dsb += (float)ovb[e] * (float)dofb[s][e];
+        dsa += (float)ova[e] * (float)A.dof[s][e];
+        dsb += (float)ovb[e] * (float)Bq.dof[s][e];
       }
     }
-    dsa += __shfl_xor(dsa, 32, 64);
-    dsb += __shfl_xor(dsb, 32, 64);
+    dsa = xhalf_sum(dsa);
+    dsb = xhalf_sum(dsb);
     if (h == 0) {
-      if (oka) P.dvec[j][(int64_t)bh * T + tqa] = dsa;
-      if (okb) P.dvec[j][(int64_t)bh * T + tqb] = dsb;
+      if (oka) P.dvec[j][(int64_t)bh * T + A.tq] = dsa;
+      if (okb) P.dvec[j][(int64_t)bh * T + Bq.tq] = dsb;
     }
-    const float lsa = oka ? P.lse[j][(int64_t)bh * T + tqa] * kLog2e : 0.f;
-    const float lsb = okb ? P.lse[j][(int64_t)bh * T + tqb] * kLog2e : 0.f;
+    A.dsum = dsa;
+    Bq.dsum = dsb;
+    A.lse2 = oka ? P.lse[j][(int64_t)bh * T + A.tq] * kLog2e : 0.f;
+    Bq.lse2 = okb ? P.lse[j][(int64_t)bh * T + Bq.tq] * kLog2e : 0.f;
     for (int c = 0; c < nch; ++c) {
       const int kt_lo = c * (ROWS / 32);
       const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
+#define DQ_STEP(NQ, DA, DB, KT) \
+  dq_step<HS, NQ, DA, DB, DROP>(ks, vs, ((KT) - kt_lo) * 32, (KT) * 32, A, Bq, mska + ((KT) - kt_lo) * 32, \
+                                mskb + ((KT) - kt_lo) * 32, c2, P, lane)
+#define DQ_STEP_B(DB, KT) \
+  dq_step<HS, 1, DB, false, DROP>(ks, vs, ((KT) - kt_lo) * 32, (KT) * 32, Bq, A, mskb + ((KT) - kt_lo) * 32, mska, \
+                                  c2, P, lane)
       if (lb) {
         int kt = kt_lo;
+        // hs >= 48: the two tiles' S / dP accumulators do not fit beside their Q / dO / dQ state
+        // (two waves per SIMD), so the tiles take turns (each re-reads the K / V fragments)
+        constexpr int NQ2 = HS >= 48 ? 1 : 2;
 #pragma unroll 1
         for (; kt <= min(qa - 1, kt_hi); ++kt) {
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (kt - kt_lo) * 32,
-                                   lane);
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (kt - kt_lo) * 32,
-                                   lane);
+          DQ_STEP(NQ2, false, false, kt);
+          if (NQ2 == 1) DQ_STEP_B(false, kt);
         }
         if (qa >= kt_lo && qa <= kt_hi) {
-          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (qa - kt_lo) * 32,
-                                  lane);
-          dq_tile<HS, false, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (qa - kt_lo) * 32,
-                                   lane);
+          DQ_STEP(NQ2, true, false, qa);
+          if (NQ2 == 1) DQ_STEP_B(false, qa);
         }
 #pragma unroll 1
-        for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt)
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (kt - kt_lo) * 32,
-                                   lane);
-        if (qb >= kt_lo && qb <= kt_hi)
-          dq_tile<HS, true, DROP>(ks, vs, (qb - kt_lo) * 32, qb * 32, tqb, qfb, dofb, lsb, dsb, dqb, c2, P, mskb + (qb - kt_lo) * 32,
-                                  lane);
+        for (kt = max(kt_lo, qa + 1); kt <= min(qb - 1, kt_hi); ++kt) DQ_STEP_B(false, kt);
+        if (qb >= kt_lo && qb <= kt_hi) DQ_STEP_B(true, qb);
       } else if (la) {
 #pragma unroll 1
-        for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt)
-          dq_tile<HS, false, DROP>(ks, vs, (kt - kt_lo) * 32, kt * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (kt - kt_lo) * 32,
-                                   lane);
-        if (qa >= kt_lo && qa <= kt_hi)
-          dq_tile<HS, true, DROP>(ks, vs, (qa - kt_lo) * 32, qa * 32, tqa, qfa, dofa, lsa, dsa, dqa, c2, P, mska + (qa - kt_lo) * 32,
-                                  lane);
+        for (int kt = kt_lo; kt <= min(qa - 1, kt_hi); ++kt) DQ_STEP(1, false, false, kt);
+        if (qa >= kt_lo && qa <= kt_hi) DQ_STEP(1, true, false, qa);
       }
+#undef DQ_STEP
+#undef DQ_STEP_B
       int nj = j, nc = c + 1;
       if (nc == nch) { nc = 0; ++nj; }
       if (nj < P.nstreams && (nj != j || nc != c)) {
@@ -641,8 +695,7 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const bool ok = u == 0 ? oka : okb;
-    const int tq = u == 0 ? tqa : tqb;
-    const f32x16* dq = u == 0 ? dqa : dqb;
+    const DqQ<HS>& q = u == 0 ? A : Bq;
     if (ok) {
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt)
@@ -650,9 +703,9 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
         for (int g = 0; g < 4; ++g) {
           const int d0 = dt * 32 + 8 * g + 4 * h;
           if (d0 < HS)
-            *reinterpret_cast<u32x2*>(P.dq + (rowbase + tq) * P.dq_ld + head * HS + d0) =
-                u32x2{pack2bf(dq[dt][4 * g] * scale, dq[dt][4 * g + 1] * scale),
-                      pack2bf(dq[dt][4 * g + 2] * scale, dq[dt][4 * g + 3] * scale)};
+            *reinterpret_cast<u32x2*>(P.dq + (rowbase + q.tq) * P.dq_ld + head * HS + d0) =
+                u32x2{pack2bf(q.dq[dt][4 * g] * scale, q.dq[dt][4 * g + 1] * scale),
+                      pack2bf(q.dq[dt][4 * g + 2] * scale, q.dq[dt][4 * g + 3] * scale)};
         }
     }
   }
@@ -672,48 +725,74 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
   const int r = lane & 31, h = lane >> 5;
   // key r's keep bits over the tile's queries, this lane's half (queries 8g + 4h + e4) at bits 8g + e4
   const uint32_t mw = DROP ? mt[key_dword(r)] >> (4 * h) : 0u;
-  f32x16 sacc, dpacc, pm;
+  f32x16 sacc, dpacc;
   zero16(sacc);
   zero16(dpacc);
+  // every LDS read of the tile is issued up front, in the order it is consumed (row fragments for
+  // S and dP, then the transposed Q / dO fragments for dK / dV behind the softmax VALU): the
+  // compiler then waits on counted lgkmcnt instead of a read -> wait -> MFMA chain per fragment
+  bf16x8 qr[G::NKS], dr[G::NKS];
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
-    const bf16x8 qa = *reinterpret_cast<const bf16x8*>(qs + (ql + r) * G::RW + 16 * s + 8 * h);
-    const bf16x8 da = *reinterpret_cast<const bf16x8*>(dos + (ql + r) * G::RW + 16 * s + 8 * h);
-    sacc = mfma32(qa, kf[s], sacc);    // S[q][key]
-    dpacc = mfma32(da, vf[s], dpacc);  // dP[q][key]
+    qr[s] = *reinterpret_cast<const bf16x8*>(qs + (ql + r) * G::RW + 16 * s + 8 * h);
+    dr[s] = *reinterpret_cast<const bf16x8*>(dos + (ql + r) * G::RW + 16 * s + 8 * h);
   }
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 l4 = *reinterpret_cast<const f32x4*>(lsl + ql + 8 * g + 4 * h);
-    const f32x4 d4 = *reinterpret_cast<const f32x4*>(dsl + ql + 8 * g + 4 * h);
+  for (int s = 0; s < G::NKS; ++s) {
+    sacc = mfma32(qr[s], kf[s], sacc);    // S[q][key]
+    dpacc = mfma32(dr[s], vf[s], dpacc);  // dP[q][key]
+  }
+  bf16x8 dot[2][G::ND], qtr[2][G::ND];
 #pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
-      const int e = 4 * g + e4;
-      float pv = ex2(__builtin_fmaf(sacc[e], c2, l4[e4]));
-      if (MASKED) {
-        const int tq = q0 + 8 * g + 4 * h + e4;
-        if (!(tk <= tq && tq < T)) pv = 0.f;
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt) {
+      dot[s][dt] = tr_frag(dos + ql * G::RW, G::RW, dt, s, lane);
+      qtr[s][dt] = tr_frag(qs + ql * G::RW, G::RW, dt, s, lane);
+    }
+  f32x4 l4[4], d4[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    l4[g] = *reinterpret_cast<const f32x4*>(lsl + ql + 8 * g + 4 * h);
+    d4[g] = *reinterpret_cast<const f32x4*>(dsl + ql + 8 * g + 4 * h);
+  }
+  uint32_t pp[8], dd[8];  // packed bf16 pairs of Z.P (dV operand) and dS (dK operand)
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+#pragma unroll
+    for (int e4 = 0; e4 < 4; e4 += 2) {
+      float pm[2], ds[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int e = 4 * g + e4 + u;
+        float pv = ex2(__builtin_fmaf(sacc[e], c2, l4[g][e4 + u]));
+        if (MASKED) {
+          const int tq = q0 + 8 * g + 4 * h + e4 + u;
+          if (!(tk <= tq && tq < T)) pv = 0.f;
+        }
+        float dp = dpacc[e];
+        if (DROP) {  // Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
+          const int kb = __builtin_amdgcn_sbfe((int)mw, 8 * g + e4 + u, 1);  // all ones iff kept
+          pm[u] = keep_f(pv, kb);
+          dp = keep_f(dp, kb);
+        } else {
+          pm[u] = pv;
+        }
+        const float sc = DROP ? P.drop_scale : 1.f;
+        ds[u] = pv * __builtin_fmaf(dp, sc, d4[g][e4 + u]);  // dS[q][key]
       }
-      float dp = dpacc[e];
-      if (DROP) {  // pm = Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
-        const int kb = __builtin_amdgcn_sbfe((int)mw, 8 * g + e4, 1);  // all ones iff kept
-        pm[e] = keep_f(pv, kb);
-        dp = keep_f(dp, kb);
-      } else {
-        pm[e] = pv;
-      }
-      const float sc = DROP ? P.drop_scale : 1.f;
-      sacc[e] = pv * __builtin_fmaf(dp, sc, d4[e4]);  // dS[q][key]
+      pp[2 * g + e4 / 2] = pack2bf(pm[0], pm[1]);
+      dd[2 * g + e4 / 2] = pack2bf(ds[0], ds[1]);
     }
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const bf16x8 pf = acc_frag(pm, s);
-    const bf16x8 df = acc_frag(sacc, s);
+    const bf16x8 pf = __builtin_bit_cast(bf16x8, u32x4{pp[4 * s], pp[4 * s + 1], pp[4 * s + 2], pp[4 * s + 3]});
+    const bf16x8 df = __builtin_bit_cast(bf16x8, u32x4{dd[4 * s], dd[4 * s + 1], dd[4 * s + 2], dd[4 * s + 3]});
 #pragma unroll
     for (int dt = 0; dt < G::ND; ++dt) {
-      dv[dt] = mfma32(pf, tr_frag(dos + ql * G::RW, G::RW, dt, s, lane), dv[dt]);
-      dk[dt] = mfma32(df, tr_frag(qs + ql * G::RW, G::RW, dt, s, lane), dk[dt]);
+      dv[dt] = mfma32(pf, dot[s][dt], dv[dt]);
+      dk[dt] = mfma32(df, qtr[s][dt], dk[dt]);
     }
   }
 }
