@@ -178,6 +178,21 @@ def mask_hash(a, b, c):
     return h.astype(_U32)
 
 
+PROB_ROW_SALT = 0x2545F491
+
+
+def prob_hash(row_hash, c):
+    """mmt_prob_hash (csrc/mmt_common.h): attention-probability keep hash of key pair c of a row."""
+    with np.errstate(over="ignore"):
+        h = np.asarray(row_hash, dtype=_U32) + np.asarray(c, dtype=_U32) * _U32(0x9E3779B9)
+        h = h ^ (h >> _U32(16))
+        h = h * _U32(0x7FEB352D)
+        h = h ^ (h >> _U32(15))
+        h = h * _U32(0x846CA68B)
+        h = h ^ (h >> _U32(16))
+    return h.astype(_U32)
+
+
 class HashDropout:
     """Dropout masks of one training forward: seed (uint64) and probability p."""
 
@@ -207,7 +222,10 @@ class HashDropout:
         """[B, T, T] probabilities of head h, stream j: row (b*H + h)*T + t, column s."""
         kj = int(mask_hash(self.key(l, i, site), j, STREAM_SALT))
         rows = ((np.arange(B)[:, None, None] * H + h) * T + np.arange(T)[None, :, None]).astype(np.int64)
-        return self._mask(kj, rows, np.arange(T)[None, None, :])
+        cols = np.arange(T, dtype=np.int64)[None, None, :]
+        hsh = prob_hash(mask_hash(kj, rows, PROB_ROW_SALT), cols >> 1)  # mmt_prob_row / mmt_prob_hash
+        half = (hsh >> ((cols & 1).astype(_U32) * _U32(16))) & _U32(0xFFFF)
+        return torch.from_numpy((half >= _U32(self.thr)).astype(np.float32) * np.float32(self.scale))
 
 
 def _drop(x, p, training, mask_fn=None):

@@ -114,12 +114,17 @@ def test_hash_dropout_mask_law():
     p1 = hd.probs(0, 1, O.SITE_CA_PROB, 1, 0, 4, 2, 32)
     ph = hd.probs(0, 1, O.SITE_CA_PROB, 0, 1, 4, 2, 32)
     assert not torch.equal(p0, p1) and not torch.equal(p0, ph)
+    pk = (hd.probs(0, 0, O.SITE_SA_PROB, 0, 0, 4, 8, 256) > 0).float()
+    assert abs(pk.mean().item() - 0.9) < 0.005, pk.mean().item()
+    assert abs(pk[:, :, 0::2].mean().item() - pk[:, :, 1::2].mean().item()) < 0.01  # both 16-bit halves
     x = torch.randn(3, 4)
     assert torch.equal(O._drop(x, 0.0, True, lambda: None), x)
     # the hash is a fixed function: pinned values guard the device/host/oracle restatements
     assert int(O.mask_hash(1, 2, 3)) == 1107639200
     assert int(O.mask_hash(0xFFFFFFFF, 0, 7)) == 352430166
     assert O.mask_hash([1, 2], 3, 4).dtype == np.uint32
+    assert int(O.prob_hash(1, 2)) == 1136996714
+    assert int(O.prob_hash(0xFFFFFFFF, 12345)) == 767955703
 
 
 def _scale_compare(z, meta, logits, losses, grads, rel_tol, grad_tol, sample_tol):

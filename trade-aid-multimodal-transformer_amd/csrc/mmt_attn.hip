@@ -1190,13 +1190,13 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH,
   const int kt = tri - qt * (qt + 1) / 2;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
-  const uint32_t drow = (uint32_t)(bh * T + qt * 32 + r);
+  const uint32_t rowh = mmt_prob_row(dkey, (uint32_t)(bh * T + qt * 32 + r));
   uint32_t out = 0;   // lane L < 32 collects key-major dword L = half (L & 1) of element (L >> 1)'s ballot
   uint32_t word = 0;  // this lane's own 16 bits: element 2i at bit i, element 2i + 1 at bit 8 + i
 #pragma unroll
   for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
     const uint32_t key = (uint32_t)(kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h);
-    const uint32_t hk = mmt_hash(dkey, drow, key >> 1);
+    const uint32_t hk = mmt_prob_hash(rowh, key >> 1);
     const bool k0 = mmt_keep(hk, 0, P.drop_thr), k1 = mmt_keep(hk, 1, P.drop_thr);
     const uint64_t b0 = __builtin_amdgcn_ballot_w64(k0);
     const uint64_t b1 = __builtin_amdgcn_ballot_w64(k1);

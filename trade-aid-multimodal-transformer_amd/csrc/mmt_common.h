@@ -102,6 +102,20 @@ __host__ __device__ __forceinline__ uint32_t mmt_hash(uint32_t a, uint32_t b, ui
   return h;
 }
 
+// attention-probability keep hash (attn_mask_kernel; restated by oracle/mmt_oracle.py probs):
+// the (stream key, score row) part is hashed once per row (mmt_hash), each key pair c then costs
+// one add of c * golden-ratio (a compile-time offset plus a per-tile base) and a two-multiply
+// finaliser — 2 instead of 5 quarter-rate 32-bit multiplies per pair
+#define MMT_PROB_ROW_SALT 0x2545F491u
+__host__ __device__ __forceinline__ uint32_t mmt_prob_row(uint32_t stream_key, uint32_t row) {
+  return mmt_hash(stream_key, row, MMT_PROB_ROW_SALT);
+}
+__host__ __device__ __forceinline__ uint32_t mmt_prob_hash(uint32_t row_hash, uint32_t c) {
+  uint32_t h = row_hash + c * 0x9E3779B9u;
+  h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+  return h;
+}
+
 // ---------------------------------------------------------------------------------------------
 // MX-fp8 (OCP e4m3fn values, E8M0 block exponents over 32 consecutive K elements): the operand
 // format of v_mfma_scale_f32_32x32x64_f8f6f4 (C4's fp8 path). A 32-element block with absolute

@@ -1466,7 +1466,19 @@ void ensure_side(mmt_ctx* c) {
   for (auto& e : c->evpool) (void)hipEventDestroy(e);  // events of the previous device
   c->evpool.clear();
   c->side = nullptr;
-  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
+  // MMT_SIDE_PRIORITY (optional): HIP stream priority of the side stream (lower = higher priority,
+  // clamped to the device's range); unset = default priority
+  static const char* prio_env = getenv("MMT_SIDE_PRIORITY");
+  hipError_t ce;
+  if (prio_env) {
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const int pr = std::max(greatest, std::min(least, atoi(prio_env)));
+    ce = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, pr);
+  } else {
+    ce = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  }
+  if (ce != hipSuccess) c->side = nullptr;
   c->side_device = dev;
   while (c->side && c->evpool.size() < 64) {
     hipEvent_t e;
