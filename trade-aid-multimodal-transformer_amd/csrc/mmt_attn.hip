@@ -53,30 +53,6 @@ struct Geo {
   static constexpr int CH = HS / 8;                    // 16-byte chunks per row
 };
 
-// LDS-DMA (the DMA forward path): buffer resource words in SGPRs, one 16-B-per-lane
-// `buffer_load_dwordx4 ... lds` per 1-KiB piece (lane L -> LDS bytes [16L, 16L + 16) of the piece);
-// offsets past the range read as zero. Inline asm so the compiler's waitcnt pass does not drain
-// the in-flight chunk before every LDS read; the kernel waits with its own s_waitcnt vmcnt(0).
-typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4 make_rsrc(const void* base, int64_t bytes) {
-  const uint64_t a = (uint64_t)base;
-  i32x4 rr;
-  rr[0] = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a);
-  rr[1] = __builtin_amdgcn_readfirstlane((int32_t)((a >> 32) & 0xffffu));  // stride 0
-  rr[2] = __builtin_amdgcn_readfirstlane((int32_t)min(bytes, (int64_t)0x7ffffff0));
-  rr[3] = 0x00020000;
-  return rr;
-}
-__device__ __forceinline__ void dma16(const i32x4& rsrc, uint32_t lds_addr, int voff) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-               :
-               : "s"(lds_addr), "v"(voff), "s"(rsrc)
-               : "memory", "m0");
-}
-__device__ __forceinline__ uint32_t lds_u32(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
-}
-
 // one 16-B chunk (8 bf16) of a 32-row tile: row r0+row, columns col..col+7 of the head (zero padded)
 __device__ __forceinline__ u32x4 tile_chunk(const bf16_t* base, int64_t rowbase, int r0, int row, int col, int T,
                                             int ld) {
@@ -353,16 +329,12 @@ __device__ __forceinline__ void fwd_step(const bf16_t* ks, const bf16_t* vs, int
 // independent MFMA -> softmax -> MFMA chains interleave in the wave; the resident K/V chunk of each
 // (stream, chunk) is loaded once per block.
 // =============================================================================================
-template <int HS, bool DROP, bool DMA>
+template <int HS, bool DROP>
 __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBatch batch, int T, int H, float scale) {
   using G = Geo<HS>;
-  // resident path: chunks of Chunk<HS>::ROWS rows through registers (one load per block when the
-  // sequence fits); DMA path (T > that): 64-row chunks in a 2-deep LDS ring filled by LDS-DMA,
-  // the next chunk in flight while the current one is consumed, one barrier per chunk
-  constexpr int ROWS = DMA ? 64 : Chunk<HS>::ROWS;
-  constexpr int NBUF = DMA ? 2 : 1;
-  constexpr int MKT = ROWS / 32;          // key tiles per chunk
-  constexpr int MDW = 8 * MKT * 32;       // keep-bit dwords per chunk
+  constexpr int ROWS = Chunk<HS>::ROWS;
+  constexpr int MKT = ROWS / 32;     // key tiles per chunk
+  constexpr int MDW = 8 * MKT * 32;  // keep-bit dwords per chunk
   const AttnProblem& P = batch.p[blockIdx.z];
   // grid.x = nb * B*H in XCD-aware logical order: the heads of one batch row (halves of the same
   // Q/K/V cache lines) run on one XCD together
@@ -378,60 +350,23 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
   const int nch = (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS;
   const int64_t rowbase = (int64_t)b * T;
   const float c2 = scale * kLog2e;
-  __shared__ __attribute__((aligned(16))) bf16_t ks_[NBUF * ROWS * G::RW];
-  __shared__ __attribute__((aligned(16))) bf16_t vs_[NBUF * ROWS * G::TW];
+  __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];
+  __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::TW];
   using MS = MaskStager<HS>;
-  __shared__ __attribute__((aligned(16))) uint32_t msk_[DROP ? NBUF * MDW : 4];  // keep-bit lane words
+  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MDW : 4];  // keep-bit lane words
   // lane-word record of the keep bits (AttnProblem::dmask): after the key-major one
   const int BH = gridDim.x / nb;
   const int64_t lw_off = (int64_t)BH * (nt * (nt + 1) / 2) * 32;
-  const int nall = P.nstreams * nch;  // (stream, chunk) steps of the block
-  // LDS-DMA of step g (stream g / nch, chunk g % nch) into ring slot g & 1: 16-B slots of the K
-  // image (RW / 8 per row), the V image (TW / 8 per row) and the keep-bit lane words; slots past
-  // HS, rows past T and tiles above the diagonal read as zero (out-of-range buffer offsets)
-  auto issue = [&](int g) {
-    const int j = g / nch, c = g % nch, buf = g & 1;
-    const i32x4 rk = make_rsrc(P.k[j], (int64_t)BH / H * T * P.kv_ld * 2);
-    const i32x4 rv = make_rsrc(P.v[j], (int64_t)BH / H * T * P.kv_ld * 2);
-    constexpr int PK = ROWS * G::RW / 8 / 64, PV = ROWS * G::TW / 8 / 64, PM = DROP ? MDW / 4 / 64 : 0;
-    static_assert((ROWS * G::RW / 8) % 64 == 0 && (ROWS * G::TW / 8) % 64 == 0, "DMA piece geometry");
-#pragma unroll
-    for (int i0 = 0; i0 < PK + PV + PM; i0 += 4) {
-      const int i = i0 + w;
-      if (i >= PK + PV + PM) break;  // wave-uniform
-      if (i < PK + PV) {
-        const bool isk = i < PK;
-        const int spr = (isk ? G::RW : G::TW) / 8;
-        const int slot = (isk ? i : i - PK) * 64 + lane;
-        const int row = slot / spr, ch = slot % spr, gr = c * ROWS + row;
-        const int voff = (ch * 8 < HS && gr < T) ? (int)(((rowbase + gr) * P.kv_ld + head * P.kv_hstride + ch * 8) * 2)
-                                                 : 0x7fffffff;
-        const bf16_t* img = isk ? ks_ + buf * ROWS * G::RW + (i * 64) * 8 : vs_ + buf * ROWS * G::TW + ((i - PK) * 64) * 8;
-        dma16(isk ? rk : rv, __builtin_amdgcn_readfirstlane(lds_u32(img)), voff);
-      } else if (DROP) {
-        const i32x4 rm = make_rsrc(P.dmask[j], 2 * lw_off * 4);
-        const int slot = (i - PK - PV) * 64 + lane;  // [8 block tiles][MKT chunk tiles][8 slots]
-        const int qt = qt0 + slot / (MKT * 8), kt = c * MKT + (slot / 8) % MKT, p = slot % 8;
-        const int voff = (qt < nt && kt <= qt) ? (int)((lw_off + ((int64_t)bh * (nt * (nt + 1) / 2) + qt * (qt + 1) / 2 + kt) * 32 + 4 * p) * 4)
-                                               : 0x7fffffff;
-        dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(msk_ + buf * MDW + (i - PK - PV) * 256)), voff);
-      }
-    }
-  };
   Stager<HS> st;
   MS mst;
-  if (DMA) {
-    issue(0);
-  } else {
-    if (HS % 32 != 0) {  // pad columns are read only when HS is not a multiple of 32
-      for (int q = tid; q < ROWS * G::RW; q += 256) if (q % G::RW >= HS) ks_[q] = 0;
-      for (int q = tid; q < ROWS * G::TW; q += 256) if (q % G::TW >= HS) vs_[q] = 0;
-    }
-    st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
-    if (DROP) mst.load(P.dmask[0] + lw_off, bh, nt, qt0, 0, true, tid);
-    st.store(ks_, G::RW, vs_, G::TW, tid);
-    if (DROP) mst.store(msk_, tid);
+  if (HS % 32 != 0) {  // pad columns are read only when HS is not a multiple of 32
+    for (int q = tid; q < ROWS * G::RW; q += 256) if (q % G::RW >= HS) ks[q] = 0;
+    for (int q = tid; q < ROWS * G::TW; q += 256) if (q % G::TW >= HS) vs[q] = 0;
   }
+  st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
+  if (DROP) mst.load(P.dmask[0] + lw_off, bh, nt, qt0, 0, true, tid);
+  st.store(ks, G::RW, vs, G::TW, tid);
+  if (DROP) mst.store(msk, tid);
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb
   const bool la = qa < nt, lb = qb < nt;     // lb implies la
@@ -444,19 +379,14 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
     A.qf[s] = ld8(P.q + (rowbase + A.tq) * P.q_ld + head * HS + d0, la && A.tq < T && d0 < HS);
     Bq.qf[s] = ld8(P.q + (rowbase + Bq.tq) * P.q_ld + head * HS + d0, lb && Bq.tq < T && d0 < HS);
   }
-  if (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int j = 0; j < P.nstreams; ++j) {
     A.m = -INFINITY; A.l = 0.f; Bq.m = -INFINITY; Bq.l = 0.f;
 #pragma unroll
     for (int dt = 0; dt < G::ND; ++dt) { zero16(A.o[dt]); zero16(Bq.o[dt]); }
     for (int c = 0; c < nch; ++c) {
-      const int g = j * nch + c, buf = DMA ? (g & 1) : 0;
-      if (DMA && g + 1 < nall) issue(g + 1);  // ring slot (g + 1) & 1 was released by the last barrier
-      const bf16_t* ks = ks_ + buf * ROWS * G::RW;
-      const bf16_t* vs = vs_ + buf * ROWS * G::TW;
-      const uint32_t* mska = msk_ + buf * MDW + (DROP ? w * MKT * 32 : 0);        // keep-bit tiles of qa, qb
-      const uint32_t* mskb = msk_ + buf * MDW + (DROP ? (7 - w) * MKT * 32 : 0);  // (chunk tile kt - kt_lo)
+      const uint32_t* mska = msk + (DROP ? w * MKT * 32 : 0);        // keep-bit tiles of qa, qb
+      const uint32_t* mskb = msk + (DROP ? (7 - w) * MKT * 32 : 0);  // (chunk tile kt - kt_lo)
       const int kt_lo = c * MKT;
       const int kt_hi = min(kt_lo + MKT, nt) - 1;
 #define FWD_STEP(NQ, DA, DB, KT) \
@@ -480,14 +410,7 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
       }
 #undef FWD_STEP
 #undef FWD_STEP_B
-      if (DMA) {
-        if (g + 1 < nall) {  // step g + 1 landed (every wave's pieces) and slot g & 1 is free again
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
-        }
-        continue;
-      }
-      // resident path: next (stream, chunk) for the whole block
+      // next (stream, chunk) resident for the whole block
       int nj = j, nc = c + 1;
       if (nc == nch) { nc = 0; ++nj; }
       if (nj < P.nstreams && (nj != j || nc != c)) {
@@ -495,8 +418,8 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
         st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
                 T, tid);
         if (DROP) mst.load(P.dmask[nj] + lw_off, bh, nt, qt0, nc * (ROWS / 32), true, tid);
-        st.store(ks_, G::RW, vs_, G::TW, tid);
-        if (DROP) mst.store(msk_, tid);
+        st.store(ks, G::RW, vs, G::TW, tid);
+        if (DROP) mst.store(msk, tid);
         __syncthreads();
       }
     }
@@ -1174,33 +1097,15 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
   }
 }
 
-// MMT_ATTN_DMA=1 puts sequences longer than one resident chunk on the LDS-DMA ring path of the
-// forward. Off by default: measured slower than the resident path (target 158 vs 134 us, C4 1185 vs
-// 978 us per launch): 64-row chunks double the barriers and the ~23 DMA pieces per chunk cost more
-// issue slots than the register-staged reload they replace
-static bool attn_dma_path() {
-  static const bool on = [] {
-    const char* e = getenv("MMT_ATTN_DMA");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
-
 template <int HS>
 static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
   const int nb = ((T + 31) / 32 + 7) / 8;
   if (!bwd) {
     bool drop = false;
     for (int g = 0; g < bt.count; ++g) drop = drop || bt.p[g].drop_thr != 0;
-    // DMA path past one resident chunk (32-bit buffer offsets: the K/V rows must span < 2 GiB)
-    bool dma = T > Chunk<HS>::ROWS && attn_dma_path();
-    for (int g = 0; g < bt.count; ++g)
-      dma = dma && (int64_t)B * T * bt.p[g].kv_ld * 2 < 0x7ffffff0 && mmt_attn_mask_dwords(B, H, T) * 4 < 0x7ffffff0;
     const dim3 grid(nb * B * H, 1, bt.count);
-    if (drop && dma) hipLaunchKernelGGL((attn_fwd_kernel<HS, true, true>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else if (drop) hipLaunchKernelGGL((attn_fwd_kernel<HS, true, false>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else if (dma) hipLaunchKernelGGL((attn_fwd_kernel<HS, false, true>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_fwd_kernel<HS, false, false>), grid, dim3(256), 0, s, bt, T, H, scale);
+    if (drop) hipLaunchKernelGGL((attn_fwd_kernel<HS, true>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_fwd_kernel<HS, false>), grid, dim3(256), 0, s, bt, T, H, scale);
   } else {
     const int ns = bt.p[0].nstreams;
     bool drop = false;
