@@ -997,10 +997,9 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
   __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // -log2-domain LSE, -D of the chunk rows
   using MS = MaskStager<HS>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // [key tile][chunk q tile]
-  // epilogue transpose slots (hs <= 32; larger heads would spill): per wave [dK, dV][32 keys][EPW]
-  constexpr bool TEPI = HS <= 32;
-  constexpr int EPW = G::W + 8;
-  __shared__ __attribute__((aligned(16))) bf16_t ept[TEPI ? 4 * 2 * 32 * EPW : 8];
+  // epilogue transpose slots, one 32-column slice at a time: per wave [dK, dV][32 keys][EPW]
+  constexpr int EPW = 40;
+  __shared__ __attribute__((aligned(16))) bf16_t ept[4 * 2 * 32 * EPW];
   if (HS % 32 != 0)  // pad columns are read only when HS is not a multiple of 32
     for (int q = tid; q < ROWS * G::RW; q += 256)
       if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
@@ -1079,48 +1078,30 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
         __syncthreads();
       }
     }
-    // dK/dV tiles: accumulator rows = key ((e&3)+8(e>>2)+4h), cols = d (lane). hs <= 32: transposed
-    // through this wave's LDS slot (ds_write_b16 at immediate offsets) so the global stores are row-major
-    // 16-B pieces: W/8 dwordx4 per lane per matrix instead of 16*ND two-byte stores with a 64-bit
-    // address computation each
-    if (TEPI && live) {
+    // dK/dV tiles: accumulator rows = key ((e&3)+8(e>>2)+4h), cols = d (lane). Each 32-column slice
+    // is transposed through this wave's LDS slot (ds_write_b16 at immediate offsets) and leaves as
+    // row-major 16-B pieces: 2 dwordx4 per lane per matrix and slice instead of 16 two-byte stores
+    // with a 64-bit address computation each
+    if (live) {
       bf16_t* et = ept + w * (2 * 32 * EPW);
-#pragma unroll
-      for (int dt = 0; dt < G::ND; ++dt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-          et[kr * EPW + dt * 32 + r] = f2bf(dk[dt][e] * scale);
-          et[32 * EPW + kr * EPW + dt * 32 + r] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
-        }
-      constexpr int CPR = G::W / 8;  // 16-B chunks per key row
-      const int k0 = kt * 32;
-#pragma unroll
-      for (int i = 0; i < G::W / 16; ++i) {
-        const int row = i * (64 / CPR) + lane / CPR, ch = lane % CPR;
-        const u32x4 vk = *reinterpret_cast<const u32x4*>(et + row * EPW + ch * 8);
-        const u32x4 vv = *reinterpret_cast<const u32x4*>(et + 32 * EPW + row * EPW + ch * 8);
-        if (k0 + row < T && ch * 8 < HS) {
-          const int64_t off = (rowbase + k0 + row) * P.dkv_ld + ch * 8;
-          *reinterpret_cast<u32x4*>(P.dk[j] + head * P.dkv_hstride + off) = vk;
-          *reinterpret_cast<u32x4*>(P.dv[j] + head * P.dkv_hstride + off) = vv;
-        }
-      }
-    }
-    if (!TEPI && live) {  // hs > 32: two-byte stores straight from the accumulators
-      bf16_t* dkp = P.dk[j] + head * P.dkv_hstride;
-      bf16_t* dvo = P.dv[j] + head * P.dkv_hstride;
       const int k0 = kt * 32;
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt) {
-        const int d = dt * 32 + r;
-        if (d >= HS) continue;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (key < T) {
-            dkp[(rowbase + key) * P.dkv_ld + d] = f2bf(dk[dt][e] * scale);
-            dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
+          const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+          et[kr * EPW + r] = f2bf(dk[dt][e] * scale);
+          et[32 * EPW + kr * EPW + r] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = i * 16 + (lane >> 2), d0 = dt * 32 + (lane & 3) * 8;
+          const u32x4 vk = *reinterpret_cast<const u32x4*>(et + row * EPW + (lane & 3) * 8);
+          const u32x4 vv = *reinterpret_cast<const u32x4*>(et + 32 * EPW + row * EPW + (lane & 3) * 8);
+          if (k0 + row < T && d0 < HS) {
+            const int64_t off = (rowbase + k0 + row) * P.dkv_ld + d0;
+            *reinterpret_cast<u32x4*>(P.dk[j] + head * P.dkv_hstride + off) = vk;
+            *reinterpret_cast<u32x4*>(P.dv[j] + head * P.dkv_hstride + off) = vv;
           }
         }
       }
