@@ -53,6 +53,15 @@ SHAPES = [
     # per-CU main-loop rate: one block per output tile over a long K (16 or 64 blocks)
     ("rate_1k_16k_s1", 0, 0, "store_f32", 1024, 1024, 16384, 1),
     ("rate_1k_16k_kc", 1, 1, "store_f32", 1024, 1024, 16384, 1),
+    # MFMA-bound shapes (256x256 tile): target / C4 FFN and a square reference
+    ("tgt_ffn0_fwd", 1, 1, "bias_relu_bf16", R, 2048, 512, 1),
+    ("c4_ffn0_fwd", 1, 1, "bias_relu_bf16", R, 4096, 1024, 1),
+    ("c4_ffn0_store", 1, 1, "store_bf16", R, 4096, 1024, 1),
+    ("c4_ffn2_dx", 1, 0, "drelu_bf16", R, 4096, 1024, 1),
+    ("c4_ffn2_fwd", 1, 1, "bias_resid_f32", R, 1024, 4096, 1),
+    ("c4_ffn_dw", 0, 0, "store_f32", 4096, 1024, 16384, 1),
+    ("sq4k_store", 1, 1, "store_bf16", 4096, 4096, 4096, 1),
+    ("sq8k_store", 1, 1, "store_bf16", 8192, 8192, 8192, 1),
 ]
 if os.environ.get("GEMM_BENCH_ONLY"):
     SHAPES = [s for s in SHAPES if any(k in s[0] for k in os.environ["GEMM_BENCH_ONLY"].split(","))]
