@@ -163,8 +163,10 @@ int mmt_batch_gather(void* stream, int32_t nmod, const int32_t* const* data, con
                      int32_t T, int64_t* const* x, int64_t* const* y);
 
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
-/* GEMM pipeline variant (tuning knob, process-wide): 0 = K-step 64 x 2 LDS stages (default),
- * 1 = 32 x 2, 2 = 32 x 3, 3 = 32 x 4, 4 = 64 x 3 */
+/* GEMM pipeline variant (tuning knob, process-wide; 128x128 tile): bits 0-3 forward / backward-data,
+ * bits 4-7 weight gradients: 0 = K-step 64 x 2 LDS stages, 1 = 32 x 2, 2 = 32 x 3, 3 = 32 x 4,
+ * 4 = 64 x 3, 5 = 32 x 3 and 6 = 32 x 2 at 3+ blocks per CU (64-row epilogue passes).
+ * variant < 0: the default policy (6 for bf16-output epilogues without an aux operand, else 0) */
 int mmt_gemm_set_variant(int variant);
 /* splits: split-K factor of EPI atomic_f32 launches (<= 0: automatic) */
 int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t splits, int32_t M, int32_t N,

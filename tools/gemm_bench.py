@@ -73,7 +73,7 @@ def r8(x):
 
 def run(variant, reps):
     L = ML.lib()
-    assert L.mmt_gemm_set_variant(variant | (variant << 4)) == 0
+    assert L.mmt_gemm_set_variant(variant if variant < 0 else variant | (variant << 4)) == 0
     out = {}
     for name, akc, bkc, epi, M, N, K, splits in SHAPES:
         if akc:
@@ -119,7 +119,7 @@ def run(variant, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2,3,4")
+    ap.add_argument("--variants", default="-1,0,6")
     ap.add_argument("--reps", type=int, default=20)
     args = ap.parse_args()
     for v in [int(x) for x in args.variants.split(",")]:

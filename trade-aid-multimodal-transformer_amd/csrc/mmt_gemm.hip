@@ -43,11 +43,13 @@ using TileL = TileCfg<2, 4, 4, 2>;
 
 // tuning knob (mmt_gemm_set_variant): pipeline variant of the forward / backward-data GEMMs in
 // bits 0-3 and of the weight-grad (split-K, atomic) GEMMs in bits 4-7:
-//   0 = BK 64 x 2 stages, 1 = BK 32 x 2, 2 = BK 32 x 3, 3 = BK 32 x 4, 4 = BK 64 x 3
-static int g_gemm_variant = 0;      // forward / backward-data
+//   0 = BK 64 x 2 stages, 1 = BK 32 x 2, 2 = BK 32 x 3, 3 = BK 32 x 4, 4 = BK 64 x 3,
+//   5 = BK 32 x 3 and 6 = BK 32 x 2 at 3 blocks per CU (64-row epilogue passes)
+static int g_gemm_variant = -1;     // forward / backward-data (-1: per-epilogue policy, launch_t)
 static int g_gemm_variant_dw = 0;   // weight grad (split-K atomic)
 extern "C" int mmt_gemm_set_variant(int v) {
-  if ((v & 15) > 4 || ((v >> 4) & 15) > 4) return -1;
+  if (v < 0) { g_gemm_variant = -1; g_gemm_variant_dw = 0; return 0; }  // back to the default policy
+  if ((v & 15) > 6 || ((v >> 4) & 15) > 6) return -1;
   g_gemm_variant = v & 15;
   g_gemm_variant_dw = (v >> 4) & 15;
   return 0;
@@ -388,8 +390,10 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
   }
 }
 
-template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
-__global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
+// MINB > 1 (128x128 tile only): a launch-bounds hint of MINB blocks per CU, with the epilogue staged in
+// 64-row passes so the LDS footprint leaves room for them (variants 5 and 6)
+template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1>
+__global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
   constexpr int IMG_A = GBM * BK * 2, IMG_B = GBN * BK * 2;  // per operand per stage (both layouts)
   constexpr int STAGE_BYTES = IMG_A + IMG_B;
@@ -420,7 +424,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmBatch batch) {
 
   // one LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads):
   // the stage ring during the K loop, the fp32 output tile (EPI_ROWS x (GBN + 4)) in the epilogue
-  constexpr int EPI_ROWS = GBM == 128 ? 128 : 64;
+  constexpr int EPI_ROWS = (GBM == 128 && MINB == 1) ? 128 : 64;
   constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
   constexpr int LDS_MAIN = RING > CTILE ? RING : CTILE;
   __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN];
@@ -656,9 +660,9 @@ __global__ __launch_bounds__(TL::NT) void gemm_f8_kernel(GemmBatch batch) {
   epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, P.o32, alpha, m0, n0, tid, lane, wave);
 }
 
-template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI>
+template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1>
 static void launch_v(const GemmBatch& b, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI>), grid, dim3(TL::NT), 0, s, b);
+  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI, MINB>), grid, dim3(TL::NT), 0, s, b);
 }
 
 template <class TL>
@@ -722,11 +726,20 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
   const int mt = max_tiles<TileS>(b, nullptr);
   if (mt == 0) return hipSuccess;
   dim3 grid(mt, EPI == EPI_ATOMIC_F32 ? auto_splits<TileS>(b, splits) : std::max(1, splits), b.count);
-  switch (EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw : g_gemm_variant) {
+  // default policy (variant knob unset): bf16-output epilogues with no aux operand stage 64 rows
+  // per epilogue pass and run 3+ blocks per CU (variant 6: 33 KB of LDS instead of 66 KB), which
+  // overlaps one block's short K loop with the others' prologue / stores; epilogues that read an aux
+  // or residual operand or store fp32 measured faster at 2 blocks per CU with the 64-deep ring
+  // (profiles/r2_gemm_bench.txt)
+  constexpr bool occ3 = EPI == EPI_STORE_BF16 || EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16;
+  const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? 6 : 0);
+  switch (var) {
     case 1: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 2: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 3: launch_v<TileS, 32, 4, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 4: launch_v<TileS, 64, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+    case 5: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
+    case 6: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
     default: launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
   }
   return hipGetLastError();
