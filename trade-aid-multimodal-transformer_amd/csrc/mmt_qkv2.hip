@@ -147,29 +147,42 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
   for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
     for (int e = 0; e < 16; ++e) dw[ot][e] = 0.f;
-  for (int r0 = rbase; r0 < min(R, rbase + QKV2_BWD_ROWS); r0 += 256) {
-  if (r0 > rbase) __syncthreads();  // the previous chunk's LDS reads are done
-  // dout chunk and h1 chunk, row per thread, zero padded
-  {
+  // chunks of 256 rows, row per thread. The next chunk's dout / h1 pieces are loaded into registers
+  // before this chunk's MFMA work (software pipeline: every wave keeps its loads in flight through
+  // the compute; the block runs 8 chunks back to back)
+  constexpr int ND4 = (HS + 3) / 4, NH4 = (HH + 3) / 4;  // 8-B pieces of a dout / h1 row slice
+  u32x2 dv[ND4], hv[NH4];
+  auto load = [&](int r0) {
     const int rr = r0 + tid;
     const bool ok = rr < R;
     const bf16_t* d = P.dout + (int64_t)rr * ld_out + blk * HS;
+    const bf16_t* hp = P.h1 + (int64_t)rr * ld_h1 + blk * HH;
+#pragma unroll
+    for (int c = 0; c < ND4; ++c) {
+      uint32_t a = 0, b = 0;
+      if (ok) ld4_guarded<4>(d + 4 * c, HS - 4 * c, a, b);
+      dv[c] = u32x2{a, b};
+    }
+#pragma unroll
+    for (int c = 0; c < NH4; ++c) {
+      uint32_t a = 0, b = 0;
+      if (ok) ld4_guarded<4>(hp + 4 * c, HH - 4 * c, a, b);
+      hv[c] = u32x2{a, b};
+    }
+  };
+  const int rend = min(R, rbase + QKV2_BWD_ROWS);
+  load(rbase);
+  for (int r0 = rbase; r0 < rend; r0 += 256) {
+  if (r0 > rbase) __syncthreads();  // the previous chunk's LDS reads are done
+  {
     bf16_t* dd = sd + tid * SDW;
 #pragma unroll
-    for (int c = 0; c < SDW; c += 4) {
-      uint32_t a = 0, b = 0;
-      if (ok && c < HS) ld4_guarded<4>(d + c, HS - c, a, b);
-      *reinterpret_cast<u32x2*>(dd + c) = u32x2{a, b};
-    }
-    const bf16_t* hp = P.h1 + (int64_t)rr * ld_h1 + blk * HH;
+    for (int c = 0; c < SDW / 4; ++c) *reinterpret_cast<u32x2*>(dd + 4 * c) = c < ND4 ? dv[c] : u32x2{0u, 0u};
     bf16_t* hd = sh + tid * SHW;
 #pragma unroll
-    for (int c = 0; c < SHW; c += 4) {
-      uint32_t a = 0, b = 0;
-      if (ok && c < HH) ld4_guarded<4>(hp + c, HH - c, a, b);
-      *reinterpret_cast<u32x2*>(hd + c) = u32x2{a, b};
-    }
+    for (int c = 0; c < SHW / 4; ++c) *reinterpret_cast<u32x2*>(hd + 4 * c) = c < NH4 ? hv[c] : u32x2{0u, 0u};
   }
+  if (r0 + 256 < rend) load(r0 + 256);
   __syncthreads();
   // ---- dh1 for this wave's 64 rows (2 sub-tiles of 32) ----
 #pragma unroll
