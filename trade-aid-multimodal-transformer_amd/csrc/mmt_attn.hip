@@ -139,9 +139,9 @@ struct Stager {
 // Dropout keep bits of one staged chunk: LDS [8 block tiles][KT chunk tiles][32 dwords]. The block
 // tiles are the block's 8 query tiles (forward, dQ) or key tiles (dK/dV); the chunk tiles are the
 // key (query) tiles of the staged chunk. Tiles above the causal diagonal are left as zeros.
-template <int HS>
+template <int HS, int KT_ = Chunk<HS>::ROWS / 32>
 struct MaskStager {
-  static constexpr int KT = Chunk<HS>::ROWS / 32;
+  static constexpr int KT = KT_;
   static constexpr int N4 = 8 * KT * 8;  // 16-B pieces
   static constexpr int PER = (N4 + 255) / 256;
   static constexpr int DWORDS = 8 * KT * 32;
@@ -574,7 +574,13 @@ template <int HS, bool DROP>
 __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnBatch batch, int T, int H,
                                                                                        float scale) {
   using G = Geo<HS>;
-  constexpr int ROWS = Chunk<HS>::ROWS;
+  // chunk rows: hs >= 48 stages 256-row chunks (two 128-row register rounds; 80 KB of LDS, still two
+  // blocks per CU, which is what the registers allow): half the reloads and barriers of 128-row
+  // chunks, and at T = 512 each chunk holds either a whole causal triangle or a full rectangle, so
+  // the four waves' work per chunk is balanced
+  constexpr int SR = Chunk<HS>::ROWS;
+  constexpr int ROWS = HS >= 48 ? 256 : SR;
+  constexpr int NR = ROWS / SR;
   const AttnProblem& P = batch.p[blockIdx.z];
   const int nb = ((T + 31) / 32 + 7) / 8;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
@@ -590,7 +596,7 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row + tr reads
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::RW];  // V chunk: row reads
-  using MS = MaskStager<HS>;
+  using MS = MaskStager<HS, ROWS / 32>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // keep-bit lane words
   if (HS % 32 != 0)  // pad columns are read only when HS is not a multiple of 32
     for (int q = tid; q < ROWS * G::RW; q += 256)
@@ -599,10 +605,17 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   MS mst;
   // lane-word record of the keep bits (AttnProblem::dmask): after the key-major one
   const int64_t lw_off = (int64_t)(gridDim.x / nb) * (nt * (nt + 1) / 2) * 32;
-  st.load(P.k[0] + head * P.kv_hstride, P.kv_ld, P.v[0] + head * P.kv_hstride, P.kv_ld, rowbase, 0, T, tid);
-  if (DROP) mst.load(P.dmask[0] + lw_off, bh, nt, qt0, 0, true, tid);
-  st.store(ks, G::RW, vs, G::RW, tid);
-  if (DROP) mst.store(msk, tid);
+  auto stage = [&](int jj, int cc) {  // K / V rows [cc*ROWS, +ROWS) of stream jj and their keep bits
+    if (DROP) mst.load(P.dmask[jj] + lw_off, bh, nt, qt0, cc * (ROWS / 32), true, tid);
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      st.load(P.k[jj] + head * P.kv_hstride, P.kv_ld, P.v[jj] + head * P.kv_hstride, P.kv_ld, rowbase,
+              cc * ROWS + rr * SR, T, tid);
+      st.store(ks + rr * SR * G::RW, G::RW, vs + rr * SR * G::RW, G::RW, tid);
+    }
+    if (DROP) mst.store(msk, tid);
+  };
+  stage(0, 0);
   __syncthreads();
 
   const int qa = qt0 + w, qb = qt0 + 7 - w;  // qa < qb; lb implies la
@@ -684,11 +697,7 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
       if (nc == nch) { nc = 0; ++nj; }
       if (nj < P.nstreams && (nj != j || nc != c)) {
         __syncthreads();
-        st.load(P.k[nj] + head * P.kv_hstride, P.kv_ld, P.v[nj] + head * P.kv_hstride, P.kv_ld, rowbase, nc * ROWS,
-                T, tid);
-        if (DROP) mst.load(P.dmask[nj] + lw_off, bh, nt, qt0, nc * (ROWS / 32), true, tid);
-        st.store(ks, G::RW, vs, G::RW, tid);
-        if (DROP) mst.store(msk, tid);
+        stage(nj, nc);
         __syncthreads();
       }
     }
