@@ -752,9 +752,12 @@ static int g_big_mode = [] {
   const char* e = getenv("MMT_GEMM_BIG");
   return e ? atoi(e) : 1;
 }();
+// K threshold 1024 (round 2 c): at K = 512 (d512 forward GEMMs and data gradients) the 128x128 tile at
+// 2-3 blocks per CU overlaps one block's epilogue with the others' K loops and shares the chip with
+// the side stream better than the single 256x256 block per CU (target step 23.13 -> 22.73 ms)
 static int g_big_kmin = [] {
   const char* e = getenv("MMT_GEMM_BIG_KMIN");
-  return e ? atoi(e) : 512;
+  return e ? atoi(e) : 1024;
 }();
 static bool use_big(const GemmBatch& b) {
   if (!g_big_mode || b.count == 0) return false;
@@ -924,7 +927,7 @@ static hipError_t launch_f8_tile(const GemmBatch& b, hipStream_t s) {
   // the 256x256 tile where every problem fills it and K is long (as the bf16 policy), else 128x128
   bool big = g_big_mode != 0;
   for (int g = 0; g < b.count; ++g)
-    if (b.p[g].M < TileL::BM || b.p[g].N < TileL::BN || b.p[g].K < 2 * g_big_kmin) big = false;
+    if (b.p[g].M < TileL::BM || b.p[g].N < TileL::BN || b.p[g].K < g_big_kmin) big = false;
   return big ? launch_f8<TileL, EPI>(b, s) : launch_f8<TileS, EPI>(b, s);
 }
 
