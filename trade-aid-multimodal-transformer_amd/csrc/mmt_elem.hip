@@ -520,11 +520,17 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackSeg* __restrict__ s
     if (r >= S.rows) break;
     const float* s = src + S.src_off + (int64_t)r * S.cols;
     uint32_t w[4];
+    if (c + 8 <= S.cols && ((S.cols | S.src_off) & 3) == 0) {  // interior chunk: two 16-B loads
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(s + c), hi = *reinterpret_cast<const f32x4*>(s + c + 4);
+      w[0] = pack2bf(lo[0], lo[1]); w[1] = pack2bf(lo[2], lo[3]);
+      w[2] = pack2bf(hi[0], hi[1]); w[3] = pack2bf(hi[2], hi[3]);
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float a = (c + 2 * e < S.cols) ? s[c + 2 * e] : 0.f;
-      const float b = (c + 2 * e + 1 < S.cols) ? s[c + 2 * e + 1] : 0.f;
-      w[e] = pack2bf(a, b);
+      for (int e = 0; e < 4; ++e) {
+        const float a = (c + 2 * e < S.cols) ? s[c + 2 * e] : 0.f;
+        const float b = (c + 2 * e + 1 < S.cols) ? s[c + 2 * e + 1] : 0.f;
+        w[e] = pack2bf(a, b);
+      }
     }
     *reinterpret_cast<u32x4*>(dst + S.dst_off + (int64_t)r * S.dld + c) = u32x4{w[0], w[1], w[2], w[3]};
   }

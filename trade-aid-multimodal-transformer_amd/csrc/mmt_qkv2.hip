@@ -5,6 +5,8 @@
 // backward  dh1^T[i][r] = (sum_o W2[o][i] dout[r][o]) * (1 - h1[r][i]^2)
 //           dW2[o][i]  += sum_r dout[r][o] h1[r][i]        K = rows, operands by transposed LDS reads
 // blk = kind*H + head; h1 / dh1 rows hold nblk*hs/2 columns, out / dout rows nblk*hs columns.
+#include <type_traits>
+
 #include "mmt_common.h"
 #include "mmt_kernels.h"
 
@@ -24,6 +26,11 @@ __device__ __forceinline__ void ld4_guarded(const bf16_t* p, int valid, uint32_t
 }
 
 // ---------------------------------------------------------------------------------------------
+// rows per forward block: qkv2_strips(HS) strips of 128 rows, the next strip's h1 loaded into
+// registers while this one computes and stores (one load -> compute -> store chain per block leaves
+// each block's latency exposed). hs 64: 4 strips (target 94 -> 66 us); hs <= 32 keeps one strip per
+// block (4 measured 33 -> 36 us at C1: the grid already holds 12k blocks)
+constexpr int qkv2_strips(int hs) { return hs >= 48 ? 4 : 1; }
 template <int HS>
 __global__ __launch_bounds__(256) void qkv2_fwd_mfma(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
   constexpr int HH = HS / 2;
@@ -31,74 +38,86 @@ __global__ __launch_bounds__(256) void qkv2_fwd_mfma(Qkv2Batch batch, int R, int
   constexpr int KS = (HH + 15) / 16;   // k-steps over i
   constexpr int SHW = KS * 16 + 8;     // h1 tile row (zero padded to the k-steps; +8 de-conflicts)
   constexpr int SOW = HS + 8;          // out tile row
+  constexpr int BR = 128 * qkv2_strips(HS);
   const Qkv2Problem& P = batch.p[blockIdx.z];
   // grid.x = row blocks x nblk, blk fastest in logical order (one row's blocks share its lines)
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int nblk = gridDim.x / ((R + 127) / 128);
+  const int nblk = gridDim.x / ((R + BR - 1) / BR);
   const int blk = tile % nblk, rb = tile / nblk;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int r0 = rb * 128;
   __shared__ __attribute__((aligned(16))) bf16_t sh[128 * SHW];
   __shared__ __attribute__((aligned(16))) bf16_t so[128 * SOW];
   // h1 strip [128][HH] in 8-B pieces, consecutive lanes along a row; pad columns zero
   constexpr int HPC = HH / 4, PPC = (KS * 16 - HH) / 4;
   constexpr int NL = (128 * HPC + 255) / 256;
-  u32x2 hv[NL];  // every load in flight before the LDS stores
+  u32x2 hv[NL];  // every load of a strip in flight before its LDS stores
+  auto load = [&](int r0) {
 #pragma unroll
-  for (int u = 0; u < NL; ++u) {
-    const int c = tid + 256 * u, row = c / HPC, col = (c % HPC) * 4;
-    hv[u] = u32x2{0u, 0u};
-    if (c < 128 * HPC && r0 + row < R)
-      hv[u] = *reinterpret_cast<const u32x2*>(P.h1 + (int64_t)(r0 + row) * ld_h1 + blk * HH + col);
-  }
-#pragma unroll
-  for (int u = 0; u < NL; ++u) {
-    const int c = tid + 256 * u;
-    if (c < 128 * HPC) *reinterpret_cast<u32x2*>(sh + (c / HPC) * SHW + (c % HPC) * 4) = hv[u];
-  }
-  if (PPC > 0)
+    for (int u = 0; u < NL; ++u) {
+      const int c = tid + 256 * u, row = c / HPC, col = (c % HPC) * 4;
+      hv[u] = u32x2{0u, 0u};
+      if (c < 128 * HPC && r0 + row < R)
+        hv[u] = *reinterpret_cast<const u32x2*>(P.h1 + (int64_t)(r0 + row) * ld_h1 + blk * HH + col);
+    }
+  };
+  if (PPC > 0)  // pad columns: zero once (the strips only rewrite columns < HH)
     for (int c = tid; c < 128 * PPC; c += 256) {
       const int row = c / PPC, col = HH + (c % PPC) * 4;
       *reinterpret_cast<u32x2*>(sh + row * SHW + col) = u32x2{0u, 0u};
     }
+  // this wave's W2 fragments (the same for every strip)
   const float* w2 = P.w2 + (int64_t)blk * HS * HH;
-  __syncthreads();
-  const int lr = w * 32;
+  bf16x8 wa[NOT][KS];
 #pragma unroll
-  for (int ot = 0; ot < NOT; ++ot) {
-    const int o = ot * 32 + r;
-    f32x16 acc;
+  for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      bf16x8 wa;
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int i = 16 * s + 8 * h + j;
-        wa[j] = (__bf16)((o < HS && i < HH) ? w2[o * HH + i] : 0.f);
+        const int o = ot * 32 + r, i = 16 * s + 8 * h + j;
+        wa[ot][s][j] = (__bf16)((o < HS && i < HH) ? w2[o * HH + i] : 0.f);
       }
-      const bf16x8 hb = *reinterpret_cast<const bf16x8*>(sh + (lr + r) * SHW + 16 * s + 8 * h);
-      acc = mfma32(wa, hb, acc);  // D[o][row]
-    }
-    // lane owns row (r) and o = ot*32 + (e&3) + 8(e>>2) + 4h
+  const int lr = w * 32;
+  const int rend = min(R, rb * BR + BR);
+  load(rb * BR);
+  for (int r0 = rb * BR; r0 < rend; r0 += 128) {
+    if (r0 > rb * BR) __syncthreads();  // the previous strip's LDS reads (sh, so) are done
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int o0 = ot * 32 + 8 * g + 4 * h;
-      if (o0 < HS)
-        *reinterpret_cast<u32x2*>(so + (lr + r) * SOW + o0) =
-            u32x2{pack2bf(acc[4 * g], acc[4 * g + 1]), pack2bf(acc[4 * g + 2], acc[4 * g + 3])};
+    for (int u = 0; u < NL; ++u) {
+      const int c = tid + 256 * u;
+      if (c < 128 * HPC) *reinterpret_cast<u32x2*>(sh + (c / HPC) * SHW + (c % HPC) * 4) = hv[u];
     }
-  }
-  __syncthreads();
-  // out strip [128][HS] in 8-B pieces, consecutive lanes along a row
-  constexpr int OPC = HS / 4;
-  for (int c = tid; c < 128 * OPC; c += 256) {
-    const int row = c / OPC, col = (c % OPC) * 4;
-    if (r0 + row < R)
-      *reinterpret_cast<u32x2*>(P.out + (int64_t)(r0 + row) * ld_out + blk * HS + col) =
-          *reinterpret_cast<const u32x2*>(so + row * SOW + col);
+    __syncthreads();
+    if (r0 + 128 < rend) load(r0 + 128);
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) {
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(sh + (lr + r) * SHW + 16 * s + 8 * h);
+        acc = mfma32(wa[ot][s], hb, acc);  // D[o][row]
+      }
+      // lane owns row (r) and o = ot*32 + (e&3) + 8(e>>2) + 4h
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int o0 = ot * 32 + 8 * g + 4 * h;
+        if (o0 < HS)
+          *reinterpret_cast<u32x2*>(so + (lr + r) * SOW + o0) =
+              u32x2{pack2bf(acc[4 * g], acc[4 * g + 1]), pack2bf(acc[4 * g + 2], acc[4 * g + 3])};
+      }
+    }
+    __syncthreads();
+    // out strip [128][HS] in 8-B pieces, consecutive lanes along a row
+    constexpr int OPC = HS / 4;
+    for (int c = tid; c < 128 * OPC; c += 256) {
+      const int row = c / OPC, col = (c % OPC) * 4;
+      if (r0 + row < R)
+        *reinterpret_cast<u32x2*>(P.out + (int64_t)(r0 + row) * ld_out + blk * HS + col) =
+            *reinterpret_cast<const u32x2*>(so + row * SOW + col);
+    }
   }
 }
 
@@ -150,37 +169,32 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
   // chunks of 256 rows, row per thread. The next chunk's dout / h1 pieces are loaded into registers
   // before this chunk's MFMA work (software pipeline: every wave keeps its loads in flight through
   // the compute; the block runs 8 chunks back to back)
-  constexpr int ND4 = (HS + 3) / 4, NH4 = (HH + 3) / 4;  // 8-B pieces of a dout / h1 row slice
-  u32x2 dv[ND4], hv[NH4];
+  // 16-B pieces of a dout / h1 row slice (8-B pieces when the h1 slice is not a multiple of 8)
+  constexpr int PW = (HH % 8 == 0) ? 8 : 4;  // elements per piece
+  constexpr int ND = HS / PW, NH = HH / PW;
+  using Piece = typename std::conditional<PW == 8, u32x4, u32x2>::type;
+  Piece dv[ND], hv[NH];
   auto load = [&](int r0) {
     const int rr = r0 + tid;
     const bool ok = rr < R;
-    const bf16_t* d = P.dout + (int64_t)rr * ld_out + blk * HS;
-    const bf16_t* hp = P.h1 + (int64_t)rr * ld_h1 + blk * HH;
+    const Piece* d = reinterpret_cast<const Piece*>(P.dout + (int64_t)rr * ld_out + blk * HS);
+    const Piece* hp = reinterpret_cast<const Piece*>(P.h1 + (int64_t)rr * ld_h1 + blk * HH);
 #pragma unroll
-    for (int c = 0; c < ND4; ++c) {
-      uint32_t a = 0, b = 0;
-      if (ok) ld4_guarded<4>(d + 4 * c, HS - 4 * c, a, b);
-      dv[c] = u32x2{a, b};
-    }
+    for (int c = 0; c < ND; ++c) dv[c] = ok ? d[c] : Piece{};
 #pragma unroll
-    for (int c = 0; c < NH4; ++c) {
-      uint32_t a = 0, b = 0;
-      if (ok) ld4_guarded<4>(hp + 4 * c, HH - 4 * c, a, b);
-      hv[c] = u32x2{a, b};
-    }
+    for (int c = 0; c < NH; ++c) hv[c] = ok ? hp[c] : Piece{};
   };
   const int rend = min(R, rbase + QKV2_BWD_ROWS);
   load(rbase);
   for (int r0 = rbase; r0 < rend; r0 += 256) {
   if (r0 > rbase) __syncthreads();  // the previous chunk's LDS reads are done
   {
-    bf16_t* dd = sd + tid * SDW;
+    Piece* dd = reinterpret_cast<Piece*>(sd + tid * SDW);
 #pragma unroll
-    for (int c = 0; c < SDW / 4; ++c) *reinterpret_cast<u32x2*>(dd + 4 * c) = c < ND4 ? dv[c] : u32x2{0u, 0u};
-    bf16_t* hd = sh + tid * SHW;
+    for (int c = 0; c < SDW / PW; ++c) dd[c] = c < ND ? dv[c] : Piece{};
+    Piece* hd = reinterpret_cast<Piece*>(sh + tid * SHW);
 #pragma unroll
-    for (int c = 0; c < SHW / 4; ++c) *reinterpret_cast<u32x2*>(hd + 4 * c) = c < NH4 ? hv[c] : u32x2{0u, 0u};
+    for (int c = 0; c < SHW / PW; ++c) hd[c] = c < NH ? hv[c] : Piece{};
   }
   if (r0 + 256 < rend) load(r0 + 256);
   __syncthreads();
@@ -250,12 +264,18 @@ static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_o
     hipLaunchKernelGGL(qkv2_bwd_mfma<HS>, dim3((R + QKV2_BWD_ROWS - 1) / QKV2_BWD_ROWS * nblk, 1, b.count), dim3(256), 0, s,
                        b, R, ld_h1, ld_out);
   else
-    hipLaunchKernelGGL(qkv2_fwd_mfma<HS>, dim3((R + 127) / 128 * nblk, 1, b.count), dim3(256), 0, s, b, R, ld_h1, ld_out);
+    hipLaunchKernelGGL(qkv2_fwd_mfma<HS>, dim3((R + 128 * qkv2_strips(HS) - 1) / (128 * qkv2_strips(HS)) * nblk, 1, b.count),
+                       dim3(256), 0, s, b, R, ld_h1, ld_out);
 }
 
 static hipError_t qkv2_dispatch(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, bool bwd,
                                 hipStream_t s) {
   if (b.count == 0 || R == 0) return hipSuccess;
+  if (bwd) {  // the backward stages dout / h1 row slices as 16-B pieces
+    if ((ld_h1 | ld_out) & 7) return hipErrorInvalidValue;
+    for (int g = 0; g < b.count; ++g)
+      if (((uintptr_t)b.p[g].h1 | (uintptr_t)b.p[g].dout) & 15) return hipErrorInvalidValue;
+  }
   switch (hs) {
     case 8: qkv2_launch<8>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
     case 16: qkv2_launch<16>(b, R, nblk, ld_h1, ld_out, bwd, s); break;
