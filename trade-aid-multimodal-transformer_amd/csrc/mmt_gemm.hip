@@ -732,7 +732,13 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
   // or residual operand or store fp32 measured faster at 2 blocks per CU with the 64-deep ring
   // (profiles/r2_gemm_bench.txt)
   constexpr bool occ3 = EPI == EPI_STORE_BF16 || EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16;
-  const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? 6 : 0);
+  static const int env_dw = [] {  // tuning knob: pipeline variant of the 128x128 weight-gradient GEMMs
+    const char* e = getenv("MMT_GEMM_DW_VARIANT");
+    return e ? atoi(e) : -1;
+  }();
+  const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw
+                  : (!A_KC && !B_KC && env_dw >= 0) ? env_dw
+                  : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? 6 : 0);
   switch (var) {
     case 1: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 2: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
