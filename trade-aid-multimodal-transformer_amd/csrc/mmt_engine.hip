@@ -1317,7 +1317,6 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   // FFN
   GemmBatch dw{}; dw.count = M;
   GemmBatch dx{}; dx.count = M;
-  ColsumBatch cs{}; cs.count = M;
   LnBatch lb{}; lb.count = M;
   for (int i = 0; i < M; ++i) {
     // dres16[i] carries the FFN dropout mask; the FFN output-bias grad was summed with it
@@ -1383,17 +1382,16 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   for (int i = 0; i < M; ++i) {
     qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].dout = r.W<bf16_t>(p.gqkv[i]);
     qb.p[i].dh1 = r.W<bf16_t>(p.gh1[i]); qb.p[i].dw2 = grads + x[i].w2;
+    qb.p[i].db1 = grads + x[i].b1;  // stage-1 bias gradient: column sums of dh1, fused
   }
   r.ok(mmt_launch_qkv2_bwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_bwd");
   for (int i = 0; i < M; ++i) {
     const bf16_t* g = r.W<bf16_t>(p.gh1[i]);
     dw.p[i] = gp_dw(g, ldh1, r.W<bf16_t>(a[i].a), C, grads, x[i].W1, R);
-    colsum_add(r, cs, i, g, ldh1, grads + x[i].b1, 3 * H * c->hh, nullptr, 1.f);
     dx.p[i] = gp_dx(g, ldh1, wpk, x[i].W1, R);
     dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
   }
   r.dwgemm(dw, "qkv1_dw");
-  r.ok(mmt_launch_colsum(cs, R, r.s), "qkv1_db");
   r.gemm(dx, true, false, EPI_STORE_F32, 1, "qkv1_dx");
   r.flush();
   d16_advance(c);

@@ -182,6 +182,8 @@ struct Qkv2Problem {
   const bf16_t* dout;  // [R, nblk*hs]
   bf16_t* dh1;         // [R, nblk*hs/2] = (W2^T dout) * (1 - h1^2)
   float* dw2;          // atomic accumulate [nblk][hs][hs/2]
+  float* db1;          // optional: atomic accumulate of the column sums of dh1 [nblk*hs/2] (the stage-1
+                       // bias gradient, model.py:36-50), fused so no separate column-sum pass reads dh1
 };
 struct Qkv2Batch { Qkv2Problem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_qkv2_fwd(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, hipStream_t s);

@@ -166,6 +166,8 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
   for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
     for (int e = 0; e < 16; ++e) dw[ot][e] = 0.f;
+  // fused stage-1 bias gradient: this lane's running column sums of dh1 (columns 8g + 4h + e)
+  float cs[4][4] = {};
   // chunks of 256 rows, row per thread. The next chunk's dout / h1 pieces are loaded into registers
   // before this chunk's MFMA work (software pipeline: every wave keeps its loads in flight through
   // the compute; the block runs 8 chunks back to back)
@@ -221,6 +223,8 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
           float t[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) { const float x = bf2f(hv[e]); t[e] = acc[4 * g + e] * (1.f - x * x); }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cs[g][e] += t[e];
           *reinterpret_cast<u32x2*>(P.dh1 + (int64_t)grow * ld_h1 + blk * HH + i0) =
               u32x2{pack2bf(t[0], t[1]), pack2bf(t[2], t[3])};
         }
@@ -239,7 +243,21 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
     }
   }
   }  // chunks
+  __shared__ float dbr[4][32];
+  if (P.db1) {  // column sums: over the 32 row lanes of each half, then the 4 waves, one atomic per column
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = cs[g][e];
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+        if (r == 0 && 8 * g + 4 * h + e < 32) dbr[w][8 * g + 4 * h + e] = v;
+      }
+  }
   __syncthreads();
+  if (P.db1 && tid < HH)
+    atomicAdd(P.db1 + (int64_t)blk * HH + tid, (dbr[0][tid] + dbr[1][tid]) + (dbr[2][tid] + dbr[3][tid]));
   float* red = reinterpret_cast<float*>(sd);  // reuse: [4 waves][NOT*32 o][32 i] floats
 #pragma unroll
   for (int ot = 0; ot < NOT; ++ot)
