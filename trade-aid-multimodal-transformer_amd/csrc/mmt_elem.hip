@@ -17,6 +17,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnBatch batch, int R, int C
   const LnProblem& P = batch.p[blockIdx.z];
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPI;
+  if (blockIdx.x == 0 && blockIdx.z == 0) {
+    if ((int)threadIdx.x < batch.nzero_f) batch.zero_f[threadIdx.x] = 0.f;
+    if ((int)threadIdx.x < batch.nzero_i) batch.zero_i[threadIdx.x] = 0;
+  }
   const int C4 = C >> 2;
   f32x4 v[RPI][NV];
 #pragma unroll

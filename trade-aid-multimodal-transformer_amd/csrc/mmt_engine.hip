@@ -933,12 +933,14 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
     h2.p[i] = gp_fwd(r.W<bf16_t>(p.hh[i]), c->ldvh[i], wpk, c->post[i].H2, R);
     h2.p[i].bias = r.P(c->post[i].b2); h2.p[i].o32 = logits[i]; h2.p[i].ldc = c->V[i];
   }
+  if (tgt) {  // the loss accumulators and this forward's flag word, zeroed by the LN launch
+    lf.zero_f = losses; lf.nzero_f = M;
+    lf.zero_i = r.W<int>(p.flag); lf.nzero_i = 1;
+  }
   r.ok(mmt_launch_ln_fwd(lf, R, C, r.s), "lnf_fwd");
   r.gemm(h0, true, true, EPI_BIAS_TANH_BF16, 1, "head0");
   r.gemm(h2, true, true, EPI_STORE_F32, 1, "head2");
   if (tgt && r.rc == MMT_OK) {
-    r.ok(hipMemsetAsync(losses, 0, sizeof(float) * M, r.s), "memset losses");
-    r.ok(hipMemsetAsync(r.W<int>(p.flag), 0, sizeof(int), r.s), "memset flag");
     CeBatch cb{}; cb.count = M;
     for (int i = 0; i < M; ++i) {
       cb.p[i].logits = logits[i]; cb.p[i].tgt = tgt[i]; cb.p[i].dlogits = r.W<bf16_t>(p.dlog[i]);

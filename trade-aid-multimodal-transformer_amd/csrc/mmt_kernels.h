@@ -105,7 +105,14 @@ struct LnProblem {
   float drop_scale;
   float* dsum;          // optional: dsum[c] += sum_r (masked) dx16 value (the consumer's bias gradient)
 };
-struct LnBatch { LnProblem p[MMT_MAX_GROUP]; int count; };
+struct LnBatch {
+  LnProblem p[MMT_MAX_GROUP];
+  int count;
+  // forward: optional words zeroed by the launch (the loss accumulators and this forward's
+  // non-finite flag the cross-entropy kernel adds into next), instead of two memset launches
+  float* zero_f; int nzero_f;
+  int* zero_i; int nzero_i;
+};
 hipError_t mmt_launch_ln_fwd(const LnBatch& b, int R, int C, hipStream_t s);
 hipError_t mmt_launch_ln_bwd(const LnBatch& b, int R, int C, hipStream_t s);
 
