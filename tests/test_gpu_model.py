@@ -125,10 +125,11 @@ def test_dropout_step_matches_oracle_masks(name, p):
         assert rel(lg[i], torch.from_numpy(z[f"logits.{i}"])) < 2e-2, i
 
 
-@pytest.mark.parametrize("C,H,T,cross,p", [(64, 2, 288, [True, False], 0.2), (128, 2, 160, [False, True], 0.1)])
+@pytest.mark.parametrize("C,H,T,cross,p", [(64, 2, 288, [True, False], 0.2), (128, 2, 160, [False, True], 0.1),
+                                             (128, 2, 300, [True, False], 0.1)])
 def test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p):
-    """Dropout at sequence lengths past one LDS chunk (hs 32: 256 rows, hs 64: 128 rows) with a
-    ragged last tile: the keep bits of attn_mask_kernel, staged chunk by chunk in all three
+    """Dropout at sequence lengths past one LDS chunk (hs 32: 256 rows, hs 64: 128 rows; the hs-64 dQ
+    pass: 256 rows, so T = 300 takes it past one) with a ragged last tile: the keep bits of attn_mask_kernel, staged chunk by chunk in all three
     attention kernels, against the oracle's hash masks (random init, the oracle as reference)."""
     import mmt_oracle as O
     import model as mmt_model
