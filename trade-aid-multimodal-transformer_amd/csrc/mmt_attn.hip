@@ -431,17 +431,33 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
       FwdQ<HS>& q = u == 0 ? A : Bq;
       const float l = xhalf_sum(q.l);
       const float inv = (l > 0.f) ? (DROP ? P.drop_scale : 1.f) / l : 0.f;
+      // row-per-lane O^T halves (lane r: d 8g..8g+3, lane r + 32: 8g+4..8g+7) exchanged across the
+      // wave halves by v_permlane32_swap so every lane holds 8 consecutive d of its row: 16-B stores,
+      // half the store instructions of the 8-B form (the epilogue store tail is issue-bound). The
+      // swaps run on every lane (both halves of a row are live or dead together).
+      u32x4 ov[G::ND][2];
+#pragma unroll
+      for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const int ga = 2 * pr, gb = 2 * pr + 1;
+          const uint32_t x0 = pack2bf(q.o[dt][4 * ga] * inv, q.o[dt][4 * ga + 1] * inv);
+          const uint32_t x1 = pack2bf(q.o[dt][4 * ga + 2] * inv, q.o[dt][4 * ga + 3] * inv);
+          const uint32_t y0 = pack2bf(q.o[dt][4 * gb] * inv, q.o[dt][4 * gb + 1] * inv);
+          const uint32_t y1 = pack2bf(q.o[dt][4 * gb + 2] * inv, q.o[dt][4 * gb + 3] * inv);
+          const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+          ov[dt][pr] = u32x4{s0[0], s1[0], s0[1], s1[1]};  // d = dt*32 + 16 pr + 8 h + 0..7
+        }
       if (live && q.tq < T) {
         if (h == 0) P.lse[j][(int64_t)bh * T + q.tq] = (q.m + __log2f(l)) * kLn2;
         bf16_t* dst = (P.nstreams > 1 ? P.oj[j] : P.o) + (rowbase + q.tq) * P.o_ld + head * HS;
 #pragma unroll
         for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int d0 = dt * 32 + 8 * g + 4 * h;
-            if (d0 < HS)
-              *reinterpret_cast<u32x2*>(dst + d0) = u32x2{pack2bf(q.o[dt][4 * g] * inv, q.o[dt][4 * g + 1] * inv),
-                                                          pack2bf(q.o[dt][4 * g + 2] * inv, q.o[dt][4 * g + 3] * inv)};
+          for (int pr = 0; pr < 2; ++pr) {
+            const int d0 = dt * 32 + 16 * pr + 8 * h;
+            if (d0 < HS) *reinterpret_cast<u32x4*>(dst + d0) = ov[dt][pr];
           }
       }
     }
@@ -458,16 +474,17 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d0 = dt * 32 + 8 * g + 4 * h;
+        for (int pr = 0; pr < 2; ++pr) {
+          const int d0 = dt * 32 + 16 * pr + 8 * h;  // the 16-B pieces this lane wrote
           if (d0 >= HS) continue;
-          float t[4] = {0.f, 0.f, 0.f, 0.f};
+          float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
           for (int jj = 0; jj < P.nstreams; ++jj) {
-            const u32x2 v = *reinterpret_cast<const u32x2*>(P.oj[jj] + off + d0);
-            t[0] += bf2f(v[0] & 0xffff); t[1] += bf2f(v[0] >> 16);
-            t[2] += bf2f(v[1] & 0xffff); t[3] += bf2f(v[1] >> 16);
+            const u32x4 v = *reinterpret_cast<const u32x4*>(P.oj[jj] + off + d0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { t[2 * e] += bf2f(v[e] & 0xffff); t[2 * e + 1] += bf2f(v[e] >> 16); }
           }
-          *reinterpret_cast<u32x2*>(P.o + off + d0) = u32x2{pack2bf(t[0], t[1]), pack2bf(t[2], t[3])};
+          *reinterpret_cast<u32x4*>(P.o + off + d0) =
+              u32x4{pack2bf(t[0], t[1]), pack2bf(t[2], t[3]), pack2bf(t[4], t[5]), pack2bf(t[6], t[7])};
         }
     }
   }
@@ -706,16 +723,29 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   for (int u = 0; u < 2; ++u) {
     const bool ok = u == 0 ? oka : okb;
     const DqQ<HS>& q = u == 0 ? A : Bq;
+    // 16-B stores of 8 consecutive d per lane after a v_permlane32_swap exchange of the row halves
+    // (as the forward's O); the swaps run on every lane
+    u32x4 dv[G::ND][2];
+#pragma unroll
+    for (int dt = 0; dt < G::ND; ++dt)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int ga = 2 * pr, gb = 2 * pr + 1;
+        const uint32_t x0 = pack2bf(q.dq[dt][4 * ga] * scale, q.dq[dt][4 * ga + 1] * scale);
+        const uint32_t x1 = pack2bf(q.dq[dt][4 * ga + 2] * scale, q.dq[dt][4 * ga + 3] * scale);
+        const uint32_t y0 = pack2bf(q.dq[dt][4 * gb] * scale, q.dq[dt][4 * gb + 1] * scale);
+        const uint32_t y1 = pack2bf(q.dq[dt][4 * gb + 2] * scale, q.dq[dt][4 * gb + 3] * scale);
+        const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        dv[dt][pr] = u32x4{s0[0], s1[0], s0[1], s1[1]};
+      }
     if (ok) {
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d0 = dt * 32 + 8 * g + 4 * h;
-          if (d0 < HS)
-            *reinterpret_cast<u32x2*>(P.dq + (rowbase + q.tq) * P.dq_ld + head * HS + d0) =
-                u32x2{pack2bf(q.dq[dt][4 * g] * scale, q.dq[dt][4 * g + 1] * scale),
-                      pack2bf(q.dq[dt][4 * g + 2] * scale, q.dq[dt][4 * g + 3] * scale)};
+        for (int pr = 0; pr < 2; ++pr) {
+          const int d0 = dt * 32 + 16 * pr + 8 * h;
+          if (d0 < HS) *reinterpret_cast<u32x4*>(P.dq + (rowbase + q.tq) * P.dq_ld + head * HS + d0) = dv[dt][pr];
         }
     }
   }
@@ -1167,12 +1197,18 @@ static hipError_t attn_dispatch(const AttnBatch& b, int B, int T, int H, int hs,
       for (int j = 0; j < b.p[g].nstreams; ++j)
         if (!b.p[g].dmask[j]) return hipErrorInvalidValue;
   }
+  for (int g = 0; g < b.count; ++g) {  // O / O_j leave the forward as 16-B row pieces
+    if (b.p[g].o_ld & 7 || ((uintptr_t)b.p[g].o & 15)) return hipErrorInvalidValue;
+    for (int j = 0; j < b.p[g].nstreams && b.p[g].nstreams > 1; ++j)
+      if ((uintptr_t)b.p[g].oj[j] & 15) return hipErrorInvalidValue;
+  }
   if (bwd) {  // all problems in a bwd batch must share nstreams (grid.y = B*H*nstreams)
     for (int g = 1; g < b.count; ++g)
       if (b.p[g].nstreams != b.p[0].nstreams) return hipErrorInvalidValue;
-    // dK / dV leave the kernel as 16-B row pieces (8-element aligned rows and head offsets)
+    // dQ, dK, dV leave the kernels as 16-B row pieces (8-element aligned rows and head offsets)
     for (int g = 0; g < b.count; ++g) {
       if ((b.p[g].dkv_ld & 7) || (b.p[g].dkv_hstride & 7)) return hipErrorInvalidValue;
+      if ((b.p[g].dq_ld & 7) || ((uintptr_t)b.p[g].dq & 15)) return hipErrorInvalidValue;
       for (int j = 0; j < b.p[g].nstreams; ++j)
         if (((uintptr_t)b.p[g].dk[j] | (uintptr_t)b.p[g].dv[j]) & 15) return hipErrorInvalidValue;
     }
