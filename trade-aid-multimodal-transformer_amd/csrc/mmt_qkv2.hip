@@ -110,13 +110,13 @@ __global__ __launch_bounds__(256) void qkv2_fwd_mfma(Qkv2Batch batch, int R, int
       }
     }
     __syncthreads();
-    // out strip [128][HS] in 8-B pieces, consecutive lanes along a row
-    constexpr int OPC = HS / 4;
+    // out strip [128][HS] in 16-B pieces, consecutive lanes along a row
+    constexpr int OPC = HS / 8;
     for (int c = tid; c < 128 * OPC; c += 256) {
-      const int row = c / OPC, col = (c % OPC) * 4;
+      const int row = c / OPC, col = (c % OPC) * 8;
       if (r0 + row < R)
-        *reinterpret_cast<u32x2*>(P.out + (int64_t)(r0 + row) * ld_out + blk * HS + col) =
-            *reinterpret_cast<const u32x2*>(so + row * SOW + col);
+        *reinterpret_cast<u32x4*>(P.out + (int64_t)(r0 + row) * ld_out + blk * HS + col) =
+            *reinterpret_cast<const u32x4*>(so + row * SOW + col);
     }
   }
 }
@@ -289,6 +289,11 @@ static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_o
 static hipError_t qkv2_dispatch(const Qkv2Batch& b, int R, int nblk, int hs, int ld_h1, int ld_out, bool bwd,
                                 hipStream_t s) {
   if (b.count == 0 || R == 0) return hipSuccess;
+  if (!bwd) {  // the forward stores 16-B row pieces of out
+    if (ld_out & 7) return hipErrorInvalidValue;
+    for (int g = 0; g < b.count; ++g)
+      if ((uintptr_t)b.p[g].out & 15) return hipErrorInvalidValue;
+  }
   if (bwd) {  // the backward stages dout / h1 row slices as 16-B pieces
     if ((ld_h1 | ld_out) & 7) return hipErrorInvalidValue;
     for (int g = 0; g < b.count; ++g)
