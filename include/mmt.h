@@ -91,12 +91,15 @@ int mmt_forward(mmt_ctx* ctx, void* stream, int32_t batch, const int64_t* const*
  * [batch, V_i], the logits at position pos. Keys / values of positions < pos come from the last
  * mmt_forward on this workspace (the prefill: prompt right-padded to block_size) and the decode
  * steps since, which this step extends by position pos. Eval semantics (no dropout); the weights
- * are the ones packed by that prefill forward. MMT_ERR_STATE without a prefill. */
+ * are the ones packed by that prefill forward. MMT_ERR_STATE without a prefill, after a prefill
+ * that sampled dropout (training != 0 with dropout > 0: its keys / values are not the eval ones),
+ * and at precision fp8 (the prefill's MX-fp8 GEMMs would not match a bf16 decode). */
 int mmt_decode_step(mmt_ctx* ctx, void* stream, int32_t batch, int32_t pos, const int64_t* const* idx,
                     const float* params, float* const* logits, void* workspace);
 
 /* failure detection (the reference's guard is the NaN check on eval losses,
- * main.py:606): byte offset in the workspace (for this batch size) of two int32 bitmasks. The
+ * main.py:606): byte offset in the workspace of two int32 bitmasks (the same for every batch size;
+ * the query never touches the workspace plan of a pending backward or decode). The
  * loss kernel sets bit i of both when modality i's mean CE is NaN or Inf; word 0 is cleared by
  * every mmt_forward with targets (the last forward's flags), word 1 only by the caller (sticky
  * since the caller last cleared it; zero it when the workspace is allocated). Read them when the

@@ -133,9 +133,10 @@ def run(cfg, data, log=print):
             losses = estimate_loss(it, max_iters)
             now = datetime.now().strftime("%H:%M:%S")
             bad = m.nonfinite_loss_mask(sticky=True, clear=True)  # device flag of the loss kernel
-            if bad is not None and int(bad.item()):
+            bad = int(bad.item()) if bad is not None else 0     # one sync
+            if bad:
                 names = [str(p[9] or f"Modality {i + 1}") for i, p in enumerate(m.all_modality_params)
-                         if int(bad.item()) >> i & 1]
+                         if bad >> i & 1]
                 log(f"Warning: non-finite loss since the last evaluation in: {', '.join(names)} | {now}")
             history.append((it, losses["train"], losses["val"]))
             if not (np.isnan(losses["train"]) or np.isnan(losses["val"])):

@@ -131,8 +131,47 @@ def init_params(cfg, generator=None):
 # --------------------------------------------------------------------------------------
 # forward (per-head eager restatement)
 # --------------------------------------------------------------------------------------
+# --------------------------------------------------------------------------------------
+# bf16 emulation (diagnostic, not the reference): every matrix product with bf16-rounded operands
+# and fp32 accumulation, in the forward AND in both backward products -- the rounding sites of the
+# build's MFMA path (LN outputs, tanh / ReLU hiddens, Q/K/V, attention probabilities P, dO, dS,
+# dlogits and every other GEMM input rounded to bf16; residual stream, softmax, LayerNorm
+# statistics and all accumulations fp32). `forward(..., emulate_bf16=True)` gives the error floor a
+# bf16-MFMA implementation of the reference algorithm is expected to show against the fp32
+# reference, which tests/test_gpu_scale.py compares the HIP path's error with.
+# --------------------------------------------------------------------------------------
+_EMU = {"bf16": False}
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+class _MMBf16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ab, bb = _bf(a), _bf(b)
+        ctx.save_for_backward(ab, bb)
+        return ab @ bb
+
+    @staticmethod
+    def backward(ctx, g):
+        ab, bb = ctx.saved_tensors
+        gb = _bf(g)
+        ga = gb @ bb.transpose(-2, -1)
+        if bb.dim() == 2:  # weight operand: sum over every leading (row) dimension
+            gw = ab.reshape(-1, ab.shape[-1]).t() @ gb.reshape(-1, gb.shape[-1])
+        else:
+            gw = ab.transpose(-2, -1) @ gb
+        return ga, gw
+
+
+def _mm(a, b):
+    return _MMBf16.apply(a, b) if _EMU["bf16"] else a @ b
+
+
 def _lin(x, w, b=None):
-    y = x @ w.t()
+    y = _mm(x, w.t())
     return y + b if b is not None else y
 
 
@@ -246,13 +285,13 @@ def _head(sd, pre, x, p, training, dm=None, fp8=False):
         return _lin(h, sd[f"{pre}{kind}.2.weight"])
     k = mlp("key")
     q = mlp("query")
-    aff = q @ k.transpose(-2, -1) * k.shape[-1] ** -0.5
+    aff = _mm(q, k.transpose(-2, -1)) * k.shape[-1] ** -0.5
     tril = torch.tril(torch.ones(T, T))
     aff = aff.masked_fill(tril == 0, float("-inf"))
     aff = F.softmax(aff, dim=-1)
     aff = _drop(aff, p, training, dm)
     v = mlp("value")
-    return aff @ v
+    return _mm(aff, v)
 
 
 def _proj(sd, pre, x):
@@ -285,12 +324,12 @@ def _cross(sd, pre, qx, kv_list, cfg, training, hd=None, l=0, i=0):
         for j, kvx in enumerate(kv_list):
             kv = _lin(kvx, sd[f"{hp}kv_projections.{j}.weight"])
             k, v = kv.split(hs, dim=-1)
-            aff = q @ k.transpose(-2, -1) * k.shape[-1] ** -0.5
+            aff = _mm(q, k.transpose(-2, -1)) * k.shape[-1] ** -0.5
             aff = aff.masked_fill(tril == 0, float("-inf"))
             aff = F.softmax(aff, dim=-1)
             aff = _drop(aff, cfg.dropout, training,
                         (lambda: hd.probs(l, i, SITE_CA_PROB, j, h, cfg.H, B, T)) if hd else None)
-            outs.append(aff @ v)
+            outs.append(_mm(aff, v))
         heads.append(sum(outs))
     out = torch.cat(heads, dim=-1)
     return _drop(_proj(sd, pre, out), cfg.dropout, training,
@@ -354,15 +393,20 @@ def forward(sd, cfg, idx_list, targets_list=None, training=False, hash_dropout=N
     return logits, losses
 
 
-def forward_backward(sd, cfg, idx_list, tgt_list, hash_dropout=None):
+def forward_backward(sd, cfg, idx_list, tgt_list, hash_dropout=None, emulate_bf16=False):
     """One train-step forward + backward of sum(losses) (main.py:642-649). Returns logits,
     losses and grads (None where the reference leaves .grad None). With hash_dropout the
-    step runs in training mode with those dropout masks."""
+    step runs in training mode with those dropout masks; emulate_bf16 rounds every matrix
+    product's operands to bf16 (the diagnostic floor model above, not the reference)."""
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
-    logits, losses = forward(leaves, cfg, idx_list, tgt_list, training=hash_dropout is not None,
-                             hash_dropout=hash_dropout)
-    total = sum(losses)
-    total.backward()
+    _EMU["bf16"] = bool(emulate_bf16)
+    try:
+        logits, losses = forward(leaves, cfg, idx_list, tgt_list, training=hash_dropout is not None,
+                                 hash_dropout=hash_dropout)
+        total = sum(losses)
+        total.backward()
+    finally:
+        _EMU["bf16"] = False
     grads = {k: (v.grad.detach().clone() if v.grad is not None else None) for k, v in leaves.items()}
     return [l.detach() for l in logits], [l.detach() for l in losses], grads
 

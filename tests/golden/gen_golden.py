@@ -23,6 +23,8 @@ Scale fixtures (model-level parity at the BASELINE configs), paramet
   f_c1     C1 dims: C=256 H=8 L=6 T=256 M=4 V=[900,13,144,5] cross=[T,F,F,F] B=2
   f_m8     8 modalities (C3's grouping): C=128 H=2 (hs 64) L=2 T=128 V=[900,13,144,5]x2
            cross=[T,T,F,F,T,T,F,F] B=2 (4 query modalities x 7 KV streams)
+  f_t1024  f_m8's modalities at C3's sequence length: C=128 H=2 (hs 64) L=1 T=1024 B=1
+  f_t4096  C4's sequence length and head size: C=64 H=1 (hs 64) L=1 T=4096 M=4 cross=[T,F,F,F] B=1
   stored: losses, logits of the last 8 positions, per-tensor gradient L2 norms, sampled gradient
   entries (every tensor's first and last element + 2048 uniform draws over the concatenation), and
   the losses after one AdamW step (lr 1e-3) on the same batch.
@@ -149,6 +151,12 @@ SCALE = {
                  cross=[True, False, False, False], B=2, param_seed=31),
     "f_m8": dict(n_embd=128, n_head=2, n_layer=2, block_size=128, V=[900, 13, 144, 5, 900, 13, 144, 5],
                  cross=[True, True, False, False, True, True, False, False], B=2, param_seed=37),
+    # long-sequence shapes: C3's sequence length and cross grouping, and C4's T = 4096
+    # attention walk at head size 64 (32 chunks of 128 rows)
+    "f_t1024": dict(n_embd=128, n_head=2, n_layer=1, block_size=1024, V=[900, 13, 144, 5, 900, 13, 144, 5],
+                    cross=[True, True, False, False, True, True, False, False], B=1, param_seed=41),
+    "f_t4096": dict(n_embd=64, n_head=1, n_layer=1, block_size=4096, V=[900, 13, 144, 5],
+                    cross=[True, False, False, False], B=1, param_seed=43),
 }
 
 

@@ -28,7 +28,7 @@ def model_fixture(name):
 MODEL_FIXTURES = ["f_demo", "f_small", "f_hs32", "f_m1", "f_tiny_v"]
 # BASELINE-config-sized fixtures: parameters are NOT stored (tens of MB); both the generator and
 # the tests rebuild them with recipe_state_dict from the key list + seed kept in the fixture
-SCALE_FIXTURES = ["f_c1", "f_m8"]
+SCALE_FIXTURES = ["f_c1", "f_m8", "f_t1024", "f_t4096"]
 
 
 def recipe_state_dict(keys_shapes, seed):

@@ -101,3 +101,46 @@ def test_gradsync_gloo_world2_averages_every_bucket():
         assert p.exitcode == 0
     for rank, ok, tail_ok, nb in res:
         assert ok and tail_ok, (rank, ok, tail_ok)
+
+
+def _seed_worker(rank, world, port, q):
+    """enable_data_parallel on a CPU-resident model (gloo): replicas broadcast from rank 0, and each
+    rank's dropout seed differs although every rank seeds torch identically."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import config_utils
+        from model import MultimodalTransformer
+        config_utils._config_cache = {"n_embd": 32, "n_head": 4, "n_layer": 1, "block_size": 8, "dropout": 0.1,
+                                      "device": "cpu", "batch_size": 2, "eval_iters": 1}
+        torch.manual_seed(1000 + rank)  # different init: the broadcast must make the replicas equal
+        m = MultimodalTransformer(2, [11, 5], [[None] * 8 + [c] + [None] * 3 for c in (True, False)])
+        mmt_dist.enable_data_parallel(m, bucket_bytes=1 << 10)
+        p0 = m.flat_params.detach().clone()
+        dist.broadcast(p0, src=0)
+        torch.manual_seed(7)
+        seeds = [m._next_dropout_seed(torch.device("cpu")) for _ in range(3)]
+        allseeds = [None] * world
+        dist.all_gather_object(allseeds, seeds)
+        q.put((rank, bool(torch.equal(p0, m.flat_params.detach())), allseeds))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_data_parallel_per_rank_dropout_seeds_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, same, allseeds in res:
+        assert same, rank
+        s0, s1 = allseeds
+        assert len(set(s0)) == 3 and not set(s0) & set(s1), allseeds

@@ -293,6 +293,60 @@ def test_kv_cache_decode_matches_full_forward(name):
         m._decode_step([s[:, 0] for s in seq], T)  # position outside the block
 
 
+@pytest.mark.parametrize("hs", [8, 16, 24, 32, 48, 64])
+def test_kv_cache_decode_every_head_size(hs):
+    """The decode attention kernel (attn_decode_kernel<HS>) and the single-row GEMMs at every
+    supported head size, incl. hs 64 (target shape, C4) and 24 / 48: decode logits of
+    positions P..T-1 after a prefill vs the full forward of the whole sequence (itself parity-checked
+    against the reference) and vs the CPU oracle; 3 modalities, cross-attention on modality 0."""
+    import mmt_oracle as O
+    H, L, T, B = 2, 2, 40, 3
+    C = H * hs
+    V = [37, 5, 11]
+    cross = [True, False, False]
+    cfg = O.OracleConfig(C, H, L, T, V, cross)
+    g = torch.Generator().manual_seed(hs)
+    sd = O.init_params(cfg, g)
+    for k in sd:  # non-trivial LayerNorm / bias values so every path carries signal
+        if k.endswith("bias") or "ln" in k or "norm" in k:
+            sd[k] = sd[k] + 0.05 * torch.randn(sd[k].shape, generator=g)
+    tril = [f"blocks.{l}.{kind}.{i}.heads.{h}.tril" for l in range(L) for i in range(len(V))
+            for kind in ("sa_layers", "cross_attention_layers") for h in range(H)
+            if kind == "sa_layers" or cross[i]]
+    meta = {"n_embd": C, "n_head": H, "n_layer": L, "block_size": T, "B": B, "V": V, "cross": cross,
+            "state_dict_keys": list(sd.keys()) + tril}
+    m = build(meta, sd)
+    m.eval()
+    idx = [torch.randint(0, v, (B, T), generator=g) for v in V]
+    P = 7
+    seq = [t.cuda() for t in idx]
+    with torch.no_grad():
+        m([s[:, :P] for s in seq])
+        dec = [m._decode_step([s[:, t] for s in seq], t) for t in range(P, T)]
+        full, _ = m(seq)
+    ref, _ = O.forward(sd, cfg, idx)
+    for i in range(len(V)):
+        got = torch.stack([d[i] for d in dec], dim=1).cpu()
+        assert rel(got, full[i][:, P:T]) < 1e-2, (hs, i, rel(got, full[i][:, P:T]))
+        assert rel(got, ref[i][:, P:T]) < 2e-2, (hs, i, rel(got, ref[i][:, P:T]))
+
+
+def test_decode_refuses_dropout_prefill():
+    """mmt_decode_step promises eval semantics (include/mmt.h): a cache left by a training forward
+    that sampled dropout is refused with MMT_ERR_STATE."""
+    z, meta, cfg, sd, idx, tgt = model_fixture("f_small")
+    m = build(meta, sd, dropout=0.1)
+    m.train()
+    seq = [t.cuda() for t in idx]
+    with torch.no_grad():
+        m(seq, [t.cuda() for t in tgt])
+        with pytest.raises(Exception, match="dropout"):
+            m._decode_step([s[:, 1] for s in seq], 1)
+        m.eval()
+        m([s[:, :4] for s in seq])  # an eval prefill re-arms the cache
+        m._decode_step([s[:, 4] for s in seq], 4)
+
+
 def test_generate_kv_cache_greedy_matches_reforward():
     """generate with the KV cache against the reference's re-forward per token (use_cache=False),
     greedy sampling on a model with peaked output heads (so argmax is stable to bf16 noise), past

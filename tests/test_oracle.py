@@ -155,7 +155,7 @@ def _scale_compare(z, meta, logits, losses, grads, rel_tol, grad_tol, sample_tol
     assert ((last - rl).norm() / rl.norm()).item() < sample_tol
 
 
-@pytest.mark.parametrize("name", ["f_c1", "f_m8"])
+@pytest.mark.parametrize("name", ["f_c1", "f_m8", "f_t1024", "f_t4096"])
 def test_scale_fixture_oracle_matches_reference(name):
     """The oracle at the BASELINE config sizes (C1 dims, 6 layers; 8 modalities with 4 x 7 KV
     streams) against the reference's own outputs (fp32 restatement tolerances), and one AdamW
@@ -172,3 +172,21 @@ def test_scale_fixture_oracle_matches_reference(name):
     _, l1 = O.forward(params, cfg, idx, tgt)
     torch.testing.assert_close(torch.stack(l1), torch.from_numpy(z["losses_after1"]), rtol=1e-5, atol=1e-5)
     torch.set_num_threads(1)
+
+
+def test_bf16_floor_at_c1_dims():
+    """The bf16 floor the GPU gradient tolerance is tied to (tests/test_gpu_scale.py): the oracle
+    with every matrix product's operands rounded to bf16 sits ~5.2 % (whole-gradient rel-L2) from
+    the fp32 oracle at C1's six layers, i.e. above SURVEY.md §8c's proposed 5e-2, and that floor is
+    made by the forward's rounding, not the backward's (tools/parity_attrib.py --sites)."""
+    from golden_io import scale_fixture
+    torch.set_num_threads(8)
+    z, meta, cfg, sd, idx, tgt = scale_fixture("f_c1")
+    names = meta["grad_names"]
+    _, _, rg = O.forward_backward(sd, cfg, idx, tgt)
+    _, _, eg = O.forward_backward(sd, cfg, idx, tgt, emulate_bf16=True)
+    ref = torch.cat([rg[k].flatten() for k in names])
+    emu = torch.cat([eg[k].flatten() for k in names])
+    floor = ((emu - ref).norm() / ref.norm()).item()
+    torch.set_num_threads(1)
+    assert 0.045 < floor < 0.06, floor

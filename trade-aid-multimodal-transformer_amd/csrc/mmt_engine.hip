@@ -366,6 +366,13 @@ void build_layout(mmt_ctx* c) {
 // -------------------------------------------------------------------------------------------
 // workspace plan for batch B
 // -------------------------------------------------------------------------------------------
+// the non-finite-loss flag words sit right after the packed weights, at the same offset for every
+// batch size, so querying them never replaces the plan of a pending backward / decode
+size_t flag_offset(const mmt_ctx* c) { return (size_t)rup(c->pack_elems * 2, 256); }
+
+// -------------------------------------------------------------------------------------------
+// workspace plan for batch B (continued)
+// -------------------------------------------------------------------------------------------
 void make_plan(mmt_ctx* c, int B) {
   Plan& p = c->plan;
   p = Plan();
@@ -379,7 +386,7 @@ void make_plan(mmt_ctx* c, int B) {
   const size_t bhT = (size_t)B * H * c->T;
   const size_t mbytes = c->cfg.dropout > 0.f ? (size_t)mmt_attn_mask_dwords(B, H, c->T) * 4 : 0;
   p.pack = A((size_t)c->pack_elems * b2);
-  p.flag = A(256);
+  p.flag = A(256);  // == flag_offset(c): fixed for every batch size (mmt_loss_flag_offset)
   p.pack8 = c->fp8 ? A((size_t)c->pack8_bytes) : 0;
   p.act.resize((size_t)c->L * M);
   for (int i = 0; i < M; ++i) p.xemb[i] = A(R * C * f4);
@@ -1549,8 +1556,7 @@ int mmt_tensor_info(const mmt_ctx* c, int32_t i, char* name, int32_t cap, int64_
 
 int64_t mmt_loss_flag_offset(mmt_ctx* c, int32_t batch) {
   if (!c || batch < 1) return -1;
-  if (c->plan.B != batch) make_plan(c, batch);
-  return (int64_t)c->plan.flag;
+  return (int64_t)flag_offset(c);  // batch-independent: the current plan is left alone
 }
 
 int64_t mmt_workspace_bytes(mmt_ctx* c, int32_t batch) {
@@ -1597,6 +1603,12 @@ int mmt_decode_step(mmt_ctx* c, void* stream, int32_t batch, int32_t pos, const 
   if (!idx || !params || !logits || !workspace) return fail(c, MMT_ERR_INVALID, "mmt_decode_step: null argument");
   if (c->plan.B != batch || !c->cache_ready)
     return fail(c, MMT_ERR_STATE, "mmt_decode_step: run mmt_forward (prefill) on this batch and workspace first");
+  if (c->fwd_drop)
+    return fail(c, MMT_ERR_STATE, "mmt_decode_step: the prefill forward sampled dropout (training mode); decode "
+                                  "has eval semantics: run the prefill with training = 0");
+  if (c->fp8)
+    return fail(c, MMT_ERR_STATE, "mmt_decode_step: precision fp8 prefills with MX-fp8 GEMMs the bf16 decode "
+                                  "would not reproduce: re-run mmt_forward per token");
   if (pos < 1 || pos >= c->T) return fail(c, MMT_ERR_INVALID, "mmt_decode_step: position outside 1..block_size-1");
   Runner r{c, (hipStream_t)stream, workspace, params, nullptr, batch, batch};
   return run_decode(c, r, pos, idx, logits);

@@ -95,4 +95,7 @@ def enable_data_parallel(model, group=None, bucket_bytes=32 << 20, broadcast=Tru
             dist.broadcast(model.flat_unused.data, src=src, group=group)
     sync = GradSync(model.backward_stage_ranges(), group=group, bucket_bytes=bucket_bytes)
     model._grad_sync = sync
+    # per-rank dropout stream: every rank seeds torch identically, so without this
+    # all ranks would draw the same masks on the same (row, column) sites of their local batches
+    model._dp_rank = dist.get_rank()
     return sync

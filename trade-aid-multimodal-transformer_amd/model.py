@@ -113,6 +113,8 @@ class MultimodalTransformer(nn.Module):
         # never-used CrossAttention parameters (M == 1): their own Parameter, .grad stays None
         self.flat_unused = nn.Parameter(flat[na:].clone()) if n > na else None
         self._dropout_counter = 0
+        self._dp_rank = 0  # data-parallel rank (mmt_dist.enable_data_parallel): folded into the dropout seed
+        self._sticky_carry = 0  # sticky non-finite bits of workspaces replaced since the last clear
         self._ws = None
         self._ws_batch = -1
         self._ws_bytes = {}
@@ -224,10 +226,12 @@ class MultimodalTransformer(nn.Module):
             if self._ws_bytes[B] < 0:
                 raise ML.MmtError("mmt_workspace_bytes failed")
         if self._ws is None or self._ws_batch != B or self._ws.device != device:
+            off = ML.lib().mmt_loss_flag_offset(self._ctx, B)  # the same offset for every batch size
+            if self._ws is not None:  # keep the sticky bits of the workspace being replaced
+                self._sticky_carry |= int(self._ws[off + 4:off + 8].view(torch.int32).item())
             self._ws = None
             self._ws = torch.empty(self._ws_bytes[B], dtype=torch.uint8, device=device)
             self._ws_batch = B
-            off = ML.lib().mmt_loss_flag_offset(self._ctx, B)
             self._ws[off:off + 8].zero_()  # non-finite-loss flags (last forward, sticky)
         return self._ws
 
@@ -254,9 +258,13 @@ class MultimodalTransformer(nn.Module):
     def _next_dropout_seed(self, dev):
         """Seed of this training step's dropout masks. The reference's nn.Dropout on a ROCm device
         draws from the device generator, never from torch's CPU generator (which get_batch's
-        torch.randint start indices consume): the seed is derived from the device generator's
-        seed and Philox offset, and the offset is advanced as a dropout launch would, so
-        torch.manual_seed makes runs repeatable and the CPU random stream stays the reference's."""
+        torch.randint start indices consume), so the seed is derived from the device generator's
+        seed and Philox offset and the CPU random stream stays the reference's. The offset is
+        bumped by a fixed 4 per forward only to keep the seed sequence repeatable under
+        torch.manual_seed; this does NOT reproduce the reference's Philox consumption (its dropout
+        calls advance the offset by tensor size), so later device-RNG users (e.g.
+        torch.multinomial in generate) see a different stream than the reference's. Under data
+        parallelism the rank is folded in: each rank draws its own masks."""
         self._dropout_counter += 1
         seed, off = 0, self._dropout_counter
         try:
@@ -266,7 +274,8 @@ class MultimodalTransformer(nn.Module):
             gen.set_offset(off + 4)
         except (AttributeError, RuntimeError, IndexError):
             pass
-        x = (seed * 0x9E3779B97F4A7C15 + off * 0xBF58476D1CE4E5B9 + self._dropout_counter) & (2 ** 64 - 1)
+        x = (seed * 0x9E3779B97F4A7C15 + off * 0xBF58476D1CE4E5B9 + self._dropout_counter
+             + self._dp_rank * 0xD1B54A32D192ED03) & (2 ** 64 - 1)
         x ^= x >> 31
         x = (x * 0x94D049BB133111EB) & (2 ** 64 - 1)
         return int(x ^ (x >> 29)) & (2 ** 62 - 1)
@@ -280,8 +289,12 @@ class MultimodalTransformer(nn.Module):
         off = ML.lib().mmt_loss_flag_offset(self._ctx, self._ws_batch) + (4 if sticky else 0)
         w = self._ws[off:off + 4]
         out = w.view(torch.int32).clone()
+        if sticky and self._sticky_carry:
+            out |= self._sticky_carry
         if clear:
             w.zero_()
+            if sticky:
+                self._sticky_carry = 0
         return out
 
     def backward_stage_ranges(self):
