@@ -33,6 +33,11 @@ Loop fixture (get_batch / estimate_loss as main.py drives them, reference traini
            get_batch('train', 1), estimate_loss (eval_iters 2), one more get_batch('train', 1);
            every batch, the estimate_loss result and its printed lines, the walked train sets.
 
+Run fixture (the reference's own main.py, end to end):
+  f_c0run  the demo config (C0) with dropout 0.0 and save_model 1, seeded, run as a script: every
+           get_batch call, the RNG states and parameters before the first one, every training
+           step's losses, stdout, the log file and the final checkpoint.
+
 Usage:  python tests/golden/gen_golden.py [fixture names...]   (default: all)
 """
 import json
@@ -307,6 +312,104 @@ def gen_loop_fixture(config_utils, seed=11):
     print("loop est", est, "\n" + "\n".join(printed))
 
 
+def gen_run_fixture(seed=2025):
+    """End-to-end C0 replay fixture: the reference's own main.py on its
+    demo config (examples/demo_config.yaml + demo_input_schemas.yaml; dropout 0.0 and save_model 1
+    so the run is deterministic and leaves a final checkpoint), seeded (Python random, numpy, torch)
+    and run as a script from the scratch copy. Recorded: every get_batch call (split, is_training,
+    xb, yb), the Python-random and torch CPU RNG states at the first call (after model creation),
+    the model's state_dict at that moment (the initial parameters), the loss of every training
+    step, the stdout lines, the log-file text, and the final saved state_dict."""
+    import contextlib
+    import io
+    import runpy
+    import torch
+    import yaml
+    cfg = yaml.safe_load(open(os.path.join(SCRATCH, "examples", "demo_config.yaml")))
+    cfg["model_architecture"]["dropout"] = 0.0
+    cfg["project_settings"]["save_model"] = 1
+    with open(os.path.join(SCRATCH, "config.yaml"), "w") as f:
+        yaml.safe_dump(cfg, f)
+    shutil.copy(os.path.join(SCRATCH, "examples", "demo_input_schemas.yaml"), os.path.join(SCRATCH, "input_schemas.yaml"))
+    out_dir = os.path.join(SCRATCH, "examples", "output")
+    if os.path.exists(out_dir):
+        shutil.rmtree(out_dir)
+    import training_utils as tu
+    import model as ref_model
+    for mod in ("config_utils", "training_utils", "model"):
+        sys.modules.pop(mod, None)  # fresh imports under the script's own config discovery
+    import config_utils as cu2
+    cu2._config_cache = None
+    import training_utils as tu
+    import model as ref_model
+    calls, steps, first = [], [], {}
+    orig_get = tu.get_batch
+
+    def rec_get_batch(split, is_training):
+        if not first:
+            first["py"] = random.getstate()
+            first["torch"] = torch.get_rng_state().clone()
+            first["sd"] = {k: v.detach().clone() for k, v in tu.m.state_dict().items() if not k.endswith("tril")}
+            first["train"] = [list(map(int, t)) for t in tu.all_train_sets]
+        xb, yb = orig_get(split, is_training)
+        calls.append((split, int(is_training), [x.clone() for x in xb], [y.clone() for y in yb]))
+        return xb, yb
+    tu.get_batch = rec_get_batch
+    orig_fwd = ref_model.MultimodalTransformer.forward
+
+    def rec_forward(self, idx_list, targets_list=None):
+        lg, ls = orig_fwd(self, idx_list, targets_list)
+        if self.training and ls is not None:
+            steps.append([float(l.item()) for l in ls])
+        return lg, ls
+    ref_model.MultimodalTransformer.forward = rec_forward
+    cwd = os.getcwd()
+    os.chdir(SCRATCH)
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    torch.set_num_threads(1)
+    buf = io.StringIO()
+    try:
+        with contextlib.redirect_stdout(buf):
+            runpy.run_path(os.path.join(SCRATCH, "main.py"), run_name="__main__")
+    finally:
+        os.chdir(cwd)
+        ref_model.MultimodalTransformer.forward = orig_fwd
+        tu.get_batch = orig_get
+    stdout = buf.getvalue()
+    log_text = open(os.path.join(out_dir, cfg["project_settings"]["output_file_name"])).read()
+    final_sd = torch.load(os.path.join(SCRATCH, cfg["project_settings"]["model_file_name"]), weights_only=True)
+    out = {}
+    for c, (split, tr, xb, yb) in enumerate(calls):
+        for i in range(len(xb)):
+            out[f"x{c}.{i}"] = xb[i].numpy()
+            out[f"y{c}.{i}"] = yb[i].numpy()
+    out["steps"] = np.array(steps, dtype=np.float64)
+    out["torch_state"] = first["torch"].numpy()
+    py = first["py"]
+    out["py_state"] = np.array(py[1], dtype=np.uint64)
+    for k, v in first["sd"].items():
+        out[f"init.{k}"] = v.numpy()
+    for k, v in final_sd.items():
+        if not k.endswith("tril"):
+            out[f"final.{k}"] = v.numpy()
+    for i, t in enumerate(first["train"]):
+        out[f"train0.{i}"] = np.array(t, dtype=np.int64)
+    for i, v in enumerate(tu.all_val_sets):
+        out[f"val.{i}"] = v.numpy()
+    meta = {"seed": seed, "config": cfg, "calls": [(sp, tr) for sp, tr, _, _ in calls],
+            "py_state_version": py[0], "py_state_gauss": py[2],
+            "vocabs": [list(v) for v in tu.all_vocabularies], "params": tu.all_modality_params,
+            "file_lengths": list(tu.file_lengths) if tu.file_lengths is not None else None,
+            "is_percents": bool(tu.is_percents), "V": [len(v) for v in tu.all_vocabularies],
+            "state_dict_keys": list(final_sd.keys()), "stdout": stdout.splitlines(), "log": log_text}
+    out["meta_json"] = np.frombuffer(json.dumps(meta, default=str).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "f_c0run.npz"), **out)
+    print("c0 run:", len(calls), "get_batch calls,", len(steps), "training steps; first losses", steps[:2],
+          "last", steps[-1])
+
+
 def gen_metric_fixture(seed=77):
     """calculate_evaluation_metrics (reference training_utils.py:215-330)."""
     import torch
@@ -407,6 +510,8 @@ if __name__ == "__main__":
             gen_scale_fixture(cu, name, cfg)
     if on("f_loop"):
         gen_loop_fixture(cu)
+    if on("f_c0run"):
+        gen_run_fixture()
     if on("eval_metrics"):
         gen_metric_fixture()
     if on("batch_indices"):

@@ -61,3 +61,32 @@ def scale_fixture(name):
     idx = [torch.from_numpy(z[f"idx.{i}"].copy()) for i in range(cfg.M)]
     tgt = [torch.from_numpy(z[f"tgt.{i}"].copy()) for i in range(cfg.M)]
     return z, meta, cfg, sd, idx, tgt
+
+
+def c0_run_oracle_replay(emulate_bf16=False):
+    """Replay the reference's recorded C0 demo run (f_c0run: the training batches it drew, its
+    initial parameters) through the oracle: forward + backward + oracle AdamW per training step.
+    Returns (per-step losses [steps, M], update rel-L2, params rel-L2) against the reference's
+    recorded losses and final checkpoint."""
+    import mmt_oracle as O
+    z, meta = load("f_c0run")
+    ma, tp = meta["config"]["model_architecture"], meta["config"]["training_parameters"]
+    V = meta["V"]
+    M = len(V)
+    cfg = O.OracleConfig(ma["n_embd"], ma["n_head"], ma["n_layer"], tp["block_size"], V, [p[8] for p in meta["params"]])
+    init = {k[len("init."):]: torch.from_numpy(z[k].copy()) for k in z.files if k.startswith("init.")}
+    fin = {k[len("final."):]: torch.from_numpy(z[k].copy()) for k in z.files if k.startswith("final.")}
+    p = {k: v.clone() for k, v in init.items()}
+    state, losses = {}, []
+    for s, c in enumerate([c for c, (_, tr) in enumerate(meta["calls"]) if tr == 1]):
+        xb = [torch.from_numpy(z[f"x{c}.{i}"]) for i in range(M)]
+        yb = [torch.from_numpy(z[f"y{c}.{i}"]) for i in range(M)]
+        _, ls, g = O.forward_backward(p, cfg, xb, yb, emulate_bf16=emulate_bf16)
+        losses.append([float(l) for l in ls])
+        O.adamw_step(p, g, state, s + 1, lr=tp["learning_rate"])
+    ks = sorted(fin)
+    got = torch.cat([p[k].flatten() for k in ks])
+    ref = torch.cat([fin[k].flatten() for k in ks])
+    i0 = torch.cat([init[k].flatten() for k in ks])
+    upd = (((got - i0) - (ref - i0)).norm() / (ref - i0).norm()).item()
+    return np.array(losses), upd, ((got - ref).norm() / ref.norm()).item()

@@ -190,3 +190,14 @@ def test_bf16_floor_at_c1_dims():
     floor = ((emu - ref).norm() / ref.norm()).item()
     torch.set_num_threads(1)
     assert 0.045 < floor < 0.06, floor
+
+
+def test_oracle_replays_reference_c0_run():
+    """The oracle (forward, backward, AdamW) replays the reference's whole recorded C0 demo run
+    (50 steps of main.py, tests/golden/f_c0run.npz) to fp32 rounding: every step's losses and the
+    final checkpoint."""
+    from golden_io import c0_run_oracle_replay, load
+    z, _ = load("f_c0run")
+    losses, upd, prm = c0_run_oracle_replay()
+    assert np.abs(losses - z["steps"]).max() <= 1e-5 * np.abs(z["steps"]).max()
+    assert upd < 1e-5 and prm < 1e-6, (upd, prm)
