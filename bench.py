@@ -17,7 +17,7 @@ given without it, this process starts that launcher itself (launch_plan) before 
 
 Roofline: the engine times every launch matching the probe patterns (default: all weight-gradient
 GEMMs, attention forward / backward, ffn0, the ffn2 data gradient) with HIP events on the stream it
-runs on, one step in four, and reports each family's algorithmic flops / bytes per launch over
+runs on, one step in eight, and reports each family's algorithmic flops / bytes per launch over
 that time; `roofline` is the family with the largest measured time per step, `kernels` all of them.
 """
 import argparse
@@ -186,8 +186,8 @@ def main():
                     help="compute precision (default: fp8 for c4 as BASELINE configs[4] names it, else bf16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--exact-steps", type=int, default=5,
-                    help="steps timed with the bit-exact host get_batch (reference RNG streams) after the main run")
+    ap.add_argument("--exact-steps", type=int, default=20,
+                    help="steps timed with the bit-exact device get_batch (reference RNG streams) after the main run")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -290,25 +290,38 @@ def main():
 
     exact = None
     if args.exact_steps > 0 and world == 1:
-        # the same loop fed by the bit-exact host get_batch (reference RNG streams, pinned-buffer copies)
+        # the same loop fed by get_batch bit-exact with the reference (its Python `random` and torch
+        # RNG streams): the device-exact batcher (MT19937 on the GPU, prefix-sum walk) over
+        # args.exact_steps steps after 2 untimed ones, and the exact host batcher over 3 steps
         import random
         mmt_data.install(TU, data, model)
         config_utils._config_cache.update({"device": str(dev)})
-        TU.use_device_batcher = False
-        random.seed(0)
-        torch.cuda.synchronize()
-        te = time.perf_counter()
-        for _ in range(args.exact_steps):
-            xb, yb = TU.get_batch("train", 1)
-            _, ls = model(xb, yb)
-            opt.zero_grad(set_to_none=True)
-            sum(ls).backward()
-            opt.step()
-        torch.cuda.synchronize()
-        te = time.perf_counter() - te
+
+        def exact_run(mode, n, warm):
+            TU.use_device_batcher = mode == "device"
+            TU.batcher_mode = "exact"
+            TU._device_batcher[0] = None
+            random.seed(0)
+            for k in range(warm + n):
+                if k == warm:
+                    torch.cuda.synchronize()
+                    t_ = time.perf_counter()
+                xb, yb = TU.get_batch("train", 1)
+                _, ls = model(xb, yb)
+                opt.zero_grad(set_to_none=True)
+                sum(ls).backward()
+                opt.step()
+            torch.cuda.synchronize()
+            t_ = time.perf_counter() - t_
+            TU.sync_host_state()
+            return {"tokens_per_s": round(B * T * M * n / t_, 1), "ms_per_step": round(t_ / n * 1e3, 2), "steps": n}
+        exact = exact_run("device", args.exact_steps, 2)
+        exact["mode"] = "device-exact get_batch (Python's MT19937 on the GPU, prefix-sum walk; bit-exact batches)"
+        exact["host_exact"] = exact_run("host", 3, 0)
+        exact["vs_headline"] = round(exact["tokens_per_s"] / value, 4)
         TU.use_device_batcher = True
-        exact = {"tokens_per_s": round(B * T * M * args.exact_steps / te, 1), "ms_per_step": round(te / args.exact_steps * 1e3, 2),
-                 "steps": args.exact_steps}
+        TU.batcher_mode = "hash"
+        TU._device_batcher[0] = None
 
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,

@@ -165,6 +165,25 @@ int mmt_batch_indices(void* stream, int32_t batch, const int64_t* cum_valid, con
 int mmt_batch_gather(void* stream, int32_t nmod, const int32_t* const* data, const int64_t* ix, int32_t batch,
                      int32_t T, int64_t* const* x, int64_t* const* y);
 
+/* ---- bit-exact device walk: get_batch's jitter (data_utils.py:342-351 through
+ * training_utils.py:350-360) with the reference's own Python `random` stream (MT19937) ----
+ * mt_state: device uint32[625] = CPython random.getstate()[1] (624 key words + index).
+ * words: device buffer of mmt_exact_words_bytes(nwords) bytes; mmt_exact_gen fills it with the
+ * generator's stream from mt_state (one workgroup; nwords >= the draws of one walk). mmt_exact_walk
+ * walks data[r] (int32, n[r] elements) for every r with rand_size[r] != 0 (0 = None) in order,
+ * each eligible element (r < x < V - r) taking the next accepted draw of random.choice, then moves
+ * mt_state past the last word drawn. *status is set to 1 if the words ran out (never, at the
+ * sizes mmt_exact_words_bytes is asked for by the Python batcher). scratch: see
+ * mmt_exact_walk_scratch_bytes(max n[r], nwords). All asynchronous on `stream`. */
+int64_t mmt_exact_words_bytes(int64_t nwords);
+int64_t mmt_exact_walk_scratch_bytes(int64_t max_n, int64_t nwords);
+int mmt_exact_gen(void* stream, const uint32_t* mt_state, uint32_t* words, int64_t nwords);
+int mmt_exact_walk(void* stream, int32_t nmod, int32_t* const* data, const int64_t* n, const int32_t* rand_size,
+                   const int32_t* vocab, uint32_t* mt_state, const uint32_t* words, int64_t nwords, void* scratch,
+                   int64_t scratch_bytes, int32_t* status);
+/* tuning knob: bit 0 / bit 1 = the slice-streamed hs-64 attention dK/dV / dQ pass, bit 2 = dK/dV at 3 waves per SIMD (default 1); returns the old value */
+int mmt_attn_set_ring(int v);
+
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
 /* GEMM pipeline variant (tuning knob, process-wide; 128x128 tile): bits 0-3 forward / backward-data,
  * bits 4-7 weight gradients: 0 = K-step 64 x 2 LDS stages, 1 = 32 x 2, 2 = 32 x 3, 3 = 32 x 4,

@@ -25,7 +25,7 @@ import training_utils as TU
 from golden_io import load, model_fixture
 
 
-def _setup(device, dropout=0.0):
+def _setup(device, dropout=0.0, mode="host"):
     z, meta = load("f_loop")
     M = len(meta["V"])
     zs, ms = load("f_small")
@@ -41,7 +41,9 @@ def _setup(device, dropout=0.0):
     TU.file_lengths = meta["file_lengths"]
     TU.num_modalities = M
     TU.is_percents = True
-    TU.use_device_batcher = False
+    TU.use_device_batcher = mode != "host"
+    TU.batcher_mode = "exact" if mode == "exact" else "hash"
+    TU._device_batcher[0] = None
     random.seed(meta["seed"])
     torch.manual_seed(meta["seed"])
     return z, meta, M
@@ -66,6 +68,7 @@ def test_host_get_batch_bit_exact_over_steps():
             np.testing.assert_array_equal(np.asarray(TU.all_train_sets[i]), z[f"train_end.{i}"])
     finally:
         TU.use_device_batcher = True
+        TU.batcher_mode = "hash"
 
 
 def _counts(lines):
@@ -78,9 +81,12 @@ def _counts(lines):
 
 
 @pytest.mark.gpu
-def test_gpu_loop_get_batch_and_estimate_loss_match_reference():
+@pytest.mark.parametrize("mode", ["host", "exact"])
+def test_gpu_loop_get_batch_and_estimate_loss_match_reference(mode):
+    """mode "host": the exact host batcher; "exact": the device-exact batcher (MT19937 on the GPU,
+    the walk as prefix-sum kernels): the same bit-exact batches, walked lists and Python state."""
     import model as mmt_model
-    z, meta, M = _setup("cuda", dropout=0.1)
+    z, meta, M = _setup("cuda", dropout=0.1, mode=mode)
     zs, ms, cfg, sd, _, _ = model_fixture("f_small")
     try:
         m = mmt_model.MultimodalTransformer(M, meta["V"], meta["params"]).to("cuda")
@@ -106,8 +112,11 @@ def test_gpu_loop_get_batch_and_estimate_loss_match_reference():
         for (a, n), (b, n_ref) in zip(got, ref):
             assert n == n_ref and abs(a - b) <= 1, (got, ref)
         _check(z, M, 2, *TU.get_batch("train", 1))
+        TU.sync_host_state()
         for i in range(M):
             np.testing.assert_array_equal(np.asarray(TU.all_train_sets[i]), z[f"train_end.{i}"])
     finally:
         TU.use_device_batcher = True
+        TU.batcher_mode = "hash"
+        TU._device_batcher[0] = None
         TU.m = None

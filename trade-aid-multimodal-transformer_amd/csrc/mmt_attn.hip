@@ -177,7 +177,6 @@ __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x)
 // this file is compiled with -fno-slp-vectorize so the compiler does not re-pack them.
 
 constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
 constexpr float kTau = 8.0f;  // lazy-rescale threshold of the forward's running max (log2 units)
 
 // waves per SIMD the forward / dQ kernels are compiled for (hs <= 32 fits two at no spill; at hs
@@ -450,7 +449,7 @@ __global__ __launch_bounds__(256, MMT_FWD_MINB(HS)) void attn_fwd_kernel(AttnBat
           ov[dt][pr] = u32x4{s0[0], s1[0], s0[1], s1[1]};  // d = dt*32 + 16 pr + 8 h + 0..7
         }
       if (live && q.tq < T) {
-        if (h == 0) P.lse[j][(int64_t)bh * T + q.tq] = (q.m + __log2f(l)) * kLn2;
+        if (h == 0) P.lse[j][(int64_t)bh * T + q.tq] = q.m + __log2f(l);  // log2 domain
         bf16_t* dst = (P.nstreams > 1 ? P.oj[j] : P.o) + (rowbase + q.tq) * P.o_ld + head * HS;
 #pragma unroll
         for (int dt = 0; dt < G::ND; ++dt)
@@ -675,8 +674,8 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
     }
     A.dsum = dsa;
     Bq.dsum = dsb;
-    A.lse2 = oka ? P.lse[j][(int64_t)bh * T + A.tq] * kLog2e : 0.f;
-    Bq.lse2 = okb ? P.lse[j][(int64_t)bh * T + Bq.tq] * kLog2e : 0.f;
+    A.lse2 = oka ? P.lse[j][(int64_t)bh * T + A.tq] : 0.f;
+    Bq.lse2 = okb ? P.lse[j][(int64_t)bh * T + Bq.tq] : 0.f;
     for (int c = 0; c < nch; ++c) {
       const int kt_lo = c * (ROWS / 32);
       const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
@@ -892,7 +891,7 @@ __global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnB
     for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
       const int t = r0 + (c % ROWS);
-      sl[u] = t < T ? ((c < ROWS) ? -lsep[t] * kLog2e : -dvp[t]) : 0.f;  // negated: fma addends
+      sl[u] = t < T ? ((c < ROWS) ? -lsep[t] : -dvp[t]) : 0.f;  // negated: fma addends
     }
   };
   auto store = [&]() {
@@ -1060,7 +1059,7 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
     for (int u = 0; u < NSL; ++u) {
       const int c = tid + 256 * u;
       const int t = r0 + (c % ROWS);
-      sl[u] = t < T ? ((c < ROWS) ? -lsep[t] * kLog2e : -dvp[t]) : 0.f;  // negated: fma addends
+      sl[u] = t < T ? ((c < ROWS) ? -lsep[t] : -dvp[t]) : 0.f;  // negated: fma addends
     }
   };
   auto store = [&]() {
@@ -1148,6 +1147,19 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
   }
 }
 
+// attention variant knob (bit 0: the slice-streamed hs-64 dK/dV pass, bit 1: its dQ pass, bit 2: the
+// dK/dV pass at 3 waves per SIMD): MMT_ATTN_RING, or
+// mmt_attn_set_ring() for in-process A/B
+static int g_attn_ring = [] {
+  const char* e = getenv("MMT_ATTN_RING");
+  return e ? atoi(e) : 1;
+}();
+extern "C" int mmt_attn_set_ring(int v) {
+  const int old = g_attn_ring;
+  g_attn_ring = v;
+  return old;
+}
+
 template <int HS>
 static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
   const int nb = ((T + 31) / 32 + 7) / 8;
@@ -1161,8 +1173,15 @@ static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, b
     const int ns = bt.p[0].nstreams;
     bool drop = false;
     for (int g = 0; g < bt.count; ++g) drop = drop || bt.p[g].drop_thr != 0;
-    if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, true>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    // hs 64: the slice-streamed kernels (mmt_attn2.hip): bit 1 of the knob the dQ pass, bit 0 the
+    // dK/dV pass; MMT_ATTN_RING=0 (or mmt_attn_set_ring(0)) keeps the chunked ones
+    if (HS == 64 && (g_attn_ring & 2)) (void)mmt_attn_bwd_dq_ring64(bt, B, T, H, scale, drop, s);
+    else if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, true>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, false>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    if (HS == 64 && (g_attn_ring & 1)) {
+      (void)mmt_attn_bwd_dkdv_ring64(bt, B, T, H, scale, drop, (g_attn_ring & 4) != 0, s);
+      return;
+    }
     // dK/dV: the paired walk needs 4 accumulator sets (1 wave per SIMD); the single-tile kernel
     // keeps 2 waves per SIMD and measured faster at hs = 32 (C1: 103 vs 127 us) and, once it fits
     // hs = 64 without AGPRs, there too (target step 25.9 -> 25.4 ms). MMT_DKDV_PAIR=1 forces the pair

@@ -1,0 +1,540 @@
+// Attention backward at head size 64 (target shape, C3, C4): slice-streamed kernels.
+//
+// The chunked kernels of mmt_attn.hip stage 128-row chunks of the shared operand through VGPRs and
+// stop the whole workgroup at every chunk reload (two barriers around a global-load -> LDS-store
+// round trip); at hs 64 and T >= 512 their waves sit 35-63 % of their cycles in those waits
+// (profiles/r2_sq_target.txt). Here the shared operand streams through an LDS ring of 32-row slices
+// filled by LDS-DMA (buffer_load ... lds, no VGPR round trip), S - 1 slices ahead of the compute,
+// with one barrier per slice: each wave waits (counted vmcnt) only for its own pieces of the slice
+// it is about to read, the barrier then publishes every wave's pieces and retires the reads of the
+// previous slice, whose slot takes the next DMA.
+//
+// Slice images: a 32-row x 64-column bf16 tile is stored as four column sub-images (16 columns =
+// 32 B per row, 1 KiB each = one LDS-DMA piece) 1152 B apart; the two 16-B halves of row r are
+// swapped when bit 3 of r is set. The swap is applied on the DMA's per-lane SOURCE address (the LDS
+// side of an LDS-DMA is lane-linear) and again on every read. Both read kinds are bank-conflict
+// free: a row read (ds_read_b128, MFMA operand with the row on the lane) of one 16-lane group covers
+// each (r mod 8) twice, once per half; the 32-lane half of a transposed read (ds_read_b64_tr_b16,
+// the tile as a k-major operand) takes 4 rows x 2 sub-images, and the 128-B pad puts the two
+// sub-images in opposite halves of the 256-B bank row. Every read address is a per-lane base plus
+// an immediate (k step s: 1152 s for row reads, 512 s for transposed reads; column block: 2304),
+// so the slice loop carries almost no address arithmetic.
+#include "mmt_common.h"
+#include "mmt_kernels.h"
+
+namespace {
+
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int32_t)((a >> 32) & 0xffffu));
+  r[2] = __builtin_amdgcn_readfirstlane((int32_t)min(bytes, (int64_t)0x7ffffff0));
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+// 16 B per lane: LDS[lds + 16 lane] = buffer[voff] (zeros when voff is out of range)
+__device__ __forceinline__ void dma16(const i32x4& rsrc, uint32_t lds, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" : : "s"(lds), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+// 4 B per lane: LDS[lds + 4 lane] = buffer[voff]
+__device__ __forceinline__ void dma4(const i32x4& rsrc, uint32_t lds, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" : : "s"(lds), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+// counted wait on this wave's outstanding vector-memory operations (immediate operand)
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+
+constexpr float kLog2e2 = 1.4426950408889634f;
+constexpr int OOB = 0x7fffffff;
+
+constexpr int SUB = 1152;          // column sub-image stride (1 KiB + 128 B pad)
+constexpr int IMG64 = 4 * SUB;      // one 32 x 64 tile
+// byte offset of 16-B half `half` (0/1) of the 16-column block `cb` (0..3) in row `row`
+__device__ __forceinline__ int img_off(int row, int cb, int half) {
+  return cb * SUB + row * 32 + ((half ^ ((row >> 3) & 1)) << 4);
+}
+__device__ __forceinline__ void zero16(f32x16& a) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e) a[e] = 0.f;
+}
+__device__ __forceinline__ float keep_f(float v, int m) { return __int_as_float(__float_as_int(v) & m); }
+__device__ __forceinline__ int key_dword(int r) { return 2 * ((r & 3) + 4 * (r >> 3)) + ((r >> 2) & 1); }
+
+}  // namespace
+
+// =============================================================================================
+// dK, dV at hs 64. grid (nkb * B*H * nstreams, 1, problems), nkb = ceil(nt / 4): a workgroup owns
+// 4 key tiles (wave w: key tile 4 kb + w, its K / V in registers, dK / dV accumulated in
+// registers) and walks the query tiles kb*4 .. nt-1 in lockstep; each query slice (Q, dO, the
+// row's LSE and D, the slice's keep bits) arrives in an LDS ring slot by LDS-DMA. Per query tile a
+// wave whose key tile is not above it computes S = Q K^T and dP = dO V^T (keys on lanes),
+// P = exp2(c2 S - LSE2), dS = P (Z dP - D), dV += (Z P)^T dO, dK += dS^T Q.
+// Workgroups are ordered heaviest key block first (the causal walk of key block kb is nt - 4 kb
+// slices long) so the launch does not end on a tail of long blocks.
+// =============================================================================================
+template <bool DROP, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch, int T, int H, float scale) {
+  constexpr int NKS = 4, ND = 2;  // hs 64: 4 k-steps of 16, 2 output tiles of 32
+  constexpr int S = 4;            // ring slots: S - 1 slices in flight
+  constexpr int OFF_DO = IMG64, OFF_L = 2 * IMG64, OFF_D = OFF_L + 256, OFF_M = OFF_D + 256;
+  constexpr int SLOT = OFF_M + (DROP ? 1024 : 0);
+  constexpr int EPW = 40;  // epilogue transpose slot row stride (bf16)
+  static_assert(S * SLOT >= 4 * 2 * 32 * EPW * 2, "epilogue slots alias the ring");
+  __shared__ __attribute__((aligned(1024))) char lds[S * SLOT];
+  const AttnProblem& P = batch.p[blockIdx.z];
+  const int nt = (T + 31) / 32;
+  const int nkb = (nt + 3) / 4;
+  const int ns = P.nstreams;
+  const int nbhs = gridDim.x / nkb;  // B*H*nstreams
+  const int BH = nbhs / ns;
+  const int kb = blockIdx.x / nbhs;  // heaviest first (no XCD remap: it would give whole XCDs the long blocks)
+  const int yy = blockIdx.x % nbhs;
+  const int j = yy / BH, bh = yy % BH;
+  const int b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int kt0 = kb * 4;
+  const int kt = kt0 + w;
+  const bool live = kt < nt;
+  const int tk = kt * 32 + r;
+  const int nq = nt - kt0;  // query tiles walked by the block
+  const int64_t rowbase = (int64_t)b * T;
+  const float c2 = scale * kLog2e2;
+  const bool ragged = (T & 31) != 0;
+
+  // this wave's K / V rows (keys on lanes): the B operands of S and dP
+  bf16x8 kf[NKS], vf[NKS];
+  {
+    const bf16_t* kp = P.k[j] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
+    const bf16_t* vp = P.v[j] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
+    const bool ok = live && tk < T;
+    u32x4 kr[NKS], vr[NKS];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      kr[s] = ok ? *reinterpret_cast<const u32x4*>(kp + 16 * s + 8 * h) : z;
+      vr[s] = ok ? *reinterpret_cast<const u32x4*>(vp + 16 * s + 8 * h) : z;
+    }
+    // consume them here: the compiler's own wait for these loads then sits before the DMA prologue
+    // instead of at their first use inside the slice loop, where its vmcnt(0) would drain the ring
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      asm volatile("" : "+v"(kr[s]));
+      asm volatile("" : "+v"(vr[s]));
+      kf[s] = __builtin_bit_cast(bf16x8, kr[s]);
+      vf[s] = __builtin_bit_cast(bf16x8, vr[s]);
+    }
+  }
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) { zero16(dk[dt]); zero16(dv[dt]); }
+
+  // DMA sources: Q / dO rows of batch b (rows past T are sent out of range: zeros), the stream's
+  // LSE / D rows, the key-major keep-bit records of (query tile, key tiles kt0..kt0+3) (contiguous)
+  const i32x4 rq = make_rsrc(P.q + head * 64, (rowbase + T) * (int64_t)P.q_ld * 2);
+  const i32x4 rdo = make_rsrc(P.dout + head * 64, (rowbase + T) * (int64_t)P.dout_ld * 2);
+  const i32x4 rl = make_rsrc(P.lse[j] + (int64_t)bh * T, (int64_t)T * 4);
+  const i32x4 rd = make_rsrc(P.dvec[j] + (int64_t)bh * T, (int64_t)T * 4);
+  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+  const i32x4 rm = make_rsrc(DROP ? P.dmask[j] + (int64_t)bh * ntri * 32 : P.dmask[0], ntri * 32 * 4);
+  // pieces this wave issues per slice: 2 sub-images (+ LSE for wave 0, D for wave 1, the keep bits
+  // for wave 2); the counted waits below count them
+  const int per = 2 + (w < 2 ? 1 : 0) + (DROP && w == 2 ? 1 : 0);
+  // per-lane source of a sub-image piece: row L/2, half L&1 (swapped on rows with bit 3 set)
+  const int prow = lane >> 1;
+  const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
+  auto issue = [&](int slot, int qt) {
+    char* sb = lds + slot * SLOT;
+    const int q0 = qt * 32;
+    const int grow = q0 + prow;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int piece = 2 * w + u;  // 0..3: Q column block w (two per wave), 4..7: dO
+      const int op = piece >> 2, cb = piece & 3;
+      const int ld = op ? P.dout_ld : P.q_ld;
+      const int voff = grow < T ? ((int)(rowbase + grow) * ld + cb * 16 + pcol) * 2 : OOB;
+      dma16(op ? rdo : rq, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_DO + cb * SUB)), voff);
+    }
+    if (w < 2) {
+      const int voff = (lane < 32 && q0 + lane < T) ? (q0 + lane) * 4 : OOB;
+      dma4(w == 0 ? rl : rd, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_L + w * 256)), voff);
+    }
+    if (DROP && w == 2) {  // 4 key tiles x 128 B of the key-major records of (qt, kt0..kt0+3)
+      const int voff = lane < 32 ? (int)(((int64_t)qt * (qt + 1) / 2 + kt0) * 128 + lane * 16) : OOB;
+      dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nq) issue(i, kt0 + i);
+
+  // per-lane read offsets (the slot base and the k step / column block are added as immediates):
+  // row reads (lane row r, half h of 16-column block s), transposed reads (tr_frag geometry: rows
+  // 16 s + 4 (g >> 1) + q and + 8, columns 32 dt + 16 (g & 1) + 4 p)
+  const int o_row = img_off(r, 0, h);
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int o_tr0 = img_off(4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
+  const int o_tr1 = img_off(8 + 4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
+  const int o_ld = (8 * 0 + 4 * h) * 4;
+  const int o_mk = ((kt - kt0) * 32 + key_dword(r)) * 4;
+  const float dsc = DROP ? P.drop_scale : 1.f;
+  // one query tile against this wave's key tile; MASKED: the diagonal tile / a ragged last tile
+  auto tile = [&](const char* sb, int qt, auto mc) {
+    constexpr bool MASKED = decltype(mc)::value;
+    const uint32_t mw = DROP ? *reinterpret_cast<const uint32_t*>(sb + OFF_M + o_mk) >> (4 * h) : 0u;
+    f32x16 sacc, dpacc;
+    zero16(sacc);
+    zero16(dpacc);
+    bf16x8 qr[NKS], dr[NKS];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      qr[s] = *reinterpret_cast<const bf16x8*>(sb + o_row + s * SUB);
+      dr[s] = *reinterpret_cast<const bf16x8*>(sb + OFF_DO + o_row + s * SUB);
+    }
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      sacc = mfma32(qr[s], kf[s], sacc);    // S[q][key]
+      dpacc = mfma32(dr[s], vf[s], dpacc);  // dP[q][key]
+    }
+    bf16x8 dot[2][ND], qtr[2][ND];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        dot[s][dt] = join4(lds_tr16(sb + OFF_DO + o_tr0 + 512 * s + 2 * SUB * dt),
+                           lds_tr16(sb + OFF_DO + o_tr1 + 512 * s + 2 * SUB * dt));
+        qtr[s][dt] = join4(lds_tr16(sb + o_tr0 + 512 * s + 2 * SUB * dt), lds_tr16(sb + o_tr1 + 512 * s + 2 * SUB * dt));
+      }
+    uint32_t pp[8], dd[8];  // packed bf16 pairs of Z.P (dV operand) and dS (dK operand)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(sb + OFF_L + o_ld + 32 * gg);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(sb + OFF_D + o_ld + 32 * gg);
+#pragma unroll
+      for (int e4 = 0; e4 < 4; e4 += 2) {
+        float pm[2], ds[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int e = 4 * gg + e4 + u;
+          float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], c2, -l4[e4 + u]));
+          if (MASKED) {
+            const int tq = qt * 32 + 8 * gg + 4 * h + e4 + u;
+            if (!(tk <= tq && tq < T)) pv = 0.f;
+          }
+          float dp = dpacc[e];
+          if (DROP) {
+            const int kbit = __builtin_amdgcn_sbfe((int)mw, 8 * gg + e4 + u, 1);  // all ones iff kept
+            pm[u] = keep_f(pv, kbit);
+            dp = keep_f(dp, kbit);
+          } else {
+            pm[u] = pv;
+          }
+          ds[u] = pv * __builtin_fmaf(dp, dsc, -d4[e4 + u]);  // dS[q][key]
+        }
+        pp[2 * gg + e4 / 2] = pack2bf(pm[0], pm[1]);
+        dd[2 * gg + e4 / 2] = pack2bf(ds[0], ds[1]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, u32x4{pp[4 * s], pp[4 * s + 1], pp[4 * s + 2], pp[4 * s + 3]});
+      const bf16x8 df = __builtin_bit_cast(bf16x8, u32x4{dd[4 * s], dd[4 * s + 1], dd[4 * s + 2], dd[4 * s + 3]});
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        dv[dt] = mfma32(pf, dot[s][dt], dv[dt]);
+        dk[dt] = mfma32(df, qtr[s][dt], dk[dt]);
+      }
+    }
+  };
+
+  // slice i: wait for it, publish it, refill the slot slice i - 1 used, compute. Three straight
+  // loops, one tile variant each (two variants merging inside one loop made the register allocator
+  // copy the dK / dV accumulators every iteration): the block's 4 diagonal slices (masked: each
+  // wave's own diagonal, and nothing above it), the plain slices, a ragged last slice (masked)
+  auto step = [&](int i, auto mc) {
+    wait_vm(per * min(S - 2, nq - 1 - i));  // this wave's pieces of slice i landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's pieces of slice i landed; slice i - 1's reads are done
+    if (i + S - 1 < nq) issue((i + S - 1) % S, kt0 + i + S - 1);
+    const int qt = kt0 + i;
+    if (live && qt >= kt) tile(lds + (i % S) * SLOT, qt, mc);
+  };
+  const int n_diag = min(4, nq);
+  const int n_plain_end = (ragged && nq > 4) ? nq - 1 : nq;
+  int i = 0;
+#pragma unroll 1
+  for (; i < n_diag; ++i) step(i, std::true_type{});
+#pragma unroll 1
+  for (; i < n_plain_end; ++i) step(i, std::false_type{});
+  if (i < nq) step(i, std::true_type{});
+  __syncthreads();  // the ring is free: the epilogue transposes through it
+
+  // dK / dV tiles: accumulator rows = key ((e&3)+8(e>>2)+4h), cols = d (lane); each 32-column slice
+  // is transposed through this wave's LDS slot and leaves as row-major 16-B pieces
+  if (live) {
+    bf16_t* et = reinterpret_cast<bf16_t*>(lds) + w * (2 * 32 * EPW);
+    const int k0 = kt * 32;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        et[kr * EPW + r] = f2bf(dk[dt][e] * scale);
+        et[32 * EPW + kr * EPW + r] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = i * 16 + (lane >> 2), d0 = dt * 32 + (lane & 3) * 8;
+        const u32x4 vk = *reinterpret_cast<const u32x4*>(et + row * EPW + (lane & 3) * 8);
+        const u32x4 vv = *reinterpret_cast<const u32x4*>(et + 32 * EPW + row * EPW + (lane & 3) * 8);
+        if (k0 + row < T) {
+          const int64_t off = (rowbase + k0 + row) * P.dkv_ld + d0;
+          *reinterpret_cast<u32x4*>(P.dk[j] + head * P.dkv_hstride + off) = vk;
+          *reinterpret_cast<u32x4*>(P.dv[j] + head * P.dkv_hstride + off) = vv;
+        }
+      }
+    }
+  }
+}
+
+// =============================================================================================
+// dQ (and D_j = rowsum(dO * O_j)) at hs 64. grid (nqb * B*H, 1, problems), nqb = ceil(nt / 4): a
+// workgroup owns 4 query tiles (wave w: query tile 4 qb + w, its Q / dO in registers, dQ
+// accumulated in registers over every KV stream) and walks (stream j, key tile 0 .. 4 qb + 3) in
+// lockstep; each key slice (K, V, the 4 query tiles' keep-bit lane words) arrives in an LDS ring
+// slot by LDS-DMA. Per key tile a wave whose query tile is not below it computes S^T = K Q^T,
+// dP^T = V dO^T (queries on lanes), dS^T = P^T (Z dP^T - D), dQ^T += K^T dS^T. Heaviest query block
+// first. The per-stream LSE / D of the block's rows live in a small LDS table.
+// =============================================================================================
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64(AttnBatch batch, int T, int H, float scale) {
+  constexpr int NKS = 4, ND = 2;
+  constexpr int S = 4;
+  constexpr int OFF_V = IMG64, OFF_M = 2 * IMG64;
+  constexpr int SLOT = OFF_M + (DROP ? 1024 : 0);
+  constexpr int TAB = S * SLOT;  // [wave][stream][query row] {lse2, D} float2
+  __shared__ __attribute__((aligned(1024))) char lds[TAB + 4 * MMT_MAX_STREAMS * 32 * 8];
+  const AttnProblem& P = batch.p[blockIdx.z];
+  const int nt = (T + 31) / 32;
+  const int nqb = (nt + 3) / 4;
+  const int ns = P.nstreams;
+  const int BH = gridDim.x / nqb;
+  const int qb = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (last) query block first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int qt = 4 * qb + w;
+  const bool live = qt < nt;
+  const int tq = qt * 32 + r;
+  const bool okq = live && tq < T;
+  const int nk = min(4 * qb + 4, nt);  // key tiles walked per stream
+  const int nsl = ns * nk;             // slices
+  const int64_t rowbase = (int64_t)b * T;
+  const float c2 = scale * kLog2e2;
+  const bool ragged = (T & 31) != 0;
+
+  // Q, dO of this wave's query rows (queries on lanes: the B operands of S^T and dP^T); per stream
+  // D_j = rowsum(dO * O_j) (written for the dK/dV pass) and the LSE into the LDS table
+  bf16x8 qf[NKS], dof[NKS];
+  float* tab = reinterpret_cast<float*>(lds + TAB) + w * (MMT_MAX_STREAMS * 64);
+  {
+    u32x4 qr[NKS], dr[NKS];
+    const bf16_t* qp = P.q + (rowbase + tq) * P.q_ld + head * 64;
+    const bf16_t* dp = P.dout + (rowbase + tq) * P.dout_ld + head * 64;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      qr[s] = okq ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * h) : z;
+      dr[s] = okq ? *reinterpret_cast<const u32x4*>(dp + 16 * s + 8 * h) : z;
+    }
+    for (int j = 0; j < ns; ++j) {
+      const bf16_t* oj = (ns > 1 ? P.oj[j] : P.o) + (rowbase + tq) * P.o_ld + head * 64;
+      float d = 0.f;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const u32x4 ov = okq ? *reinterpret_cast<const u32x4*>(oj + 16 * s + 8 * h) : z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          d += bf2f(ov[e] & 0xffff) * bf2f(dr[s][e] & 0xffff);
+          d += bf2f(ov[e] >> 16) * bf2f(dr[s][e] >> 16);
+        }
+      }
+      d += __shfl_xor(d, 32, 64);
+      const float l2 = okq ? P.lse[j][(int64_t)bh * T + tq] : 0.f;
+      if (h == 0) {
+        if (okq) P.dvec[j][(int64_t)bh * T + tq] = d;
+        tab[j * 64 + 2 * r] = l2;
+        tab[j * 64 + 2 * r + 1] = d;
+      }
+    }
+    // consumed here: the compiler's wait for these loads sits before the DMA prologue
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      asm volatile("" : "+v"(qr[s]));
+      asm volatile("" : "+v"(dr[s]));
+      qf[s] = __builtin_bit_cast(bf16x8, qr[s]);
+      dof[s] = __builtin_bit_cast(bf16x8, dr[s]);
+    }
+  }
+  f32x16 dq[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) zero16(dq[dt]);
+
+  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+  const int64_t ntiles = (int64_t)BH * ntri;
+  // per-lane source of a sub-image piece: row L/2, half L&1 (swapped on rows with bit 3 set)
+  const int prow = lane >> 1;
+  const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
+  const int per = 2 + (DROP && w == 0 ? 1 : 0);
+  auto issue = [&](int slot, int sl) {
+    char* sb = lds + slot * SLOT;
+    const int j = sl / nk, kt = sl % nk;
+    const int grow = kt * 32 + prow;
+    const i32x4 rk = make_rsrc(P.k[j] + head * P.kv_hstride, (rowbase + T) * (int64_t)P.kv_ld * 2);
+    const i32x4 rv = make_rsrc(P.v[j] + head * P.kv_hstride, (rowbase + T) * (int64_t)P.kv_ld * 2);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int piece = 2 * w + u;  // 0..3: K column block, 4..7: V
+      const int op = piece >> 2, cb = piece & 3;
+      const int voff = grow < T ? ((int)(rowbase + grow) * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
+      dma16(op ? rv : rk, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_V + cb * SUB)), voff);
+    }
+    if (DROP && w == 0) {  // lane words of (query tile 4 qb + u, key tile kt), u = 0..3: 4 x 128 B
+      const i32x4 rm = make_rsrc(P.dmask[j], ntiles * 2 * 32 * 4);
+      const int u = lane >> 3, q_ = 4 * qb + u;
+      const int64_t t = (int64_t)bh * ntri + (int64_t)q_ * (q_ + 1) / 2 + kt;
+      const int voff = (lane < 32 && q_ < nt && kt <= q_) ? (int)((ntiles + t) * 128 + (lane & 7) * 16) : OOB;
+      dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nsl) issue(i, i);
+
+  const int o_row = img_off(r, 0, h);
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int o_tr0 = img_off(4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
+  const int o_tr1 = img_off(8 + 4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
+  const float dsc = DROP ? P.drop_scale : 1.f;
+  // one key tile against this wave's query tile; MASKED: the diagonal tile / a ragged tile
+  auto tile = [&](const char* sb, int j, int kt, auto mc) {
+    constexpr bool MASKED = decltype(mc)::value;
+    const uint32_t mw = DROP ? reinterpret_cast<const uint16_t*>(sb + OFF_M)[w * 64 + lane] : 0u;
+    const float l2 = tab[j * 64 + 2 * r], dsum = tab[j * 64 + 2 * r + 1];
+    f32x16 sa, pa;
+    zero16(sa);
+    zero16(pa);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sb + o_row + s * SUB);
+      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sb + OFF_V + o_row + s * SUB);
+      sa = mfma32(kf, qf[s], sa);    // S^T[key][q]
+      pa = mfma32(vf, dof[s], pa);   // dP^T[key][q]
+    }
+    bf16x8 ktr[2][ND];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+        ktr[s][dt] = join4(lds_tr16(sb + o_tr0 + 512 * s + 2 * SUB * dt), lds_tr16(sb + o_tr1 + 512 * s + 2 * SUB * dt));
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[e], c2, -l2));
+      if (MASKED) {
+        const int key = kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (key > tq || key >= T) pv = 0.f;
+      }
+      float dp = pa[e];
+      if (DROP) dp = keep_f(dp, __builtin_amdgcn_sbfe((int)mw, (e & 1) * 8 + (e >> 1), 1));
+      sa[e] = pv * __builtin_fmaf(dp, dsc, -dsum);  // dS^T
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const u32x4 v = {pack2bf(sa[8 * s], sa[8 * s + 1]), pack2bf(sa[8 * s + 2], sa[8 * s + 3]),
+                       pack2bf(sa[8 * s + 4], sa[8 * s + 5]), pack2bf(sa[8 * s + 6], sa[8 * s + 7])};
+      const bf16x8 df = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) dq[dt] = mfma32(ktr[s][dt], df, dq[dt]);
+    }
+  };
+  // per stream: the plain key tiles 0 .. 4 qb - 1 (all below every wave's diagonal; the last one
+  // masked when T is ragged and it is the sequence's last tile), then the block's 4 diagonal tiles
+  // masked (each wave its own diagonal; tiles above it skipped)
+  auto step = [&](int i, auto mc) {
+    wait_vm(per * min(S - 2, nsl - 1 - i));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (i + S - 1 < nsl) issue((i + S - 1) % S, i + S - 1);
+    const int j = i / nk, kt = i % nk;
+    if (live && kt <= qt) tile(lds + (i % S) * SLOT, j, kt, mc);
+  };
+  int i = 0;
+  for (int j = 0; j < ns; ++j) {
+    const int nplain = min(4 * qb, nk);
+#pragma unroll 1
+    for (int kt = 0; kt < nplain; ++kt, ++i) step(i, std::false_type{});
+#pragma unroll 1
+    for (int kt = nplain; kt < nk; ++kt, ++i) step(i, std::true_type{});
+  }
+  // 16-B stores of 8 consecutive d per lane after a v_permlane32_swap exchange of the row halves
+  // (the swaps run on every lane: both halves of a row are live or dead together)
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int ga = 2 * pr, gb = 2 * pr + 1;
+      const uint32_t x0 = pack2bf(dq[dt][4 * ga] * scale, dq[dt][4 * ga + 1] * scale);
+      const uint32_t x1 = pack2bf(dq[dt][4 * ga + 2] * scale, dq[dt][4 * ga + 3] * scale);
+      const uint32_t y0 = pack2bf(dq[dt][4 * gb] * scale, dq[dt][4 * gb + 1] * scale);
+      const uint32_t y1 = pack2bf(dq[dt][4 * gb + 2] * scale, dq[dt][4 * gb + 3] * scale);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+      const int d0 = dt * 32 + 16 * pr + 8 * h;
+      if (okq)
+        *reinterpret_cast<u32x4*>(P.dq + (rowbase + tq) * P.dq_ld + head * 64 + d0) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    }
+}
+
+hipError_t mmt_attn_bwd_dq_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, hipStream_t s) {
+  const int nt = (T + 31) / 32;
+  const int nqb = (nt + 3) / 4;
+  const dim3 grid(nqb * B * H, 1, bt.count);
+  if (drop) hipLaunchKernelGGL((attn_bwd_dq_ring64<true>), grid, dim3(256), 0, s, bt, T, H, scale);
+  else hipLaunchKernelGGL((attn_bwd_dq_ring64<false>), grid, dim3(256), 0, s, bt, T, H, scale);
+  return hipGetLastError();
+}
+
+hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, bool occ3,
+                                    hipStream_t s) {
+  const int nt = (T + 31) / 32;
+  const int nkb = (nt + 3) / 4;
+  const dim3 grid(nkb * B * H * bt.p[0].nstreams, 1, bt.count);
+  if (occ3) {  // 3 waves per SIMD (<= 168 VGPRs)
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 3>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 3>), grid, dim3(256), 0, s, bt, T, H, scale);
+  } else {
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2>), grid, dim3(256), 0, s, bt, T, H, scale);
+  }
+  return hipGetLastError();
+}

@@ -129,7 +129,7 @@ struct AttnProblem {
   int kv_ld, kv_hstride;
   bf16_t* o; int o_ld;
   bf16_t* oj[MMT_MAX_STREAMS];   // per-stream normalised outputs (nullable when nstreams == 1)
-  float* lse[MMT_MAX_STREAMS];   // [B*H*T] per stream
+  float* lse[MMT_MAX_STREAMS];   // [B*H*T] per stream, log2 domain: log2 sum_s 2^(log2e * scale * q.k_s)
   // backward
   const bf16_t* dout; int dout_ld;
   float* dvec[MMT_MAX_STREAMS];  // rowsum(dO * O_j) per stream [B*H*T]
@@ -160,6 +160,11 @@ inline int64_t mmt_attn_mask_dwords(int B, int H, int T) { return 2 * 32 * mmt_a
 struct AttnBatch { AttnProblem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
 hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
+// hs 64 dK/dV pass streaming the query slices through an LDS-DMA ring (mmt_attn2.hip)
+hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, bool occ3,
+                                    hipStream_t s);
+// hs 64 dQ pass (and D_j) streaming the key slices through an LDS-DMA ring (mmt_attn2.hip)
+hipError_t mmt_attn_bwd_dq_ring64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, hipStream_t s);
 // fill dmask[j] (j < nstreams) of every problem with drop_thr != 0 from its counter hash
 hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStream_t s);
 

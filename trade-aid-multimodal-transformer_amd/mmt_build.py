@@ -16,13 +16,13 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(CSRC, "build")
 LIB = os.path.join(HERE, "libmmt_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["mmt_gemm.hip", "mmt_attn.hip", "mmt_elem.hip", "mmt_qkv2.hip", "mmt_engine.hip", "mmt_ops.hip", "mmt_batch.hip", "mmt_decode.hip"]
+SOURCES = ["mmt_gemm.hip", "mmt_attn.hip", "mmt_attn2.hip", "mmt_elem.hip", "mmt_qkv2.hip", "mmt_engine.hip", "mmt_ops.hip", "mmt_batch.hip", "mmt_decode.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(REPO, "include"), "-I" + CSRC,
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
 
 # per-file flags: the attention softmax keeps scalar fp32 ops (packed v_pk_*_f32 issue slower
 # beside MFMAs, MI355X_MICROARCH.md), so the SLP vectoriser must not re-pack them
-FILE_FLAGS = {"mmt_attn.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"mmt_attn.hip": ["-fno-slp-vectorize"], "mmt_attn2.hip": ["-fno-slp-vectorize"]}
 
 
 def _deps_mtime():

@@ -78,6 +78,12 @@ _SIGS = {
     "mmt_batch_indices": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     "mmt_batch_gather": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), c_vp, c_i32, c_i32, ctypes.POINTER(c_vp),
                                  ctypes.POINTER(c_vp)]),
+    "mmt_exact_words_bytes": (c_i64, [c_i64]),
+    "mmt_exact_walk_scratch_bytes": (c_i64, [c_i64, c_i64]),
+    "mmt_exact_gen": (c_i32, [c_vp, c_vp, c_vp, c_i64]),
+    "mmt_exact_walk": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), ctypes.POINTER(c_i32),
+                               ctypes.POINTER(c_i32), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "mmt_attn_set_ring": (c_i32, [ctypes.c_int]),
     "mmt_gemm_set_variant": (c_i32, [ctypes.c_int]),
     "mmt_op_gemm": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp,
                             c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32]),
@@ -147,5 +153,7 @@ def ptr_array(ts):
     return arr
 
 
-def stream_ptr(device=None):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+def stream_ptr(device=None, stream=None):
+    """HIP stream handle of `stream` (default: torch's current stream on `device`)."""
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)

@@ -16,10 +16,19 @@ lines and log lines. What changed underneath:
       - fast (default on a GPU): DeviceBatcher, the streams resident in HBM and the walk, the
         start indices and the gather as HIP kernels driven by a counter hash: the same laws
         (tested), not the same draws;
+      - exact on the device (batcher_mode = "exact", or MMT_EXACT_BATCHER=device):
+        ExactDeviceBatcher, bit-exact like the host mode at device speed: the streams resident in
+        HBM, Python's MT19937 run on the GPU from random.getstate() (mmt_exact_gen, a side stream,
+        overlapping the previous step) and the walk as prefix-sum kernels (mmt_exact_walk); the
+        start indices drawn with the reference's torch.randint calls on the CPU (a few dozen
+        values), the windows gathered on the device. Python's `random` state and the host
+        training lists are brought up to date at every estimate_loss and by sync_host_state();
   * calculate_evaluation_metrics runs the per-sample argmax / direction / softmax-certainty loop
     (training_utils.py:259-304) as one HIP kernel per modality (mmt_eval_direction) with a single
     device->host copy, instead of B*V `.item()` syncs.
 """
+import ctypes
+import math
 import numbers
 import os
 import random
@@ -257,20 +266,151 @@ class DeviceBatcher:
         return xs, ys
 
 
+class ExactDeviceBatcher:
+    """get_batch bit-exact with the reference (walk, Python `random` consumption, torch start
+    indices) with the token streams resident in HBM: see the module docstring and
+    csrc/mmt_batch.hip (mmt_exact_gen / mmt_exact_walk)."""
+
+    def __init__(self, train_sets, val_sets, vocab_sizes, rand_sizes, file_lengths_, is_percents_, block_size,
+                 batch_size, device):
+        self.device = torch.device(device)
+        self.T, self.B = int(block_size), int(batch_size)
+        self.file_lengths, self.is_percents = file_lengths_, bool(is_percents_)
+        self.V = [int(v) for v in vocab_sizes]
+        rs = []
+        for r in rand_sizes:  # the reference's checks (data_utils.py:322-330)
+            if r is None:
+                rs.append(0)
+                continue
+            if not isinstance(r, (int, np.integer)):
+                raise TypeError("rand_size must be an integer or null.")
+            if int(r) < 1 or int(r) > 3:
+                raise ValueError("rand_size must be an integer between 1 and 3, or null.")
+            rs.append(int(r))
+        self.rs = rs
+        self.host_train = train_sets
+
+        def dev32(a):
+            a = a.numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+            return torch.from_numpy(a.astype(np.int32)).to(self.device)
+
+        self.data = {"train": [dev32(_as_array(i)) for i in range(len(train_sets))],
+                     "val": [dev32(v) for v in val_sets]}
+        n = [int(t.numel()) for t in self.data["train"]]
+        # words per step: every element eligible, 2% over the expected draws + a fixed margin (the
+        # shortfall probability is astronomically small; the walk flags it in self.status)
+        self.nwords = 16384 + sum(int(math.ceil(ni * (1 << (2 * r + 1).bit_length()) / (2 * r + 1) * 1.02))
+                                  for ni, r in zip(n, rs) if r)
+        L = ML.lib()
+        self.words = torch.empty(max(1, L.mmt_exact_words_bytes(self.nwords)) // 4, dtype=torch.int32,
+                                 device=self.device)
+        self.scratch = torch.empty(L.mmt_exact_walk_scratch_bytes(max(n + [1]), self.nwords), dtype=torch.uint8,
+                                   device=self.device)
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.n = (ctypes.c_int64 * len(n))(*n)
+        self.rs_c = (ctypes.c_int32 * len(rs))(*rs)
+        self.V_c = (ctypes.c_int32 * len(self.V))(*self.V)
+        self._load_state(random.getstate())
+        self.side = torch.cuda.Stream(device=self.device)
+        self.gen_done = None  # event: the words of the next walk are generated
+        self.dirty = False    # device walk / generator state ahead of the host copies
+
+    def _load_state(self, st):
+        key = np.asarray(st[1], dtype=np.uint32)  # 624 key words + index
+        self.mt = torch.from_numpy(key.view(np.int32).copy()).to(self.device)
+        self.py_state = st
+
+    def _gen(self, stream):
+        ML.check(ML.lib().mmt_exact_gen(ML.stream_ptr(self.device, stream), ML.ptr(self.mt), ML.ptr(self.words),
+                                        self.nwords), None, "mmt_exact_gen")
+
+    def next(self, split, is_training):
+        L = ML.lib()
+        cur = torch.cuda.current_stream(self.device)
+        if is_training == 1 and any(self.rs):
+            if random.getstate() != self.py_state:
+                raise RuntimeError("Python's `random` was used between device-exact get_batch calls: the reference "
+                                   "shares that stream with its walk; call training_utils.sync_host_state() first")
+            if self.gen_done is None:
+                self._gen(cur)
+            else:
+                cur.wait_event(self.gen_done)
+            ptrs = (ctypes.c_void_p * len(self.rs))(*[t.data_ptr() for t in self.data["train"]])
+            ML.check(L.mmt_exact_walk(ML.stream_ptr(self.device, cur), len(self.rs), ptrs, self.n, self.rs_c, self.V_c,
+                                      ML.ptr(self.mt), ML.ptr(self.words), self.nwords, ML.ptr(self.scratch),
+                                      self.scratch.numel(), ML.ptr(self.status)), None, "mmt_exact_walk")
+            # the next step's words, generated on the side stream while this step computes
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self.side.wait_event(ev)
+            self._gen(self.side)
+            self.gen_done = torch.cuda.Event()
+            self.gen_done.record(self.side)
+            self.dirty = True
+        data = self.data[split]
+        ix = generate_batch_starting_indices(int(data[0].numel()), self.T, self.B, split, self.file_lengths,
+                                             self.is_percents)  # the reference's torch.randint calls
+        slot = _ring_slot()
+        ixp = _pinned_buf(("ix", slot), (self.B,))
+        ixp.copy_(ix)
+        ixd = ixp.to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        _ring_events[slot] = ev
+        xs = [torch.empty(self.B, self.T, dtype=torch.long, device=self.device) for _ in data]
+        ys = [torch.empty(self.B, self.T, dtype=torch.long, device=self.device) for _ in data]
+        ML.check(L.mmt_batch_gather(ML.stream_ptr(self.device, cur), len(data), ML.ptr_array(data), ML.ptr(ixd), self.B,
+                                    self.T, ML.ptr_array(xs), ML.ptr_array(ys)), None, "mmt_batch_gather")
+        return xs, ys
+
+    def sync_host_state(self):
+        """Python's `random` state and the walked training lists (in place) as the reference's loop
+        leaves them; one device sync."""
+        if not self.dirty:
+            return
+        if int(self.status.item()):
+            raise RuntimeError("device-exact get_batch: the generated MT19937 words ran out (walk incomplete)")
+        key = self.mt.cpu().numpy().view(np.uint32)
+        st = (self.py_state[0], tuple(int(x) for x in key), self.py_state[2])
+        random.setstate(st)
+        self.py_state = random.getstate()
+        for i, t in enumerate(self.data["train"]):
+            arr = _as_array(i)
+            arr[...] = t.cpu().numpy()
+        self.dirty = False
+
+
 _device_batcher = [None]
-use_device_batcher = os.environ.get("MMT_EXACT_BATCHER", "0") in ("", "0")
+use_device_batcher = os.environ.get("MMT_EXACT_BATCHER", "0") in ("", "0", "device")
+# "hash": DeviceBatcher (counter-hash draws, same laws), "exact": ExactDeviceBatcher (bit-exact)
+batcher_mode = "exact" if os.environ.get("MMT_EXACT_BATCHER", "") == "device" else "hash"
 
 
 def _get_device_batcher():
     b = _device_batcher[0]
-    key = (id(all_train_sets), id(all_val_sets), _get_block_size(), _get_batch_size(), str(_get_device()))
+    key = (id(all_train_sets), id(all_val_sets), _get_block_size(), _get_batch_size(), str(_get_device()), batcher_mode)
     if b is None or b[0] != key:
-        inst = DeviceBatcher(all_train_sets, all_val_sets, [len(v) for v in all_vocabularies],
-                             [p[2] for p in all_modality_params], file_lengths, is_percents, _get_block_size(),
-                             _get_batch_size(), _get_device(), seed=random.getrandbits(63))
+        if b is not None and isinstance(b[1], ExactDeviceBatcher):
+            b[1].sync_host_state()
+        if batcher_mode == "exact":
+            inst = ExactDeviceBatcher(all_train_sets, all_val_sets, [len(v) for v in all_vocabularies],
+                                      [p[2] for p in all_modality_params], file_lengths, is_percents,
+                                      _get_block_size(), _get_batch_size(), _get_device())
+        else:
+            inst = DeviceBatcher(all_train_sets, all_val_sets, [len(v) for v in all_vocabularies],
+                                 [p[2] for p in all_modality_params], file_lengths, is_percents, _get_block_size(),
+                                 _get_batch_size(), _get_device(), seed=random.getrandbits(63))
         b = (key, inst)
         _device_batcher[0] = b
     return b[1]
+
+
+def sync_host_state():
+    """Device-exact mode: write the device's walk and generator state back into the training lists
+    and Python's `random` (as the reference's loop leaves them); a no-op in the other modes."""
+    b = _device_batcher[0]
+    if b is not None and isinstance(b[1], ExactDeviceBatcher):
+        b[1].sync_host_state()
 
 
 def get_batch(split, is_training):
@@ -453,6 +593,7 @@ def estimate_loss(current_step=None, max_steps=None):
         if state == "train":
             print()
     m.train()
+    sync_host_state()  # device-exact batcher: the host lists / Python random as the reference leaves them
     return out
 
 
