@@ -204,6 +204,18 @@ int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, con
                          void* y16, float* mean, float* rstd);
 int mmt_op_layernorm_bwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* mean,
                          const float* rstd, const float* dy, float* dx, void* dx16, float* dgamma, float* dbeta);
+/* backward-data GEMM with the LayerNorm backward of its rows fused (the engine's path when C == 256;
+ * replaces the pair mmt_op_gemm(EPI store_f32) + mmt_op_layernorm_bwd, model.py:189-190 under
+ * autograd): dy = alpha * A[M, K] B[K, N] (A K-contiguous, B MN-contiguous, bf16), never stored;
+ * dx[M, N] += rstd * (g dy - mean(g dy) - xhat mean(g dy xhat)) with xhat = (x - mean) * rstd;
+ * dx16 (nullable) = bf16(keep(m, n) * dx) with the hash mask of drop_key / drop_thr (0: no mask,
+ * kept values times drop_scale) and dsum (nullable) += its column sums; dgamma += colsum(dy xhat),
+ * dbeta += colsum(dy). N must be 256 or 512; row strides: A lda, B ldb, x / dx N, dx16 N.
+ * MMT_ERR_UNSUPPORTED when the shape does not fit the fused kernel. */
+int mmt_op_gemm_ln_bwd(void* stream, int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, const void* B,
+                       int32_t ldb, float alpha, const float* x, const float* gamma, const float* mean,
+                       const float* rstd, float* dx, void* dx16, float* dgamma, float* dbeta, float* dsum,
+                       uint32_t drop_key, uint32_t drop_thr, float drop_scale);
 /* causal attention over nstreams KV streams; layouts as in the engine (row = b*T + t) */
 int mmt_op_attention_fwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams,
                          const void* q, int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld,

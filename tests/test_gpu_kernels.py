@@ -238,6 +238,60 @@ def test_layernorm(R, C):
     assert rel(db, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,drop", [(1000, 256, 1024, 0.0), (256, 256, 384, 0.1), (300, 256, 72, 0.1),
+                                         (4096, 256, 256, 0.0), (2, 256, 450, 0.1), (1000, 512, 2048, 0.0),
+                                         (300, 512, 768, 0.1), (130, 512, 72, 0.1)])
+def test_gemm_ln_bwd_fused(M, N, K, drop):
+    """Backward-data GEMM with the LayerNorm backward fused into its epilogue (the engine's path at
+    C = 256) against torch: dy = alpha A B in fp32, F.layer_norm's autograd for dx / dgamma / dbeta,
+    the bf16 copy with the hash dropout mask of the consuming branch and its column sums."""
+    import mmt_oracle as O
+    torch.manual_seed(M + K)
+    A = bf(torch.randn(M, K, device=DEV))
+    Bm = bf(torch.randn(K, N, device=DEV) * 0.05)
+    x = torch.randn(M, N, device=DEV) * 2 + 0.5
+    g = torch.randn(N, device=DEV)
+    b = torch.randn(N, device=DEV)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    mean = torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    L = ML.lib()
+    assert L.mmt_op_layernorm_fwd(_s(), M, N, ML.ptr(x), ML.ptr(g), ML.ptr(b), ML.ptr(y), ML.ptr(mean), ML.ptr(rstd)) == 0
+    alpha = 0.7
+    dy = alpha * (A.float() @ Bm.float())
+    xr = x.clone().requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (N,), gr, br, 1e-5).backward(dy)
+    dx0 = torch.randn(M, N, device=DEV)
+    dx = dx0.clone()
+    dx16 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    dg = torch.zeros(N, device=DEV)
+    db = torch.zeros(N, device=DEV)
+    ds = torch.zeros(N, device=DEV)
+    hd = O.HashDropout(7, drop) if drop else None
+    key = 0x1234567
+    assert L.mmt_op_gemm_ln_bwd(_s(), M, N, K, ML.ptr(A), K, ML.ptr(Bm), N, alpha, ML.ptr(x), ML.ptr(g), ML.ptr(mean),
+                                ML.ptr(rstd), ML.ptr(dx), ML.ptr(dx16), ML.ptr(dg), ML.ptr(db), ML.ptr(ds), key,
+                                hd.thr if hd else 0, hd.scale if hd else 1.0) == 0
+    _sync()
+    assert rel(dx - dx0, xr.grad) < 1e-4
+    assert rel(dg, gr.grad) < 1e-4
+    assert rel(db, br.grad) < 1e-4
+    if hd:
+        rows = torch.arange(M).numpy()[:, None]
+        cols = torch.arange(N).numpy()[None, :]
+        exp16 = dx.cpu() * hd._mask(key, rows, cols)
+    else:
+        exp16 = dx.cpu()
+    assert rel(dx16.cpu(), exp16) < 1e-2
+    assert rel(ds.cpu(), exp16.sum(0)) < 1e-4
+    # a row width other than 256 is refused, nothing launched
+    assert L.mmt_op_gemm_ln_bwd(_s(), M, 128, K, ML.ptr(A), K, ML.ptr(Bm), N, alpha, ML.ptr(x), ML.ptr(g), ML.ptr(mean),
+                                ML.ptr(rstd), ML.ptr(dx), ML.ptr(dx16), ML.ptr(dg), ML.ptr(db), ML.ptr(ds), 0, 0,
+                                1.0) == -2  # MMT_ERR_UNSUPPORTED
+
+
 # --------------------------------------------------------------------------------- attention
 def _attn_ref(q, ks, vs, scale):
     # q [B,H,T,hs], ks/vs list of [B,H,T,hs]; sum over streams of causal softmax attention

@@ -59,7 +59,15 @@ __device__ __forceinline__ void wait_vm(int n) {
     case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
   }
 }
 
@@ -91,10 +99,10 @@ __device__ __forceinline__ int key_dword(int r) { return 2 * ((r & 3) + 4 * (r >
 // Workgroups are ordered heaviest key block first (the causal walk of key block kb is nt - 4 kb
 // slices long) so the launch does not end on a tail of long blocks.
 // =============================================================================================
-template <bool DROP, int OCC>
+template <bool DROP, int OCC, int S>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch, int T, int H, float scale) {
   constexpr int NKS = 4, ND = 2;  // hs 64: 4 k-steps of 16, 2 output tiles of 32
-  constexpr int S = 4;            // ring slots: S - 1 slices in flight
+  static_assert(S >= 3 && 4 * (S - 2) <= 16, "ring slots: S - 1 slices in flight, counted waits <= 16");
   constexpr int OFF_DO = IMG64, OFF_L = 2 * IMG64, OFF_D = OFF_L + 256, OFF_M = OFF_D + 256;
   constexpr int SLOT = OFF_M + (DROP ? 1024 : 0);
   constexpr int EPW = 40;  // epilogue transpose slot row stride (bf16)
@@ -325,10 +333,10 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch
 // dP^T = V dO^T (queries on lanes), dS^T = P^T (Z dP^T - D), dQ^T += K^T dS^T. Heaviest query block
 // first. The per-stream LSE / D of the block's rows live in a small LDS table.
 // =============================================================================================
-template <bool DROP>
+template <bool DROP, int S>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64(AttnBatch batch, int T, int H, float scale) {
   constexpr int NKS = 4, ND = 2;
-  constexpr int S = 4;
+  static_assert(S >= 3 && 3 * (S - 2) <= 16, "ring slots: S - 1 slices in flight, counted waits <= 16");
   constexpr int OFF_V = IMG64, OFF_M = 2 * IMG64;
   constexpr int SLOT = OFF_M + (DROP ? 1024 : 0);
   constexpr int TAB = S * SLOT;  // [wave][stream][query row] {lse2, D} float2
@@ -515,13 +523,39 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64(AttnBatch batch, in
     }
 }
 
+// ring depth knob (slots; S - 1 slices in flight): MMT_ATTN_RING_SLOTS = 4 (default) or 6
+static int ring_slots() {
+  static const int v = [] {
+    const char* e = getenv("MMT_ATTN_RING_SLOTS");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 hipError_t mmt_attn_bwd_dq_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, hipStream_t s) {
   const int nt = (T + 31) / 32;
   const int nqb = (nt + 3) / 4;
   const dim3 grid(nqb * B * H, 1, bt.count);
-  if (drop) hipLaunchKernelGGL((attn_bwd_dq_ring64<true>), grid, dim3(256), 0, s, bt, T, H, scale);
-  else hipLaunchKernelGGL((attn_bwd_dq_ring64<false>), grid, dim3(256), 0, s, bt, T, H, scale);
+  const bool deep = ring_slots() >= 6;
+  if (drop) {
+    if (deep) hipLaunchKernelGGL((attn_bwd_dq_ring64<true, 6>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dq_ring64<true, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
+  } else {
+    if (deep) hipLaunchKernelGGL((attn_bwd_dq_ring64<false, 6>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dq_ring64<false, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
+  }
   return hipGetLastError();
+}
+
+template <int S>
+static void dkdv_launch(const AttnBatch& bt, dim3 grid, int T, int H, float scale, bool drop, bool occ3, hipStream_t s) {
+  if (occ3) {  // 3 waves per SIMD (<= 168 VGPRs)
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 3, S>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 3, S>), grid, dim3(256), 0, s, bt, T, H, scale);
+  } else {
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2, S>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2, S>), grid, dim3(256), 0, s, bt, T, H, scale);
+  }
 }
 
 hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, bool occ3,
@@ -529,12 +563,7 @@ hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& bt, int B, int T, int H, fl
   const int nt = (T + 31) / 32;
   const int nkb = (nt + 3) / 4;
   const dim3 grid(nkb * B * H * bt.p[0].nstreams, 1, bt.count);
-  if (occ3) {  // 3 waves per SIMD (<= 168 VGPRs)
-    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 3>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 3>), grid, dim3(256), 0, s, bt, T, H, scale);
-  } else {
-    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2>), grid, dim3(256), 0, s, bt, T, H, scale);
-  }
+  if (ring_slots() >= 6) dkdv_launch<6>(bt, grid, T, H, scale, drop, occ3, s);
+  else dkdv_launch<4>(bt, grid, T, H, scale, drop, occ3, s);
   return hipGetLastError();
 }

@@ -530,6 +530,9 @@ void gemm_cost(const GemmBatch& b, int epi, double* fl, double* by) {
     if (epi == EPI_BIAS_RESID_F32) x += M * N * 4.0 + (P.o16 ? M * N * 2.0 : 0.0);
     if (epi == EPI_ACC_F32) x += M * N * 4.0;
     if (epi == EPI_DTANH_BF16 || epi == EPI_DRELU_BF16) x += M * N * 2.0;
+    // fused LayerNorm backward: LN input and the accumulated gradient read, that gradient (+ its bf16
+    // copy) written, row statistics read
+    if (epi == EPI_LN_BWD_F32) x += M * N * 8.0 + (P.o16 ? M * N * 2.0 : 0.0) + M * 8.0;
     *by += x;
   }
 }
@@ -635,6 +638,43 @@ struct Runner {
       for (int g = 0; g < b.count; ++g) by -= ((double)b.p[g].M + b.p[g].N) * b.p[g].K;  // 1-byte operands
       probe_end(id, s, fl, by);
     }
+  }
+  // backward-data GEMM dy = A B (EPI_STORE_F32 into lb's dy) followed by the LayerNorm backward lb
+  // (model.py:189-190, 210, 330 under autograd): ONE launch with the LayerNorm fused into the GEMM's
+  // epilogue when every problem's rows fit one tile (C == 256 or 512; MMT_LN_FUSE=0 disables), else
+  // the two passes. The fused launch never materialises dy (the fp32 round trip of the two-pass form)
+  void gemm_ln_bwd(const GemmBatch& dx, const LnBatch& lb, int R, int C, const char* gname, const char* lname) {
+    if (rc != MMT_OK) return;
+    static const bool fuse = [] {
+      const char* e = getenv("MMT_LN_FUSE");
+      return e ? atoi(e) != 0 : true;
+    }();
+    if (fuse && lb.count == dx.count) {
+      GemmBatch f = dx;
+      for (int g = 0; g < f.count; ++g) {
+        GemmProblem& P = f.p[g];
+        const LnProblem& Lp = lb.p[g];
+        P.o32 = Lp.dx; P.ldc = C;
+        P.resid = Lp.x; P.ldres = C;
+        P.ln_gamma = Lp.gamma; P.ln_mean = Lp.mean; P.ln_rstd = Lp.rstd;
+        P.ln_dgamma = Lp.dgamma; P.ln_dbeta = Lp.dbeta;
+        P.o16 = Lp.dx16; P.ldo16 = C; P.dbias = Lp.dsum;
+        P.drop_key = Lp.drop_key; P.drop_thr = Lp.drop_thr; P.drop_scale = Lp.drop_scale;
+        P.bias = nullptr; P.aux = nullptr; P.split_stride = 0;
+      }
+      if (mmt_gemm_ln_bwd_ok(f)) {
+        const int id = probe_begin(gname, s);
+        ok(mmt_launch_gemm_ln_bwd(f, s), gname);
+        if (id >= 0) {
+          double fl = 0, by = 0;
+          gemm_cost(f, EPI_LN_BWD_F32, &fl, &by);
+          probe_end(id, s, fl, by);
+        }
+        return;
+      }
+    }
+    gemm(dx, true, false, EPI_STORE_F32, 1, gname);
+    ok(mmt_launch_ln_bwd(lb, R, C, s), lname);
   }
   void gemm(const GemmBatch& b, bool akc, bool bkc, int epi, int splits, const char* what) {
     if (rc != MMT_OK) return;
@@ -1198,7 +1238,6 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
     }
     r.dwgemm(dw, "head0_dw");
-    r.gemm(dx, true, false, EPI_STORE_F32, 1, "head0_dx");
     r.flush();
     LnBatch lb{}; lb.count = M;
     d16_advance(c);
@@ -1212,7 +1251,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       set_dres16_consumer(c, r, lb.p[i], i, L - 1, grads);
       lb.p[i].dgamma = grads + c->post[i].lnw; lb.p[i].dbeta = grads + c->post[i].lnb;
     }
-    r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "lnf_bwd");
+    r.gemm_ln_bwd(dx, lb, R, C, "head0_dx", "lnf_bwd");
     return r.rc;
   }
   // layer stage
@@ -1282,7 +1321,6 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       dx.p[u].o32 = r.W<float>(p.dln[i]); dx.p[u].ldc = C;
     }
     r.dwgemm(dw, "ca_q_dw");
-    r.gemm(dx, true, false, EPI_STORE_F32, 1, "ca_q_dx");
     LnBatch lc{}; lc.count = nc;
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
@@ -1290,7 +1328,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       lc.p[u].rstd = r.W<float>(a[i].rstdc); lc.p[u].dy = r.W<float>(p.dln[i]); lc.p[u].dx = r.W<float>(p.dres[i]);
       lc.p[u].dgamma = grads + x[i].lncw; lc.p[u].dbeta = grads + x[i].lncb;
     }
-    r.ok(mmt_launch_ln_bwd(lc, R, C, r.s), "lnc_bwd");
+    r.gemm_ln_bwd(dx, lc, R, C, "ca_q_dx", "lnc_bwd");
     // KV projections: dWkv += dkv^T x2_j ; dres[j] += dkv Wkv (one launch per query modality:
     // different query modalities accumulate into the same dres[j])
     for (int i : cx) {
@@ -1344,7 +1382,6 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
   }
   r.dwgemm(dw, "ffn0_dw");
-  r.gemm(dx, true, false, EPI_STORE_F32, 1, "ffn0_dx");
   r.flush();
   d16_advance(c);
   for (int i = 0; i < M; ++i) {
@@ -1354,7 +1391,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     r.set_drop(lb.p[i], l, i, DS_SA_PROJ);  // the copy feeds the SA projection backward
     lb.p[i].dsum = grads + x[i].bp2;
   }
-  r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln2_bwd");
+  r.gemm_ln_bwd(dx, lb, R, C, "ffn0_dx", "ln2_bwd");
   // SA output projection
   for (int i = 0; i < M; ++i) {
     const bf16_t* g = d16_cur(c, r, i);
@@ -1401,7 +1438,6 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
   }
   r.dwgemm(dw, "qkv1_dw");
-  r.gemm(dx, true, false, EPI_STORE_F32, 1, "qkv1_dx");
   r.flush();
   d16_advance(c);
   for (int i = 0; i < M; ++i) {
@@ -1410,7 +1446,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     lb.p[i].dgamma = grads + x[i].ln1w; lb.p[i].dbeta = grads + x[i].ln1b;
     set_dres16_consumer(c, r, lb.p[i], i, l - 1, grads);
   }
-  r.ok(mmt_launch_ln_bwd(lb, R, C, r.s), "ln1_bwd");
+  r.gemm_ln_bwd(dx, lb, R, C, "qkv1_dx", "ln1_bwd");
   return r.rc;
 }
 

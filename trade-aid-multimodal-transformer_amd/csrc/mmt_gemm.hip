@@ -40,6 +40,9 @@ using TileS = TileCfg<2, 2, 2, 2>;
 // stage in flight has ~2 k cycles of matrix work per SIMD to land behind (long-K shapes, weight
 // gradients); 128 KiB ring -> 1 block per CU
 using TileL = TileCfg<2, 4, 4, 2>;
+// 128 x 512, 8 waves (1 x 8) of 128 x 64 (TileL's per-wave shape): whole 512-wide rows per block for
+// the fused LayerNorm-backward epilogue at C = 512 (BK 32 x 2 stages = 80 KiB of ring)
+using TileW = TileCfg<1, 8, 4, 2>;
 
 // tuning knob (mmt_gemm_set_variant): pipeline variant of the forward / backward-data GEMMs in
 // bits 0-3 and of the weight-grad (split-K, atomic) GEMMs in bits 4-7:
@@ -224,7 +227,15 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
   constexpr bool CAN_DB = EPI == EPI_STORE_BF16 || EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
   // MX-fp8 copy of a forward activation (P.o8; needs N % 32 == 0 and the vector path)
   constexpr bool MX_OUT = EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_STORE_BF16;
-  const bool want_db = CAN_DB && P.dbias != nullptr;
+  // fused LayerNorm backward (whole rows per block: N == GBN, checked by the launcher)
+  constexpr bool LNB = EPI == EPI_LN_BWD_F32;
+  const bool want_db = (CAN_DB || LNB) && P.dbias != nullptr;
+  float cg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, cb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x4 gam0 = {0.f, 0.f, 0.f, 0.f}, gam1 = {0.f, 0.f, 0.f, 0.f};
+  if (LNB && n + 8 <= N) {
+    gam0 = *reinterpret_cast<const f32x4*>(P.ln_gamma + n);
+    gam1 = *reinterpret_cast<const f32x4*>(P.ln_gamma + n + 4);
+  }
   // 16-B vector accesses need bf16 leading dimensions % 8 and fp32 ones % 4 (bias pointers are
   // 64-B aligned by the parameter layout)
   const bool vec_ok = ((P.ldo16 | P.ldaux) & 7) == 0 && ((P.ldc | P.ldres) & 3) == 0;
@@ -254,7 +265,80 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
       }
     __syncthreads();
     const int mb = m0 + pass * EPI_ROWS;
-    if (n + 8 <= N && vec_ok) {
+    if constexpr (LNB) {
+      // a row's GBN columns are TPR = 32 consecutive threads (one half wave): row sums by 5 xor
+      // shuffles inside the half. Loads per row (all IT rows' loads up front spill next to the
+      // accumulators still live for the later passes)
+      const float invn = 1.0f / (float)N;
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int ml = it * RPI + rsub;
+        const int m = mb + ml;
+        if (m >= M) continue;  // a whole half wave (one row) at once: the shuffles stay inside it
+        f32x4 xv[1][2], dv[1][2];
+        float mu[1], rs[1];
+        {
+          const float* xp = P.resid + (int64_t)m * P.ldres + n;
+          const float* dp = o32 + (int64_t)m * P.ldc + n;
+          xv[0][0] = *reinterpret_cast<const f32x4*>(xp);
+          xv[0][1] = *reinterpret_cast<const f32x4*>(xp + 4);
+          dv[0][0] = *reinterpret_cast<const f32x4*>(dp);
+          dv[0][1] = *reinterpret_cast<const f32x4*>(dp + 4);
+          mu[0] = P.ln_mean[m];
+          rs[0] = P.ln_rstd[m];
+        }
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8 + 4);
+        float dy[8], xh[8], gd[8];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          dy[e] = alpha * v0[e];
+          dy[e + 4] = alpha * v1[e];
+          xh[e] = (xv[0][0][e] - mu[0]) * rs[0];
+          xh[e + 4] = (xv[0][1][e] - mu[0]) * rs[0];
+          gd[e] = dy[e] * gam0[e];
+          gd[e + 4] = dy[e + 4] * gam1[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1 += gd[e];
+          s2 += gd[e] * xh[e];
+          cg[e] += dy[e] * xh[e];
+          cb[e] += dy[e];
+        }
+#pragma unroll
+        for (int o = 1; o < TPR; o <<= 1) {
+          s1 += __shfl_xor(s1, o, 64);
+          s2 += __shfl_xor(s2, o, 64);
+        }
+        s1 *= invn;
+        s2 *= invn;
+        float r[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r[e] = dv[0][0][e] + rs[0] * (gd[e] - s1 - xh[e] * s2);
+          r[e + 4] = dv[0][1][e] + rs[0] * (gd[e + 4] - s1 - xh[e + 4] * s2);
+        }
+        float* op = o32 + (int64_t)m * P.ldc + n;
+        *reinterpret_cast<f32x4*>(op) = f32x4{r[0], r[1], r[2], r[3]};
+        *reinterpret_cast<f32x4*>(op + 4) = f32x4{r[4], r[5], r[6], r[7]};
+        if (P.o16) {
+          if (P.drop_thr) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // n is even: one hash per column pair (as ln_bwd_kernel)
+              const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n >> 1) + q);
+              r[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? r[2 * q] * P.drop_scale : 0.0f;
+              r[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? r[2 * q + 1] * P.drop_scale : 0.0f;
+            }
+          }
+          *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+              u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += r[e];
+        }
+      }
+    } else if (n + 8 <= N && vec_ok) {
       // issue every operand load of this thread's rows first (memory-level parallelism)
       u32x4 auxv[IT];
       f32x4 resv[IT][2];
@@ -366,27 +450,32 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
       }
     }
   }
-  if (want_db) {
-    // rows of a column group live in lanes l, l^TPR, ... of every wave: fold those, then the
-    // waves via LDS (the staged tile is dead: every thread has read its own rows), one atomic
-    // per column
+  // column sums: rows of a column group live in lanes l, l^TPR, ... of every wave: fold those, then
+  // the waves via LDS (the staged tile is dead: every thread has read its own rows), one atomic per
+  // column
+  auto flush_colsums = [&](float (&v)[8], float* dst) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
-      for (int o = TPR; o < 64; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
+      for (int o = TPR; o < 64; o <<= 1) v[e] += __shfl_xor(v[e], o, 64);
     __syncthreads();
     float* red = ct;  // [NW waves][GBN columns]
     if (lane < TPR) {
-      *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8) = f32x4{cs[0], cs[1], cs[2], cs[3]};
-      *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8 + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+      *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(red + wave * GBN + 8 * c8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
     __syncthreads();
     if (tid < GBN && n0 + tid < N) {
       float sum = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) sum += red[w * GBN + tid];
-      atomicAdd(P.dbias + n0 + tid, sum);
+      atomicAdd(dst + n0 + tid, sum);
     }
+  };
+  if (want_db) flush_colsums(cs, P.dbias);
+  if constexpr (LNB) {
+    flush_colsums(cg, P.ln_dgamma);
+    flush_colsums(cb, P.ln_dbeta);
   }
 }
 
@@ -424,7 +513,7 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
 
   // one LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads):
   // the stage ring during the K loop, the fp32 output tile (EPI_ROWS x (GBN + 4)) in the epilogue
-  constexpr int EPI_ROWS = (GBM == 128 && MINB == 1) ? 128 : 64;
+  constexpr int EPI_ROWS = GBN >= 512 ? 32 : (GBM == 128 && MINB == 1) ? 128 : 64;
   constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
   constexpr int LDS_MAIN = RING > CTILE ? RING : CTILE;
   __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN];
@@ -917,6 +1006,34 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
 
 
 bool mmt_gemm_wgrad_big(const GemmBatch& b) { return use_big(b); }
+
+bool mmt_gemm_ln_bwd_ok(const GemmBatch& b) {
+  if (b.count == 0) return false;
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& P = b.p[g];
+    if ((P.N != TileL::BN && P.N != TileW::BN) || P.N != b.p[0].N || !P.resid || !P.o32 || !P.ln_gamma || !P.ln_mean || !P.ln_rstd || !P.ln_dgamma ||
+        !P.ln_dbeta || (P.ldc & 3) || (P.ldres & 3) || (P.o16 && (P.ldo16 & 7)) || (P.lda & 7) || (P.ldb & 7) ||
+        (((uintptr_t)P.A | (uintptr_t)P.B | (uintptr_t)P.o32 | (uintptr_t)P.resid | (uintptr_t)P.ln_gamma) & 15))
+      return false;
+  }
+  return true;
+}
+
+hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
+  if (!mmt_gemm_ln_bwd_ok(b)) return hipErrorInvalidValue;
+  // a tile as wide as the row, whatever K: its block owns whole rows of the LayerNorm (C = 256:
+  // 256 x 256; C = 512: 128 x 512)
+  if (b.p[0].N == TileW::BN) {
+    const int mt = max_tiles<TileW>(b, nullptr);
+    if (mt == 0) return hipSuccess;
+    launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+  } else {
+    const int mt = max_tiles<TileL>(b, nullptr);
+    if (mt == 0) return hipSuccess;
+    launch_v<TileL, 64, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+  }
+  return hipGetLastError();
+}
 
 template <class TL, int EPI>
 static hipError_t launch_f8(const GemmBatch& b, hipStream_t s) {

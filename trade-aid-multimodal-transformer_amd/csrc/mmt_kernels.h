@@ -26,6 +26,12 @@ enum MmtEpi {
   EPI_DRELU_BF16,       // o16 = aux > 0 ? alpha*acc : 0
   EPI_ACC_F32,          // o32 += alpha*acc
   EPI_ATOMIC_F32,       // atomicAdd(o32, alpha*acc)
+  // LayerNorm backward of the rows this GEMM's dy = alpha*acc belongs to (the block's tile must
+  // span every column: N == 256 on the 256x256 tile, N == 512 on 128x512; mmt_launch_gemm_ln_bwd):
+  //   xhat = (resid - ln_mean) * ln_rstd ; o32 += ln_rstd * (g dy - mean(g dy) - xhat mean(g dy xhat))
+  //   o16 (optional) = bf16 of the dropout-masked o32 (mask as EPI_BIAS_RESID_F32), dbias += its column
+  //   sums; ln_dgamma += column sums of dy * xhat, ln_dbeta += column sums of dy  (ln_bwd_kernel fused)
+  EPI_LN_BWD_F32,
   EPI_COUNT
 };
 
@@ -60,6 +66,13 @@ struct GemmProblem {
   uint8_t* o8;
   uint8_t* s8;
   int ld8, lds8;
+  // EPI_LN_BWD_F32: the LayerNorm's weight, saved row statistics and parameter gradients (the LN
+  // input rows are resid / ldres, the accumulated input gradient o32 / ldc)
+  const float* ln_gamma;
+  const float* ln_mean;
+  const float* ln_rstd;
+  float* ln_dgamma;
+  float* ln_dbeta;
 };
 
 struct GemmBatch {
@@ -68,6 +81,11 @@ struct GemmBatch {
 };
 
 hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, int splits, hipStream_t s);
+// backward-data GEMM dy = alpha * A B (A K-contiguous, B MN-contiguous) with the LayerNorm backward of
+// its rows fused (EPI_LN_BWD_F32) on a tile spanning the row: every problem needs N == 256 (256x256
+// tile) or N == 512 (128x512; all problems alike) and 16-B aligned rows. Returns hipErrorInvalidValue otherwise (the caller runs the two passes)
+bool mmt_gemm_ln_bwd_ok(const GemmBatch& b);
+hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s);
 // weight gradients o32 += alpha * A^T B over K rows (both operands MN-contiguous): split-K into fp32
 // slabs in `slab` (capacity slab_bytes) + one reduce pass; without room, one K pass accumulating
 hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_bytes, hipStream_t s);

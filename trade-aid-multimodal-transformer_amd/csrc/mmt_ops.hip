@@ -57,6 +57,22 @@ int mmt_op_layernorm_bwd(void* stream, int32_t R, int32_t C, const float* x, con
   return st(mmt_launch_ln_bwd(b, R, C, (hipStream_t)stream));
 }
 
+int mmt_op_gemm_ln_bwd(void* stream, int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, const void* B,
+                       int32_t ldb, float alpha, const float* x, const float* gamma, const float* mean,
+                       const float* rstd, float* dx, void* dx16, float* dgamma, float* dbeta, float* dsum,
+                       uint32_t drop_key, uint32_t drop_thr, float drop_scale) {
+  if (M < 0 || N < 0 || K < 0) return MMT_ERR_INVALID;
+  GemmBatch b{};
+  b.count = 1;
+  GemmProblem& p = b.p[0];
+  p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb; p.alpha = alpha; p.M = M; p.N = N; p.K = K;
+  p.resid = x; p.ldres = N; p.o32 = dx; p.ldc = N; p.o16 = (bf16_t*)dx16; p.ldo16 = N; p.dbias = dsum;
+  p.ln_gamma = gamma; p.ln_mean = mean; p.ln_rstd = rstd; p.ln_dgamma = dgamma; p.ln_dbeta = dbeta;
+  p.drop_key = drop_key; p.drop_thr = drop_thr; p.drop_scale = drop_scale;
+  if (!mmt_gemm_ln_bwd_ok(b)) return MMT_ERR_UNSUPPORTED;
+  return st(mmt_launch_gemm_ln_bwd(b, (hipStream_t)stream));
+}
+
 static void fill_attn(AttnProblem& p, int nstreams, const void* q, int q_ld, const void* const* k, const void* const* v,
                       int kv_ld, int kv_hstride) {
   p.q = (const bf16_t*)q; p.q_ld = q_ld; p.kv_ld = kv_ld; p.kv_hstride = kv_hstride; p.nstreams = nstreams;
