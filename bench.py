@@ -63,7 +63,8 @@ def train_flops_per_row(M, C, H, L, T, V, cross, a=0.5):
 PROBES = ["*_dw", "attn_fwd", "attn_bwd", "ffn0", "ffn2_dx"]  # engine launch labels timed live
 PROBE_NAMES = {"*_dw": "weight-gradient GEMMs (all *_dw launches: split-K 256x256 / 128x128 gemm_kernel)",
                "attn_fwd": "attn_fwd_kernel (causal self-attention forward)",
-               "attn_bwd": "attn_bwd_dq_kernel + attn_bwd_dkdv1_kernel (self-attention backward)",
+               "attn_bwd": "self-attention backward: dQ pass + dK/dV pass (attn_bwd_dq_kernel + attn_bwd_dkdv1_kernel; "
+                           "hs 64: attn_bwd_dkdv_ring64, the slice-streamed dK/dV pass)",
                "ffn0": "gemm_kernel ffn0 (X W0^T + b, ReLU, bf16 out)",
                "ffn2_dx": "gemm_kernel ffn2 data gradient (dY W2, ReLU' epilogue, bias-grad column sums)"}
 

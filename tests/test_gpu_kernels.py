@@ -247,7 +247,8 @@ def test_gemm_ln_bwd_fused(M, N, K, drop):
     the bf16 copy with the hash dropout mask of the consuming branch and its column sums."""
     import mmt_oracle as O
     torch.manual_seed(M + K)
-    A = bf(torch.randn(M, K, device=DEV))
+    lda = r8(K)  # 16-B operand staging: row strides padded to 8 elements (as the engine's)
+    A = pad_cols(bf(torch.randn(M, K, device=DEV)), lda)
     Bm = bf(torch.randn(K, N, device=DEV) * 0.05)
     x = torch.randn(M, N, device=DEV) * 2 + 0.5
     g = torch.randn(N, device=DEV)
@@ -258,7 +259,7 @@ def test_gemm_ln_bwd_fused(M, N, K, drop):
     L = ML.lib()
     assert L.mmt_op_layernorm_fwd(_s(), M, N, ML.ptr(x), ML.ptr(g), ML.ptr(b), ML.ptr(y), ML.ptr(mean), ML.ptr(rstd)) == 0
     alpha = 0.7
-    dy = alpha * (A.float() @ Bm.float())
+    dy = alpha * (A[:, :K].float() @ Bm.float())
     xr = x.clone().requires_grad_(True)
     gr = g.clone().requires_grad_(True)
     br = b.clone().requires_grad_(True)
@@ -271,7 +272,7 @@ def test_gemm_ln_bwd_fused(M, N, K, drop):
     ds = torch.zeros(N, device=DEV)
     hd = O.HashDropout(7, drop) if drop else None
     key = 0x1234567
-    assert L.mmt_op_gemm_ln_bwd(_s(), M, N, K, ML.ptr(A), K, ML.ptr(Bm), N, alpha, ML.ptr(x), ML.ptr(g), ML.ptr(mean),
+    assert L.mmt_op_gemm_ln_bwd(_s(), M, N, K, ML.ptr(A), lda, ML.ptr(Bm), N, alpha, ML.ptr(x), ML.ptr(g), ML.ptr(mean),
                                 ML.ptr(rstd), ML.ptr(dx), ML.ptr(dx16), ML.ptr(dg), ML.ptr(db), ML.ptr(ds), key,
                                 hd.thr if hd else 0, hd.scale if hd else 1.0) == 0
     _sync()
@@ -287,7 +288,7 @@ def test_gemm_ln_bwd_fused(M, N, K, drop):
     assert rel(dx16.cpu(), exp16) < 1e-2
     assert rel(ds.cpu(), exp16.sum(0)) < 1e-4
     # a row width other than 256 is refused, nothing launched
-    assert L.mmt_op_gemm_ln_bwd(_s(), M, 128, K, ML.ptr(A), K, ML.ptr(Bm), N, alpha, ML.ptr(x), ML.ptr(g), ML.ptr(mean),
+    assert L.mmt_op_gemm_ln_bwd(_s(), M, 128, K, ML.ptr(A), lda, ML.ptr(Bm), N, alpha, ML.ptr(x), ML.ptr(g), ML.ptr(mean),
                                 ML.ptr(rstd), ML.ptr(dx), ML.ptr(dx16), ML.ptr(dg), ML.ptr(db), ML.ptr(ds), 0, 0,
                                 1.0) == -2  # MMT_ERR_UNSUPPORTED
 
@@ -384,6 +385,20 @@ def test_attention_fwd_bwd(B, T, H, hs, ns):
     for j in range(ns):
         assert rel(heads(got_k[j]), kf[j].grad) < 2e-2, (j, rel(heads(got_k[j]), kf[j].grad))
         assert rel(heads(got_v[j]), vf[j].grad) < 2e-2, (j, rel(heads(got_v[j]), vf[j].grad))
+
+
+@pytest.mark.parametrize("ring", [0, 1, 3])
+@pytest.mark.parametrize("B,T,H,ns", [(2, 100, 2, 1), (1, 520, 2, 2), (1, 1024, 1, 1), (2, 300, 2, 3), (1, 33, 2, 1)])
+def test_attention_hs64_backward_variants(B, T, H, ns, ring):
+    """Every hs-64 backward variant (mmt_attn_set_ring: 0 the chunked dQ and dK/dV passes, 1 the
+    slice-streamed dK/dV ring, 3 both rings with two query tiles per wave in the dQ ring) against the
+    same torch reference, ragged T and multi-stream included."""
+    L = ML.lib()
+    old = L.mmt_attn_set_ring(ring)
+    try:
+        test_attention_fwd_bwd(B, T, H, 64, ns)
+    finally:
+        L.mmt_attn_set_ring(old)
 
 
 # ------------------------------------------------------------------------------ small kernels

@@ -523,6 +523,208 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64(AttnBatch batch, in
     }
 }
 
+
+// =============================================================================================
+// dQ (and D_j) at hs 64, two query tiles per wave. grid (nqb * B*H, 1, problems), nqb = ceil(nt / 8):
+// a workgroup owns 8 query tiles 8 qb .. 8 qb + 7 (wave w: tiles A = 8 qb + w and B = 8 qb + 7 - w,
+// so every wave's causal walk is equally long) and walks (stream j, key tile 0 .. 8 qb + 7) through
+// the LDS ring; a wave reads each slice's K / V fragments (rows and K transposed) ONCE and runs both
+// of its query tiles on them: half the fragment reads, DMA pieces and barriers per MFMA of the
+// one-tile kernel above. Diagonal tiles are masked at run time (a uniform branch around the mask).
+// =============================================================================================
+template <bool DROP, int S>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, int T, int H, float scale) {
+  constexpr int NKS = 4, ND = 2;
+  static_assert(S >= 3 && 3 * (S - 2) <= 16, "ring slots: S - 1 slices in flight, counted waits <= 16");
+  constexpr int OFF_V = IMG64, OFF_M = 2 * IMG64;
+  constexpr int SLOT = OFF_M + (DROP ? 1024 : 0);
+  constexpr int TAB = S * SLOT;  // [wave][tile A / B][stream][query row] {lse2, D} float2
+  __shared__ __attribute__((aligned(1024))) char lds[TAB + 4 * 2 * MMT_MAX_STREAMS * 32 * 8];
+  const AttnProblem& P = batch.p[blockIdx.z];
+  const int nt = (T + 31) / 32;
+  const int nqb = (nt + 7) / 8;
+  const int ns = P.nstreams;
+  const int BH = gridDim.x / nqb;
+  const int qb = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (last) query block first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int qt[2] = {8 * qb + w, 8 * qb + 7 - w};
+  const bool live[2] = {qt[0] < nt, qt[1] < nt};
+  const int tq[2] = {qt[0] * 32 + r, qt[1] * 32 + r};
+  const bool okq[2] = {live[0] && tq[0] < T, live[1] && tq[1] < T};
+  const int nk = min(8 * qb + 8, nt);  // key tiles walked per stream
+  const int nsl = ns * nk;             // slices
+  const int64_t rowbase = (int64_t)b * T;
+  const float c2 = scale * kLog2e2;
+
+  // Q, dO of both query tiles (queries on lanes: the B operands of S^T and dP^T); per stream
+  // D_j = rowsum(dO * O_j) (written for the dK/dV pass) and the LSE into the LDS table
+  bf16x8 qf[2][NKS], dof[2][NKS];
+  float* tab = reinterpret_cast<float*>(lds + TAB) + w * (2 * MMT_MAX_STREAMS * 64);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    u32x4 qr[NKS], dr[NKS];
+    const bf16_t* qp = P.q + (rowbase + tq[u]) * P.q_ld + head * 64;
+    const bf16_t* dp = P.dout + (rowbase + tq[u]) * P.dout_ld + head * 64;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      qr[s] = okq[u] ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * h) : z;
+      dr[s] = okq[u] ? *reinterpret_cast<const u32x4*>(dp + 16 * s + 8 * h) : z;
+    }
+    for (int j = 0; j < ns; ++j) {
+      const bf16_t* oj = (ns > 1 ? P.oj[j] : P.o) + (rowbase + tq[u]) * P.o_ld + head * 64;
+      float d = 0.f;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const u32x4 ov = okq[u] ? *reinterpret_cast<const u32x4*>(oj + 16 * s + 8 * h) : z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          d += bf2f(ov[e] & 0xffff) * bf2f(dr[s][e] & 0xffff);
+          d += bf2f(ov[e] >> 16) * bf2f(dr[s][e] >> 16);
+        }
+      }
+      d += __shfl_xor(d, 32, 64);
+      const float l2 = okq[u] ? P.lse[j][(int64_t)bh * T + tq[u]] : 0.f;
+      if (h == 0) {
+        if (okq[u]) P.dvec[j][(int64_t)bh * T + tq[u]] = d;
+        tab[(u * MMT_MAX_STREAMS + j) * 64 + 2 * r] = l2;
+        tab[(u * MMT_MAX_STREAMS + j) * 64 + 2 * r + 1] = d;
+      }
+    }
+    // consumed here: the compiler's wait for these loads sits before the DMA prologue
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      asm volatile("" : "+v"(qr[s]));
+      asm volatile("" : "+v"(dr[s]));
+      qf[u][s] = __builtin_bit_cast(bf16x8, qr[s]);
+      dof[u][s] = __builtin_bit_cast(bf16x8, dr[s]);
+    }
+  }
+  f32x16 dq[2][ND];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) zero16(dq[u][dt]);
+
+  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+  const int64_t ntiles = (int64_t)BH * ntri;
+  const int prow = lane >> 1;
+  const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
+  const int per = 2 + (DROP && w == 0 ? 1 : 0);
+  auto issue = [&](int slot, int sl) {
+    char* sb = lds + slot * SLOT;
+    const int j = sl / nk, kt = sl % nk;
+    const int grow = kt * 32 + prow;
+    const i32x4 rk = make_rsrc(P.k[j] + head * P.kv_hstride, (rowbase + T) * (int64_t)P.kv_ld * 2);
+    const i32x4 rv = make_rsrc(P.v[j] + head * P.kv_hstride, (rowbase + T) * (int64_t)P.kv_ld * 2);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int piece = 2 * w + u;  // 0..3: K column block, 4..7: V
+      const int op = piece >> 2, cb = piece & 3;
+      const int voff = grow < T ? ((int)(rowbase + grow) * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
+      dma16(op ? rv : rk, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_V + cb * SUB)), voff);
+    }
+    if (DROP && w == 0) {  // lane words of (query tile 8 qb + u, key tile kt), u = 0..7: 8 x 128 B
+      const i32x4 rm = make_rsrc(P.dmask[j], ntiles * 2 * 32 * 4);
+      const int u = lane >> 3, q_ = 8 * qb + u;
+      const int64_t t = (int64_t)bh * ntri + (int64_t)q_ * (q_ + 1) / 2 + kt;
+      const int voff = (q_ < nt && kt <= q_) ? (int)((ntiles + t) * 128 + (lane & 7) * 16) : OOB;
+      dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nsl) issue(i, i);
+
+  const int o_row = img_off(r, 0, h);
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int o_tr0 = img_off(4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
+  const int o_tr1 = img_off(8 + 4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
+  const float dsc = DROP ? P.drop_scale : 1.f;
+  // one key tile against query tile u of this wave, on the slice's fragments (masked: the diagonal)
+  auto tile = [&](const char* sb, int u, int j, int kt, const bf16x8 (&kf)[NKS], const bf16x8 (&vf)[NKS],
+                  const bf16x8 (&ktr)[2][ND], bool masked) {
+    const int ut = u == 0 ? w : 7 - w;  // the tile's index in the block (keep-bit record)
+    const uint32_t mw = DROP ? reinterpret_cast<const uint16_t*>(sb + OFF_M)[ut * 64 + lane] : 0u;
+    const float l2 = tab[(u * MMT_MAX_STREAMS + j) * 64 + 2 * r], dsum = tab[(u * MMT_MAX_STREAMS + j) * 64 + 2 * r + 1];
+    f32x16 sa, pa;
+    zero16(sa);
+    zero16(pa);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      sa = mfma32(kf[s], qf[u][s], sa);   // S^T[key][q]
+      pa = mfma32(vf[s], dof[u][s], pa);  // dP^T[key][q]
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[e], c2, -l2));
+      float dp = pa[e];
+      if (DROP) dp = keep_f(dp, __builtin_amdgcn_sbfe((int)mw, (e & 1) * 8 + (e >> 1), 1));
+      sa[e] = pv * __builtin_fmaf(dp, dsc, -dsum);  // dS^T
+    }
+    if (masked) {  // keys above the query (and past T) contribute nothing
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int key = kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (key > tq[u] || key >= T) sa[e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const u32x4 v = {pack2bf(sa[8 * s], sa[8 * s + 1]), pack2bf(sa[8 * s + 2], sa[8 * s + 3]),
+                       pack2bf(sa[8 * s + 4], sa[8 * s + 5]), pack2bf(sa[8 * s + 6], sa[8 * s + 7])};
+      const bf16x8 df = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) dq[u][dt] = mfma32(ktr[s][dt], df, dq[u][dt]);
+    }
+  };
+#pragma unroll 1
+  for (int i = 0; i < nsl; ++i) {
+    wait_vm(per * min(S - 2, nsl - 1 - i));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (i + S - 1 < nsl) issue((i + S - 1) % S, i + S - 1);
+    const int j = i / nk, kt = i % nk;
+    const bool needB = live[1] && kt <= qt[1];  // qt[0] < qt[1]: A needs the slice only if B does
+    if (needB) {
+      const char* sb = lds + (i % S) * SLOT;
+      bf16x8 kf[NKS], vf[NKS], ktr[2][ND];
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        kf[s] = *reinterpret_cast<const bf16x8*>(sb + o_row + s * SUB);
+        vf[s] = *reinterpret_cast<const bf16x8*>(sb + OFF_V + o_row + s * SUB);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+          ktr[s][dt] = join4(lds_tr16(sb + o_tr0 + 512 * s + 2 * SUB * dt), lds_tr16(sb + o_tr1 + 512 * s + 2 * SUB * dt));
+      if (live[0] && kt <= qt[0]) tile(sb, 0, j, kt, kf, vf, ktr, kt == qt[0]);
+      tile(sb, 1, j, kt, kf, vf, ktr, kt == qt[1]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int ga = 2 * pr, gb = 2 * pr + 1;
+        const uint32_t x0 = pack2bf(dq[u][dt][4 * ga] * scale, dq[u][dt][4 * ga + 1] * scale);
+        const uint32_t x1 = pack2bf(dq[u][dt][4 * ga + 2] * scale, dq[u][dt][4 * ga + 3] * scale);
+        const uint32_t y0 = pack2bf(dq[u][dt][4 * gb] * scale, dq[u][dt][4 * gb + 1] * scale);
+        const uint32_t y1 = pack2bf(dq[u][dt][4 * gb + 2] * scale, dq[u][dt][4 * gb + 3] * scale);
+        const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        const int d0 = dt * 32 + 16 * pr + 8 * h;
+        if (okq[u])
+          *reinterpret_cast<u32x4*>(P.dq + (rowbase + tq[u]) * P.dq_ld + head * 64 + d0) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+      }
+}
+
 // ring depth knob (slots; S - 1 slices in flight): MMT_ATTN_RING_SLOTS = 4 (default) or 6
 static int ring_slots() {
   static const int v = [] {
@@ -532,11 +734,23 @@ static int ring_slots() {
   return v;
 }
 
+// dQ ring variant: MMT_ATTN_DQ_X2 = 1 (default) two query tiles per wave, 0 one
+static const int g_dq_x2 = [] {
+  const char* e = getenv("MMT_ATTN_DQ_X2");
+  return e ? atoi(e) : 1;
+}();
+
 hipError_t mmt_attn_bwd_dq_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, hipStream_t s) {
   const int nt = (T + 31) / 32;
   const int nqb = (nt + 3) / 4;
   const dim3 grid(nqb * B * H, 1, bt.count);
   const bool deep = ring_slots() >= 6;
+  if (g_dq_x2) {  // two query tiles per wave (8 per workgroup)
+    const dim3 g2(((nt + 7) / 8) * B * H, 1, bt.count);
+    if (drop) hipLaunchKernelGGL((attn_bwd_dq_ring64x2<true, 4>), g2, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dq_ring64x2<false, 4>), g2, dim3(256), 0, s, bt, T, H, scale);
+    return hipGetLastError();
+  }
   if (drop) {
     if (deep) hipLaunchKernelGGL((attn_bwd_dq_ring64<true, 6>), grid, dim3(256), 0, s, bt, T, H, scale);
     else hipLaunchKernelGGL((attn_bwd_dq_ring64<true, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
