@@ -1152,7 +1152,7 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
 // mmt_attn_set_ring() for in-process A/B
 static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 3;  // both hs-64 passes on the rings (dQ: two query tiles per wave)
 }();
 extern "C" int mmt_attn_set_ring(int v) {
   const int old = g_attn_ring;

@@ -688,8 +688,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
     __builtin_amdgcn_s_barrier();
     if (i + S - 1 < nsl) issue((i + S - 1) % S, i + S - 1);
     const int j = i / nk, kt = i % nk;
-    const bool needB = live[1] && kt <= qt[1];  // qt[0] < qt[1]: A needs the slice only if B does
-    if (needB) {
+    // tile B (the later one) may lie past the sequence's last tile while A does not
+    const bool needA = live[0] && kt <= qt[0], needB = live[1] && kt <= qt[1];
+    if (needA || needB) {
       const char* sb = lds + (i % S) * SLOT;
       bf16x8 kf[NKS], vf[NKS], ktr[2][ND];
 #pragma unroll
@@ -702,8 +703,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt)
           ktr[s][dt] = join4(lds_tr16(sb + o_tr0 + 512 * s + 2 * SUB * dt), lds_tr16(sb + o_tr1 + 512 * s + 2 * SUB * dt));
-      if (live[0] && kt <= qt[0]) tile(sb, 0, j, kt, kf, vf, ktr, kt == qt[0]);
-      tile(sb, 1, j, kt, kf, vf, ktr, kt == qt[1]);
+      if (needA) tile(sb, 0, j, kt, kf, vf, ktr, kt == qt[0]);
+      if (needB) tile(sb, 1, j, kt, kf, vf, ktr, kt == qt[1]);
     }
   }
 #pragma unroll
