@@ -1148,7 +1148,7 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
 }
 
 // attention variant knob (bit 0: the slice-streamed hs-64 dK/dV pass, bit 1: its dQ pass, bit 2: the
-// dK/dV pass at 3 waves per SIMD): MMT_ATTN_RING, or
+// dK/dV pass at 3 waves per SIMD, bits 3 / 4: its 8 / 4 key tiles per workgroup at every T): MMT_ATTN_RING, or
 // mmt_attn_set_ring() for in-process A/B
 static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
@@ -1179,7 +1179,7 @@ static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, b
     else if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, true>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, false>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
     if (HS == 64 && (g_attn_ring & 1)) {
-      (void)mmt_attn_bwd_dkdv_ring64(bt, B, T, H, scale, drop, (g_attn_ring & 4) != 0, s);
+      (void)mmt_attn_bwd_dkdv_ring64(bt, B, T, H, scale, drop, g_attn_ring, s);
       return;
     }
     // dK/dV: the paired walk needs 4 accumulator sets (1 wave per SIMD); the single-tile kernel

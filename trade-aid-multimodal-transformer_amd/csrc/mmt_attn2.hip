@@ -91,26 +91,28 @@ __device__ __forceinline__ int key_dword(int r) { return 2 * ((r & 3) + 4 * (r >
 
 // =============================================================================================
 // dK, dV at hs 64. grid (nkb * B*H * nstreams, 1, problems), nkb = ceil(nt / 4): a workgroup owns
-// 4 key tiles (wave w: key tile 4 kb + w, its K / V in registers, dK / dV accumulated in
-// registers) and walks the query tiles kb*4 .. nt-1 in lockstep; each query slice (Q, dO, the
+// NWV = 4 or 8 key tiles (wave w: key tile NWV kb + w, its K / V in registers, dK / dV accumulated
+// in registers) and walks the query tiles NWV kb .. nt-1 in lockstep; each query slice (Q, dO, the
 // row's LSE and D, the slice's keep bits) arrives in an LDS ring slot by LDS-DMA. Per query tile a
 // wave whose key tile is not above it computes S = Q K^T and dP = dO V^T (keys on lanes),
 // P = exp2(c2 S - LSE2), dS = P (Z dP - D), dV += (Z P)^T dO, dK += dS^T Q.
-// Workgroups are ordered heaviest key block first (the causal walk of key block kb is nt - 4 kb
+// Workgroups are ordered heaviest key block first (the causal walk of key block kb is nt - NWV kb
 // slices long) so the launch does not end on a tail of long blocks.
 // =============================================================================================
-template <bool DROP, int OCC, int S>
-__global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch, int T, int H, float scale) {
+template <bool DROP, int OCC, int S, int NWV>
+__global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch, int T, int H, float scale) {
   constexpr int NKS = 4, ND = 2;  // hs 64: 4 k-steps of 16, 2 output tiles of 32
   static_assert(S >= 3 && 4 * (S - 2) <= 16, "ring slots: S - 1 slices in flight, counted waits <= 16");
   constexpr int OFF_DO = IMG64, OFF_L = 2 * IMG64, OFF_D = OFF_L + 256, OFF_M = OFF_D + 256;
   constexpr int SLOT = OFF_M + (DROP ? 1024 : 0);
   constexpr int EPW = 40;  // epilogue transpose slot row stride (bf16)
-  static_assert(S * SLOT >= 4 * 2 * 32 * EPW * 2, "epilogue slots alias the ring");
-  __shared__ __attribute__((aligned(1024))) char lds[S * SLOT];
+  static_assert(NWV == 4 || NWV == 8, "4 or 8 key tiles (waves) per workgroup");
+  constexpr int PPW = 8 / NWV;  // Q / dO sub-image pieces per wave per slice
+  constexpr int EPI_BYTES = NWV * 2 * 32 * EPW * 2;  // per-wave epilogue transpose slots (alias the ring)
+  __shared__ __attribute__((aligned(1024))) char lds[S * SLOT > EPI_BYTES ? S * SLOT : EPI_BYTES];
   const AttnProblem& P = batch.p[blockIdx.z];
   const int nt = (T + 31) / 32;
-  const int nkb = (nt + 3) / 4;
+  const int nkb = (nt + NWV - 1) / NWV;
   const int ns = P.nstreams;
   const int nbhs = gridDim.x / nkb;  // B*H*nstreams
   const int BH = nbhs / ns;
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch
   const int b = bh / H, head = bh % H;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const int kt0 = kb * 4;
+  const int kt0 = kb * NWV;
   const int kt = kt0 + w;
   const bool live = kt < nt;
   const int tk = kt * 32 + r;
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch
   const i32x4 rm = make_rsrc(DROP ? P.dmask[j] + (int64_t)bh * ntri * 32 : P.dmask[0], ntri * 32 * 4);
   // pieces this wave issues per slice: 2 sub-images (+ LSE for wave 0, D for wave 1, the keep bits
   // for wave 2); the counted waits below count them
-  const int per = 2 + (w < 2 ? 1 : 0) + (DROP && w == 2 ? 1 : 0);
+  const int per = PPW + (w < 2 ? 1 : 0) + (DROP && w == 2 ? 1 : 0);
   // per-lane source of a sub-image piece: row L/2, half L&1 (swapped on rows with bit 3 set)
   const int prow = lane >> 1;
   const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
@@ -175,8 +177,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch
     const int q0 = qt * 32;
     const int grow = q0 + prow;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int piece = 2 * w + u;  // 0..3: Q column block w (two per wave), 4..7: dO
+    for (int u = 0; u < PPW; ++u) {
+      const int piece = PPW * w + u;  // 0..3: Q column blocks, 4..7: dO
       const int op = piece >> 2, cb = piece & 3;
       const int ld = op ? P.dout_ld : P.q_ld;
       const int voff = grow < T ? ((int)(rowbase + grow) * ld + cb * 16 + pcol) * 2 : OOB;
@@ -186,8 +188,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch
       const int voff = (lane < 32 && q0 + lane < T) ? (q0 + lane) * 4 : OOB;
       dma4(w == 0 ? rl : rd, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_L + w * 256)), voff);
     }
-    if (DROP && w == 2) {  // 4 key tiles x 128 B of the key-major records of (qt, kt0..kt0+3)
-      const int voff = lane < 32 ? (int)(((int64_t)qt * (qt + 1) / 2 + kt0) * 128 + lane * 16) : OOB;
+    if (DROP && w == 2) {  // NWV key tiles x 128 B of the key-major records of (qt, kt0..kt0+NWV-1)
+      const int voff = lane < 8 * NWV ? (int)(((int64_t)qt * (qt + 1) / 2 + kt0) * 128 + lane * 16) : OOB;
       dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
     }
   };
@@ -286,7 +288,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch
     const int qt = kt0 + i;
     if (live && qt >= kt) tile(lds + (i % S) * SLOT, qt, mc);
   };
-  const int n_diag = min(4, nq);
+  const int n_diag = min(NWV, nq);
   const int n_plain_end = (ragged && nq > 4) ? nq - 1 : nq;
   int i = 0;
 #pragma unroll 1
@@ -762,23 +764,44 @@ hipError_t mmt_attn_bwd_dq_ring64(const AttnBatch& bt, int B, int T, int H, floa
   return hipGetLastError();
 }
 
-template <int S>
+template <int S, int NWV>
 static void dkdv_launch(const AttnBatch& bt, dim3 grid, int T, int H, float scale, bool drop, bool occ3, hipStream_t s) {
+  const dim3 blk(64 * NWV);
   if (occ3) {  // 3 waves per SIMD (<= 168 VGPRs)
-    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 3, S>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 3, S>), grid, dim3(256), 0, s, bt, T, H, scale);
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 3, S, NWV>), grid, blk, 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 3, S, NWV>), grid, blk, 0, s, bt, T, H, scale);
   } else {
-    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2, S>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2, S>), grid, dim3(256), 0, s, bt, T, H, scale);
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2, S, NWV>), grid, blk, 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2, S, NWV>), grid, blk, 0, s, bt, T, H, scale);
   }
 }
 
-hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, bool occ3,
+// key tiles per dK/dV workgroup: MMT_ATTN_DKDV_WAVES = 4 or 8 (8: half the query-slice DMA and L2
+// traffic per key, longer diagonal ramp); default 4: 8 measured slower (C3 cross-attention backward
+// 2483 -> 2709 us, C4 2270 -> 2364 us, C3 step +1.5 %: profiles/r3h_dkdv_waves_ab.txt); kept as a knob
+// (MMT_ATTN_DKDV8_TMIN: 8 from that T on)
+static int dkdv_waves(int T) {
+  static const int env = [] {
+    const char* e = getenv("MMT_ATTN_DKDV_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  static const int tmin = [] {
+    const char* e = getenv("MMT_ATTN_DKDV8_TMIN");
+    return e ? atoi(e) : (1 << 30);
+  }();
+  if (env == 4 || env == 8) return env;
+  return T >= tmin ? 8 : 4;
+}
+
+hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, int variant,
                                     hipStream_t s) {
   const int nt = (T + 31) / 32;
-  const int nkb = (nt + 3) / 4;
+  const bool occ3 = (variant & 4) != 0;
+  const int nwv = (variant & 8) ? 8 : (variant & 16) ? 4 : dkdv_waves(T);
+  const int nkb = (nt + nwv - 1) / nwv;
   const dim3 grid(nkb * B * H * bt.p[0].nstreams, 1, bt.count);
-  if (ring_slots() >= 6) dkdv_launch<6>(bt, grid, T, H, scale, drop, occ3, s);
-  else dkdv_launch<4>(bt, grid, T, H, scale, drop, occ3, s);
+  if (nwv == 8) dkdv_launch<4, 8>(bt, grid, T, H, scale, drop, occ3, s);
+  else if (ring_slots() >= 6) dkdv_launch<6, 4>(bt, grid, T, H, scale, drop, occ3, s);
+  else dkdv_launch<4, 4>(bt, grid, T, H, scale, drop, occ3, s);
   return hipGetLastError();
 }

@@ -43,6 +43,9 @@ using TileL = TileCfg<2, 4, 4, 2>;
 // 128 x 512, 8 waves (1 x 8) of 128 x 64 (TileL's per-wave shape): whole 512-wide rows per block for
 // the fused LayerNorm-backward epilogue at C = 512 (BK 32 x 2 stages = 80 KiB of ring)
 using TileW = TileCfg<1, 8, 4, 2>;
+// 128 x 256, 4 waves (1 x 4) of 128 x 64: whole 256-wide rows at twice the blocks of TileL, two
+// blocks per CU, so one block's LayerNorm epilogue (HBM-bound) overlaps another's K loop
+using TileH = TileCfg<1, 4, 4, 2>;
 
 // tuning knob (mmt_gemm_set_variant): pipeline variant of the forward / backward-data GEMMs in
 // bits 0-3 and of the weight-grad (split-K, atomic) GEMMs in bits 4-7:
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
 
   // one LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads):
   // the stage ring during the K loop, the fp32 output tile (EPI_ROWS x (GBN + 4)) in the epilogue
-  constexpr int EPI_ROWS = GBN >= 512 ? 32 : (GBM == 128 && MINB == 1) ? 128 : 64;
+  constexpr int EPI_ROWS = (GBN >= 512 || (GBM == 128 && GBN == 256)) ? 32 : (GBM == 128 && MINB == 1) ? 128 : 64;
   constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
   constexpr int LDS_MAIN = RING > CTILE ? RING : CTILE;
   __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN];
@@ -1019,6 +1022,12 @@ bool mmt_gemm_ln_bwd_ok(const GemmBatch& b) {
   return true;
 }
 
+// tile of the fused LayerNorm backward at C = 256: MMT_LNB_TILE = 1 (default) 128 x 256, 0 256 x 256
+static const int g_lnb_tile = [] {
+  const char* e = getenv("MMT_LNB_TILE");
+  return e ? atoi(e) : 1;
+}();
+
 hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
   if (!mmt_gemm_ln_bwd_ok(b)) return hipErrorInvalidValue;
   // a tile as wide as the row, whatever K: its block owns whole rows of the LayerNorm (C = 256:
@@ -1027,10 +1036,14 @@ hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
     const int mt = max_tiles<TileW>(b, nullptr);
     if (mt == 0) return hipSuccess;
     launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
-  } else {
+  } else if (g_lnb_tile == 0) {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
     launch_v<TileL, 64, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+  } else {
+    const int mt = max_tiles<TileH>(b, nullptr);
+    if (mt == 0) return hipSuccess;
+    launch_v<TileH, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
   }
   return hipGetLastError();
 }
