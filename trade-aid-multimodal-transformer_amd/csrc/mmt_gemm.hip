@@ -1022,10 +1022,12 @@ bool mmt_gemm_ln_bwd_ok(const GemmBatch& b) {
   return true;
 }
 
-// tile of the fused LayerNorm backward at C = 256: MMT_LNB_TILE = 1 (default) 128 x 256, 0 256 x 256
+// tile of the fused LayerNorm backward at C = 256: MMT_LNB_TILE = 0 (default) 256 x 256, 1 128 x 256
+// (twice the blocks, two per CU: measured slower, C1 4-problem launches 63.7 -> 92.9 us, step
+// 9.11 -> 9.29 ms: profiles/r3i_lnb_tile_ab.txt)
 static const int g_lnb_tile = [] {
   const char* e = getenv("MMT_LNB_TILE");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }();
 
 hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
