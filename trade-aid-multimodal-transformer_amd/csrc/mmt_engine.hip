@@ -1512,8 +1512,24 @@ void ensure_side(mmt_ctx* c) {
   // MMT_SIDE_PRIORITY (optional): HIP stream priority of the side stream (lower = higher priority,
   // clamped to the device's range); unset = default priority
   static const char* prio_env = getenv("MMT_SIDE_PRIORITY");
+  // MMT_SIDE_CUS (optional): confine the side stream to N of the device's CUs (a CU mask spread evenly
+  // over the XCDs whether the mask bits map to CUs XCD-major or round-robin), so the weight gradients
+  // and keep-bit hashing never take more than N CUs from the main stream's chain
+  static const int side_cus = [] {
+    const char* e = getenv("MMT_SIDE_CUS");
+    return e ? atoi(e) : 0;
+  }();
   hipError_t ce;
-  if (prio_env) {
+  int ncu = 0;
+  if (side_cus > 0) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (side_cus > 0 && ncu > 0 && side_cus < ncu && ncu % 8 == 0) {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    const int stride = std::max(1, ncu / side_cus);
+    int set = 0;
+    for (int i = 0; i < ncu && set < side_cus; ++i)
+      if (((i % 8) + (i / 8)) % stride == 0) { mask[i / 32] |= 1u << (i % 32); ++set; }
+    ce = hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data());
+  } else if (prio_env) {
     int least = 0, greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
     const int pr = std::max(greatest, std::min(least, atoi(prio_env)));
