@@ -1037,7 +1037,13 @@ hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
   if (b.p[0].N == TileW::BN) {
     const int mt = max_tiles<TileW>(b, nullptr);
     if (mt == 0) return hipSuccess;
-    launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+    // K-step: 32 (80 KiB ring) or, MMT_LNB_W_BK=64, 64 (the whole 160 KiB of LDS, half the barriers)
+    static const int bk = [] {
+      const char* e = getenv("MMT_LNB_W_BK");
+      return e ? atoi(e) : 32;
+    }();
+    if (bk == 64) launch_v<TileW, 64, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+    else launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
   } else if (g_lnb_tile == 0) {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
