@@ -676,6 +676,20 @@ struct Runner {
     gemm(dx, true, false, EPI_STORE_F32, 1, gname);
     ok(mmt_launch_ln_bwd(lb, R, C, s), lname);
   }
+  // forward residual GEMM with the next LayerNorm's forward fused (mmt_launch_gemm_resid_ln)
+  bool gemm_resid_ln(const GemmBatch& b, const char* what) {
+    if (rc != MMT_OK || !mmt_gemm_resid_ln_ok(b)) return false;
+    const int id = probe_begin(what, s);
+    ok(mmt_launch_gemm_resid_ln(b, s), what);
+    if (id >= 0) {
+      double fl = 0, by = 0;
+      gemm_cost(b, EPI_BIAS_RESID_F32, &fl, &by);
+      for (int g = 0; g < b.count; ++g)
+        if (b.p[g].lnf_y) by += (double)b.p[g].M * b.p[g].N * 2.0 + b.p[g].M * 8.0;
+      probe_end(id, s, fl, by);
+    }
+    return true;
+  }
   void gemm(const GemmBatch& b, bool akc, bool bkc, int epi, int splits, const char* what) {
     if (rc != MMT_OK) return;
     const int id = probe_begin(what, s);
@@ -826,19 +840,33 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   }
   std::vector<const float*> xin(M);
   for (int i = 0; i < M; ++i) xin[i] = r.W<float>(p.xemb[i]);
+  // LayerNorm forwards already done by the previous residual GEMM's epilogue (lnf_fused: the post
+  // block's); fused only in bf16 at C == 256 (whole rows per 256x256 tile), MMT_LN_FUSE=0 or
+  // MMT_LN_FUSE_FWD=0 disables
+  static const bool ln_fuse = [] {
+    const char* e = getenv("MMT_LN_FUSE");
+    const char* f = getenv("MMT_LN_FUSE_FWD");
+    return (e ? atoi(e) != 0 : true) && (f ? atoi(f) != 0 : true);
+  }();
+  const bool fuse_fwd = ln_fuse && !f8 && C == 256;
+  std::vector<char> ln1_done(M, 0), lnf_done(M, 0);
   for (int l = 0; l < c->L && r.rc == MMT_OK; ++l) {
     const LM* x = &c->lm[(size_t)l * M];
     const ActLM* a = &p.act[(size_t)l * M];
     // attention dropout keep bits: layer 0's made on the side stream while the first LayerNorm and
     // Q/K/V GEMMs run, all later layers' while layer 0 computes (two forks, two joins per forward)
     if (r.drop && l == 0) gen_masks(0);
-    LnBatch lb{}; lb.count = M;
+    LnBatch lb{}; lb.count = 0;
     for (int i = 0; i < M; ++i) {
-      lb.p[i].x = xin[i]; lb.p[i].gamma = r.P(x[i].ln1w); lb.p[i].beta = r.P(x[i].ln1b);
-      lb.p[i].y = r.W<bf16_t>(a[i].a); lb.p[i].mean = r.W<float>(a[i].mean1); lb.p[i].rstd = r.W<float>(a[i].rstd1);
-      ln8(lb.p[i], a[i].a8, a[i].as8);
+      if (ln1_done[i]) continue;
+      LnProblem& q = lb.p[lb.count++];
+      q.x = xin[i]; q.gamma = r.P(x[i].ln1w); q.beta = r.P(x[i].ln1b);
+      q.y = r.W<bf16_t>(a[i].a); q.mean = r.W<float>(a[i].mean1); q.rstd = r.W<float>(a[i].rstd1);
+      ln8(q, a[i].a8, a[i].as8);
     }
-    r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "ln1_fwd");
+    if (lb.count) r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "ln1_fwd");
+    std::fill(ln1_done.begin(), ln1_done.end(), 0);
+    lb.count = M;
     GemmBatch g{}; g.count = M;
     for (int i = 0; i < M; ++i) {
       g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].a8), C, r.W<uint8_t>(a[i].as8), ldsC, w8, x[i].W1, R)
@@ -901,8 +929,41 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       if (c->any_cross) { g.p[i].o16 = r.W<bf16_t>(a[i].x2h); g.p[i].ldo16 = C; }
       r.set_drop(g.p[i], l, i, DS_FFN);
     }
-    if (f8) r.gemm8(g, EPI_BIAS_RESID_F32, "ffn2");
-    else r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "ffn2");
+    bool lnc_done = false;
+    if (fuse_fwd) {
+      // the LayerNorm that reads each problem's x2 next: lnc (cross-attention query side), else the
+      // next layer's ln1, else (last layer) the post block's
+      for (int i = 0; i < M; ++i) {
+        GemmProblem& q = g.p[i];
+        if (c->any_cross && x[i].cross) {
+          q.lnf_gamma = r.P(x[i].lncw); q.lnf_beta = r.P(x[i].lncb); q.lnf_y = r.W<bf16_t>(a[i].d);
+          q.lnf_mean = r.W<float>(a[i].meanc); q.lnf_rstd = r.W<float>(a[i].rstdc);
+        } else if (l + 1 < c->L) {
+          const LM& xn = c->lm[(size_t)(l + 1) * M + i];
+          const ActLM& an = p.act[(size_t)(l + 1) * M + i];
+          q.lnf_gamma = r.P(xn.ln1w); q.lnf_beta = r.P(xn.ln1b); q.lnf_y = r.W<bf16_t>(an.a);
+          q.lnf_mean = r.W<float>(an.mean1); q.lnf_rstd = r.W<float>(an.rstd1);
+        } else {
+          q.lnf_gamma = r.P(c->post[i].lnw); q.lnf_beta = r.P(c->post[i].lnb); q.lnf_y = r.W<bf16_t>(p.lnf16[i]);
+          q.lnf_mean = r.W<float>(p.meanf[i]); q.lnf_rstd = r.W<float>(p.rstdf[i]);
+        }
+      }
+      if (r.gemm_resid_ln(g, "ffn2")) {
+        for (int i = 0; i < M; ++i) {
+          if (c->any_cross && x[i].cross) lnc_done = true;
+          else if (l + 1 < c->L) ln1_done[i] = 1;
+          else lnf_done[i] = 1;
+        }
+      } else {
+        for (int i = 0; i < M; ++i) g.p[i].lnf_y = nullptr;
+        r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "ffn2");
+      }
+    } else if (f8) {
+      r.gemm8(g, EPI_BIAS_RESID_F32, "ffn2");
+    } else {
+      r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "ffn2");
+    }
+    for (int i = 0; i < M; ++i) g.p[i].lnf_y = nullptr;  // g is reused: no stale LayerNorm outputs
     std::vector<const float*> xout(M);
     for (int i = 0; i < M; ++i) xout[i] = r.W<float>(a[i].x2);
     if (c->any_cross) {
@@ -919,7 +980,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
                      : gp_fwd(r.W<bf16_t>(a[i].d), C, wpk, x[i].Wq, R);
         gq.p[u].o16 = r.W<bf16_t>(a[i].qc); gq.p[u].ldo16 = C;
       }
-      r.ok(mmt_launch_ln_fwd(lc, R, C, r.s), "lnc_fwd");
+      if (!lnc_done) r.ok(mmt_launch_ln_fwd(lc, R, C, r.s), "lnc_fwd");
       if (f8) r.gemm8(gq, EPI_STORE_BF16, "ca_q");
       else r.gemm(gq, true, true, EPI_STORE_BF16, 1, "ca_q");
       // KV projections of the other modalities' post-FFN states, grouped up to 8 per launch
@@ -969,12 +1030,15 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   }
   if (r.rc != MMT_OK) return r.rc;
   // post block + CE
-  LnBatch lf{}; lf.count = M;
+  LnBatch lf{}; lf.count = 0;
   GemmBatch h0{}; h0.count = M;
   GemmBatch h2{}; h2.count = M;
   for (int i = 0; i < M; ++i) {
-    lf.p[i].x = xin[i]; lf.p[i].gamma = r.P(c->post[i].lnw); lf.p[i].beta = r.P(c->post[i].lnb);
-    lf.p[i].y = r.W<bf16_t>(p.lnf16[i]); lf.p[i].mean = r.W<float>(p.meanf[i]); lf.p[i].rstd = r.W<float>(p.rstdf[i]);
+    if (!lnf_done[i]) {
+      LnProblem& q = lf.p[lf.count++];
+      q.x = xin[i]; q.gamma = r.P(c->post[i].lnw); q.beta = r.P(c->post[i].lnb);
+      q.y = r.W<bf16_t>(p.lnf16[i]); q.mean = r.W<float>(p.meanf[i]); q.rstd = r.W<float>(p.rstdf[i]);
+    }
     h0.p[i] = gp_fwd(r.W<bf16_t>(p.lnf16[i]), C, wpk, c->post[i].H0, R);
     h0.p[i].bias = r.P(c->post[i].b0); h0.p[i].o16 = r.W<bf16_t>(p.hh[i]); h0.p[i].ldo16 = c->ldvh[i];
     h2.p[i] = gp_fwd(r.W<bf16_t>(p.hh[i]), c->ldvh[i], wpk, c->post[i].H2, R);
@@ -984,7 +1048,12 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
     lf.zero_f = losses; lf.nzero_f = M;
     lf.zero_i = r.W<int>(p.flag); lf.nzero_i = 1;
   }
-  r.ok(mmt_launch_ln_fwd(lf, R, C, r.s), "lnf_fwd");
+  if (lf.count) {
+    r.ok(mmt_launch_ln_fwd(lf, R, C, r.s), "lnf_fwd");
+  } else if (tgt) {  // every post-block LayerNorm was fused: zero the accumulators here
+    r.ok(hipMemsetAsync(losses, 0, sizeof(float) * M, r.s), "memset losses");
+    r.ok(hipMemsetAsync(r.W<int>(p.flag), 0, sizeof(int), r.s), "memset flag");
+  }
   r.gemm(h0, true, true, EPI_BIAS_TANH_BF16, 1, "head0");
   r.gemm(h2, true, true, EPI_STORE_F32, 1, "head2");
   if (tgt && r.rc == MMT_OK) {

@@ -415,6 +415,36 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
           if (EPI == EPI_BIAS_RESID_F32 && P.o16)
             *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
                 u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+          if (EPI == EPI_BIAS_RESID_F32 && GBN == 256 && P.lnf_y) {
+            // the next LayerNorm on this row (whole rows per block: N == GBN, mmt_launch_gemm_resid_ln;
+            // lnf_y is uniform per problem and m < M per half wave, so every lane of the row's half
+            // wave takes the shuffles): mean, then the centred sum of squares (as ln_fwd_kernel)
+            float sm = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sm += r[e];
+#pragma unroll
+            for (int o = 1; o < TPR; o <<= 1) sm += __shfl_xor(sm, o, 64);
+            const float mean = sm * (1.0f / (float)GBN);
+            float q = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q += (r[e] - mean) * (r[e] - mean);
+#pragma unroll
+            for (int o = 1; o < TPR; o <<= 1) q += __shfl_xor(q, o, 64);
+            const float rstd = rsqrtf(q * (1.0f / (float)GBN) + 1e-5f);
+            const f32x4 g0 = *reinterpret_cast<const f32x4*>(P.lnf_gamma + n);
+            const f32x4 g1 = *reinterpret_cast<const f32x4*>(P.lnf_gamma + n + 4);
+            const f32x4 b0 = *reinterpret_cast<const f32x4*>(P.lnf_beta + n);
+            const f32x4 b1 = *reinterpret_cast<const f32x4*>(P.lnf_beta + n + 4);
+            float y[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              y[e] = (r[e] - mean) * rstd * g0[e] + b0[e];
+              y[e + 4] = (r[e + 4] - mean) * rstd * g1[e] + b1[e];
+            }
+            *reinterpret_cast<u32x4*>(P.lnf_y + (int64_t)m * N + n) =
+                u32x4{pack2bf(y[0], y[1]), pack2bf(y[2], y[3]), pack2bf(y[4], y[5]), pack2bf(y[6], y[7])};
+            if (c8 == 0) { P.lnf_mean[m] = mean; P.lnf_rstd[m] = rstd; }
+          }
         } else {
           *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
               u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
@@ -491,16 +521,30 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   constexpr int STAGE_BYTES = IMG_A + IMG_B;
   constexpr int PIECES = (GBM + GBN) * BK / 512 / NW;        // LDS-DMA pieces per wave per stage (A + B)
   constexpr int AI = SWAP ? TN : TM, AJ = SWAP ? TM : TN;    // accumulator sub-tile grid
-  const GemmProblem& P = batch.p[blockIdx.z];
+  // XCD-aware remap (bijective): blocks b and b+8 share an XCD; give each XCD a contiguous run
+  // of tiles so neighbouring tiles (same A row panel) share that XCD's L2
+  int tile = blockIdx.x;
+  int split = blockIdx.y;
+  int prob = blockIdx.z;
+  const int nsplit = gridDim.y;
+  if (batch.xcd_plane) {
+    // weight gradients: remap the whole (tile, split, problem) grid XCD-major, so the tiles of one
+    // (K slice, problem) -- which share its dY / X panels -- run on one XCD's L2 instead of being
+    // spread over the eight (C1: dW fetch bytes per launch 214 -> 166 MB)
+    const int nwg = gridDim.x * nsplit * gridDim.z;
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + nsplit * blockIdx.z);
+    const int x = lin % 8, q = nwg / 8, rr = nwg % 8;
+    const int l2 = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + lin / 8;
+    tile = l2 % gridDim.x;
+    split = (l2 / gridDim.x) % nsplit;
+    prob = l2 / (gridDim.x * nsplit);
+  }
+  const GemmProblem& P = batch.p[prob];
   const int M = P.M, N = P.N, K = P.K;
   const int tiles_n = (N + GBN - 1) / GBN;
   const int tiles_m = (M + GBM - 1) / GBM;
   const int ntiles = tiles_m * tiles_n;
-  // XCD-aware remap (bijective): blocks b and b+8 share an XCD; give each XCD a contiguous run
-  // of tiles so neighbouring tiles (same A row panel) share that XCD's L2
-  int tile = blockIdx.x;
-  const int split = blockIdx.y, nsplit = gridDim.y;
-  {
+  if (!batch.xcd_plane) {
     const int nwg = gridDim.x;
     const int x = tile % 8, q = nwg / 8, rr = nwg % 8;
     tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + tile / 8;
@@ -978,12 +1022,19 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
   } else {
     splits = 1;
   }
+  // XCD-major remap of the (tile, split, problem) grid (MMT_DW_XCD_PLANE=0 turns it off)
+  static const int xcd_plane = [] {
+    const char* e = getenv("MMT_DW_XCD_PLANE");
+    return e ? atoi(e) : 1;
+  }();
   if (splits <= 1) {  // one K pass: accumulate straight into the gradient
     GemmBatch d = b;
+    d.xcd_plane = xcd_plane;
     for (int g = 0; g < d.count; ++g) d.p[g].split_stride = 0;
     return launch_t<false, false, true, EPI_ACC_F32>(d, 1, big, s);
   }
   GemmBatch d = b;
+  d.xcd_plane = xcd_plane;
   SlabBatch sb{};
   sb.count = b.count;
   sb.splits = splits;
@@ -1009,6 +1060,29 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
 
 
 bool mmt_gemm_wgrad_big(const GemmBatch& b) { return use_big(b); }
+
+bool mmt_gemm_resid_ln_ok(const GemmBatch& b) {
+  if (b.count == 0) return false;
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& P = b.p[g];
+    if (P.N != TileL::BN || !P.resid || !P.o32 || (P.ldc & 3) || (P.ldres & 3) || (P.o16 && (P.ldo16 & 7)) ||
+        (P.lda & 7) || (P.ldb & 7) || (((uintptr_t)P.A | (uintptr_t)P.B | (uintptr_t)P.o32 | (uintptr_t)P.resid) & 15))
+      return false;
+    if (P.lnf_y && (!P.lnf_gamma || !P.lnf_beta || !P.lnf_mean || !P.lnf_rstd ||
+                    (((uintptr_t)P.lnf_y | (uintptr_t)P.lnf_gamma | (uintptr_t)P.lnf_beta) & 15)))
+      return false;
+  }
+  return true;
+}
+
+hipError_t mmt_launch_gemm_resid_ln(const GemmBatch& b, hipStream_t s) {
+  if (!mmt_gemm_resid_ln_ok(b)) return hipErrorInvalidValue;
+  // the 256x256 tile whatever K (its block owns whole rows); as launch_t's big path, variant 0
+  const int mt = max_tiles<TileL>(b, nullptr);
+  if (mt == 0) return hipSuccess;
+  launch_v<TileL, 64, 2, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
+  return hipGetLastError();
+}
 
 bool mmt_gemm_ln_bwd_ok(const GemmBatch& b) {
   if (b.count == 0) return false;

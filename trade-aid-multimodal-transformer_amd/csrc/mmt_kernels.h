@@ -73,11 +73,20 @@ struct GemmProblem {
   const float* ln_rstd;
   float* ln_dgamma;
   float* ln_dbeta;
+  // EPI_BIAS_RESID_F32 + the NEXT LayerNorm's forward on the stored rows (whole rows per block:
+  // mmt_launch_gemm_resid_ln): lnf_y = bf16((o32 - mean) * rstd * lnf_gamma + lnf_beta) [M][N], and
+  // the row statistics lnf_mean / lnf_rstd (as ln_fwd_kernel, eps 1e-5); null lnf_y: off
+  const float* lnf_gamma;
+  const float* lnf_beta;
+  bf16_t* lnf_y;
+  float* lnf_mean;
+  float* lnf_rstd;
 };
 
 struct GemmBatch {
   GemmProblem p[MMT_MAX_GROUP];
   int count;
+  int xcd_plane;  // split-K launches: 1 = XCD-major remap of the whole (tile, split) plane
 };
 
 hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, int splits, hipStream_t s);
@@ -85,6 +94,11 @@ hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, in
 // its rows fused (EPI_LN_BWD_F32) on a tile spanning the row: every problem needs N == 256 (256x256
 // tile) or N == 512 (128x512; all problems alike) and 16-B aligned rows. Returns hipErrorInvalidValue otherwise (the caller runs the two passes)
 bool mmt_gemm_ln_bwd_ok(const GemmBatch& b);
+// forward residual GEMM (EPI_BIAS_RESID_F32) with the next LayerNorm's forward fused on the problems
+// whose lnf_y is set; every problem needs N == 256 (256x256 tile, any K). hipErrorInvalidValue
+// otherwise (the caller launches the LayerNorm itself)
+bool mmt_gemm_resid_ln_ok(const GemmBatch& b);
+hipError_t mmt_launch_gemm_resid_ln(const GemmBatch& b, hipStream_t s);
 hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s);
 // weight gradients o32 += alpha * A^T B over K rows (both operands MN-contiguous): split-K into fp32
 // slabs in `slab` (capacity slab_bytes) + one reduce pass; without room, one K pass accumulating
