@@ -99,7 +99,7 @@ __device__ __forceinline__ int key_dword(int r) { return 2 * ((r & 3) + 4 * (r >
 // Workgroups are ordered heaviest key block first (the causal walk of key block kb is nt - NWV kb
 // slices long) so the launch does not end on a tail of long blocks.
 // =============================================================================================
-template <bool DROP, int OCC, int S, int NWV>
+template <bool DROP, int OCC, int S, int NWV, bool PAIR = false>
 __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch, int T, int H, float scale) {
   constexpr int NKS = 4, ND = 2;  // hs 64: 4 k-steps of 16, 2 output tiles of 32
   static_assert(S >= 3 && 4 * (S - 2) <= 16, "ring slots: S - 1 slices in flight, counted waits <= 16");
@@ -193,9 +193,14 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
       dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
     }
   };
+  int nis = 0;  // slices issued so far (uniform)
+  if (PAIR) {
+    for (; nis < S - 1 && nis < nq; ++nis) issue(nis, kt0 + nis);
+  } else {
 #pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < nq) issue(i, kt0 + i);
+    for (int i = 0; i < S - 1; ++i)
+      if (i < nq) issue(i, kt0 + i);
+  }
 
   // per-lane read offsets (the slot base and the k step / column block are added as immediates):
   // row reads (lane row r, half h of 16-column block s), transposed reads (tr_frag geometry: rows
@@ -291,11 +296,32 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
   const int n_diag = min(NWV, nq);
   const int n_plain_end = (ragged && nq > 4) ? nq - 1 : nq;
   int i = 0;
+  if (PAIR) {
+    // PAIR: the plain slices two per barrier (their tiles' independent S / dP chains interleave); the
+    // ring refills every slot whose slice is consumed, so slices in flight drop from S - 1 to S - 2
+    auto step_n = [&](int i0, int n, auto mc) {
+      wait_vm(per * (nis - i0 - n));  // this wave's pieces of slices i0 .. i0 + n - 1 landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // everyone's landed; every read of slices < i0 is done
+      for (; nis <= i0 + S - 1 && nis < nq; ++nis) issue(nis % S, kt0 + nis);
+      for (int u = 0; u < n; ++u) {
+        const int qt = kt0 + i0 + u;
+        if (live && qt >= kt) tile(lds + ((i0 + u) % S) * SLOT, qt, mc);
+      }
+    };
 #pragma unroll 1
-  for (; i < n_diag; ++i) step(i, std::true_type{});
+    for (; i < n_diag; ++i) step_n(i, 1, std::true_type{});
 #pragma unroll 1
-  for (; i < n_plain_end; ++i) step(i, std::false_type{});
-  if (i < nq) step(i, std::true_type{});
+    for (; i + 1 < n_plain_end; i += 2) step_n(i, 2, std::false_type{});
+    if (i < n_plain_end) { step_n(i, 1, std::false_type{}); ++i; }
+    if (i < nq) step_n(i, 1, std::true_type{});
+  } else {
+#pragma unroll 1
+    for (; i < n_diag; ++i) step(i, std::true_type{});
+#pragma unroll 1
+    for (; i < n_plain_end; ++i) step(i, std::false_type{});
+    if (i < nq) step(i, std::true_type{});
+  }
   __syncthreads();  // the ring is free: the epilogue transposes through it
 
   // dK / dV tiles: accumulator rows = key ((e&3)+8(e>>2)+4h), cols = d (lane); each 32-column slice
@@ -800,6 +826,11 @@ hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& bt, int B, int T, int H, fl
   const int nwv = (variant & 8) ? 8 : (variant & 16) ? 4 : dkdv_waves(T);
   const int nkb = (nt + nwv - 1) / nwv;
   const dim3 grid(nkb * B * H * bt.p[0].nstreams, 1, bt.count);
+  if (variant & 32) {  // two plain slices per barrier on a 6-slot ring
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2, 6, 4, true>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2, 6, 4, true>), grid, dim3(256), 0, s, bt, T, H, scale);
+    return hipGetLastError();
+  }
   if (nwv == 8) dkdv_launch<4, 8>(bt, grid, T, H, scale, drop, occ3, s);
   else if (ring_slots() >= 6) dkdv_launch<6, 4>(bt, grid, T, H, scale, drop, occ3, s);
   else dkdv_launch<4, 4>(bt, grid, T, H, scale, drop, occ3, s);
