@@ -415,7 +415,7 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
           if (EPI == EPI_BIAS_RESID_F32 && P.o16)
             *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
                 u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
-          if (EPI == EPI_BIAS_RESID_F32 && GBN == 256 && P.lnf_y) {
+          if (EPI == EPI_BIAS_RESID_F32 && (GBN == 256 || GBN == 512) && P.lnf_y) {
             // the next LayerNorm on this row (whole rows per block: N == GBN, mmt_launch_gemm_resid_ln;
             // lnf_y is uniform per problem and m < M per half wave, so every lane of the row's half
             // wave takes the shuffles): mean, then the centred sum of squares (as ln_fwd_kernel)
@@ -1065,8 +1065,9 @@ bool mmt_gemm_resid_ln_ok(const GemmBatch& b) {
   if (b.count == 0) return false;
   for (int g = 0; g < b.count; ++g) {
     const GemmProblem& P = b.p[g];
-    if (P.N != TileL::BN || !P.resid || !P.o32 || (P.ldc & 3) || (P.ldres & 3) || (P.o16 && (P.ldo16 & 7)) ||
-        (P.lda & 7) || (P.ldb & 7) || (((uintptr_t)P.A | (uintptr_t)P.B | (uintptr_t)P.o32 | (uintptr_t)P.resid) & 15))
+    if ((P.N != TileL::BN && P.N != TileW::BN) || P.N != b.p[0].N || !P.resid || !P.o32 || (P.ldc & 3) ||
+        (P.ldres & 3) || (P.o16 && (P.ldo16 & 7)) || (P.lda & 7) || (P.ldb & 7) ||
+        (((uintptr_t)P.A | (uintptr_t)P.B | (uintptr_t)P.o32 | (uintptr_t)P.resid) & 15))
       return false;
     if (P.lnf_y && (!P.lnf_gamma || !P.lnf_beta || !P.lnf_mean || !P.lnf_rstd ||
                     (((uintptr_t)P.lnf_y | (uintptr_t)P.lnf_gamma | (uintptr_t)P.lnf_beta) & 15)))
@@ -1077,10 +1078,17 @@ bool mmt_gemm_resid_ln_ok(const GemmBatch& b) {
 
 hipError_t mmt_launch_gemm_resid_ln(const GemmBatch& b, hipStream_t s) {
   if (!mmt_gemm_resid_ln_ok(b)) return hipErrorInvalidValue;
-  // the 256x256 tile whatever K (its block owns whole rows); as launch_t's big path, variant 0
-  const int mt = max_tiles<TileL>(b, nullptr);
-  if (mt == 0) return hipSuccess;
-  launch_v<TileL, 64, 2, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
+  // a tile as wide as the row whatever K (its block owns whole rows): 256 x 256 (as launch_t's big
+  // path, variant 0) at C = 256, 128 x 512 at C = 512
+  if (b.p[0].N == TileW::BN) {
+    const int mt = max_tiles<TileW>(b, nullptr);
+    if (mt == 0) return hipSuccess;
+    launch_v<TileW, 32, 2, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
+  } else {
+    const int mt = max_tiles<TileL>(b, nullptr);
+    if (mt == 0) return hipSuccess;
+    launch_v<TileL, 64, 2, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
+  }
   return hipGetLastError();
 }
 

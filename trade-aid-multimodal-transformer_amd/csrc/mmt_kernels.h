@@ -95,7 +95,8 @@ hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, in
 // tile) or N == 512 (128x512; all problems alike) and 16-B aligned rows. Returns hipErrorInvalidValue otherwise (the caller runs the two passes)
 bool mmt_gemm_ln_bwd_ok(const GemmBatch& b);
 // forward residual GEMM (EPI_BIAS_RESID_F32) with the next LayerNorm's forward fused on the problems
-// whose lnf_y is set; every problem needs N == 256 (256x256 tile, any K). hipErrorInvalidValue
+// whose lnf_y is set; every problem needs N == 256 (256x256 tile) or N == 512 (128x512; all alike),
+// any K. hipErrorInvalidValue
 // otherwise (the caller launches the LayerNorm itself)
 bool mmt_gemm_resid_ln_ok(const GemmBatch& b);
 hipError_t mmt_launch_gemm_resid_ln(const GemmBatch& b, hipStream_t s);
