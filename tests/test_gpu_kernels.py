@@ -387,11 +387,12 @@ def test_attention_fwd_bwd(B, T, H, hs, ns):
         assert rel(heads(got_v[j]), vf[j].grad) < 2e-2, (j, rel(heads(got_v[j]), vf[j].grad))
 
 
-@pytest.mark.parametrize("ring", [0, 1, 3, 3 | 8, 3 | 16, 3 | 32])
+@pytest.mark.parametrize("ring", [0, 1, 3, 7, 3 | 8, 3 | 16, 3 | 32])
 @pytest.mark.parametrize("B,T,H,ns", [(2, 100, 2, 1), (1, 520, 2, 2), (1, 1024, 1, 1), (2, 300, 2, 3), (1, 33, 2, 1)])
 def test_attention_hs64_backward_variants(B, T, H, ns, ring):
     """Every hs-64 backward variant (mmt_attn_set_ring: 0 the chunked dQ and dK/dV passes, 1 the
-    slice-streamed dK/dV ring, 3 both rings with two query tiles per wave in the dQ ring; + 8 / 16:
+    slice-streamed dK/dV ring, 3 both rings with two query tiles per wave in the dQ ring, 7 (the
+    default) that with the dK/dV ring at 3 waves per SIMD; + 8 / 16:
     8 / 4 key tiles per dK/dV workgroup at every T; + 32: plain slices two per barrier) against the same torch reference, ragged T and
     multi-stream included."""
     L = ML.lib()

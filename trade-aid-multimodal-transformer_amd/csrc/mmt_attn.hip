@@ -1152,7 +1152,10 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
 // mmt_attn_set_ring() for in-process A/B
 static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
-  return e ? atoi(e) : 3;  // both hs-64 passes on the rings (dQ: two query tiles per wave)
+  // both hs-64 passes on the rings (dQ: two query tiles per wave), dK/dV at 3 waves per SIMD
+  // (standalone backward: target 277 -> 273 us, C3 cross-attention 2461 -> 2298, C4 2237 -> 2116;
+  // C3 step -1.5 %: profiles/r3u_ring_ab.txt)
+  return e ? atoi(e) : 7;
 }();
 extern "C" int mmt_attn_set_ring(int v) {
   const int old = g_attn_ring;
