@@ -46,6 +46,9 @@ using TileW = TileCfg<1, 8, 4, 2>;
 // 128 x 256, 4 waves (1 x 4) of 128 x 64: whole 256-wide rows at twice the blocks of TileL, two
 // blocks per CU, so one block's LayerNorm epilogue (HBM-bound) overlaps another's K loop
 using TileH = TileCfg<1, 4, 4, 2>;
+// 256 x 128, 4 waves (2 x 2) of 128 x 64 (TileL's per-wave shape: 0.75 fragment reads per MFMA
+// instead of TileS's 1) at two blocks per CU (variants 7 / 8 of the short-K path)
+using TileM = TileCfg<2, 2, 4, 2>;
 
 // tuning knob (mmt_gemm_set_variant): pipeline variant of the forward / backward-data GEMMs in
 // bits 0-3 and of the weight-grad (split-K, atomic) GEMMs in bits 4-7:
@@ -55,7 +58,7 @@ static int g_gemm_variant = -1;     // forward / backward-data (-1: per-epilogue
 static int g_gemm_variant_dw = 0;   // weight grad (split-K atomic)
 extern "C" int mmt_gemm_set_variant(int v) {
   if (v < 0) { g_gemm_variant = -1; g_gemm_variant_dw = 0; return 0; }  // back to the default policy
-  if ((v & 15) > 6 || ((v >> 4) & 15) > 6) return -1;
+  if ((v & 15) > 8 || ((v >> 4) & 15) > 6) return -1;
   g_gemm_variant = v & 15;
   g_gemm_variant_dw = (v >> 4) & 15;
   return 0;
@@ -882,6 +885,20 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     case 4: launch_v<TileS, 64, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 5: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
     case 6: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
+    case 7:
+    case 8: {
+      if constexpr (SWAP) {  // 256 x 128 tile: its own grid
+        const int mtm = max_tiles<TileM>(b, nullptr);
+        if (mtm == 0) return hipSuccess;
+        const dim3 gm(mtm, grid.y, grid.z);
+        // two blocks per CU (8 waves): the launch bound caps the registers at 256 per lane
+        if (var == 7) launch_v<TileM, 32, 2, A_KC, B_KC, SWAP, EPI, 2>(b, gm, s);
+        else launch_v<TileM, 64, 2, A_KC, B_KC, SWAP, EPI, 2>(b, gm, s);
+      } else {
+        launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s);
+      }
+      break;
+    }
     default: launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
   }
   return hipGetLastError();
