@@ -118,6 +118,22 @@ def test_gemm_backward_data(M, N, K, epi):
         assert rel(o32, base + ref) < 1e-5
 
 
+@pytest.mark.parametrize("variant", [7, 8])
+@pytest.mark.parametrize("M,N,K", [(256, 128, 64), (200, 136, 72), (33, 17, 45), (600, 300, 512), (16384 // 64, 384, 256)])
+def test_gemm_tile_256x128_variants(variant, M, N, K):
+    """The 256 x 128 tile (mmt_gemm_set_variant 7 / 8: the ReLU forward at K >= 512 uses 7 by
+    default) on every forward and backward-data epilogue, ragged edges included."""
+    L = ML.lib()
+    assert L.mmt_gemm_set_variant(variant) == 0
+    try:
+        for epi in ["store_bf16", "bias_tanh_bf16", "bias_relu_bf16", "bias_resid_f32", "store_f32"]:
+            test_gemm_forward_linear(M, N, K, epi)
+        for epi in ["store_bf16", "dtanh_bf16", "drelu_bf16", "store_f32", "acc_f32"]:
+            test_gemm_backward_data(M, N, K, epi)
+    finally:
+        L.mmt_gemm_set_variant(-1)
+
+
 @pytest.mark.parametrize("M,N,R", [(384, 256, 4096), (1024, 256, 2048), (900, 450, 1000), (6, 32, 300), (32, 16, 77)])
 @pytest.mark.parametrize("splits", [1, 4, 0])
 def test_gemm_weight_grad(M, N, R, splits):

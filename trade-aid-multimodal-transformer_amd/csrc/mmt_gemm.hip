@@ -875,9 +875,19 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     const char* e = getenv("MMT_GEMM_DW_VARIANT");
     return e ? atoi(e) : -1;
   }();
+  // the bias+ReLU forward (ffn0) at K >= 512 (target / C3 shapes) takes the 256 x 128 tile (TileM, 2
+  // blocks per CU): standalone 214 -> 194 us at the target; the other short-K shapes measured slower
+  // on it (profiles/r3x_gemm_tilem.txt). MMT_GEMM_TILEM=0 turns the policy off
+  static const int tilem = [] {
+    const char* e = getenv("MMT_GEMM_TILEM");
+    return e ? atoi(e) : 1;
+  }();
+  int kmax = 0;
+  for (int g = 0; g < b.count; ++g) kmax = std::max(kmax, b.p[g].K);
+  const bool relu_wide = tilem && EPI == EPI_BIAS_RELU_BF16 && A_KC && B_KC && kmax >= 512;
   const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw
                   : (!A_KC && !B_KC && env_dw >= 0) ? env_dw
-                  : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? 6 : 0);
+                  : (g_gemm_variant >= 0 ? g_gemm_variant : relu_wide ? 7 : occ3 ? 6 : 0);
   switch (var) {
     case 1: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 2: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
