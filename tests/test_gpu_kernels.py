@@ -121,8 +121,8 @@ def test_gemm_backward_data(M, N, K, epi):
 @pytest.mark.parametrize("variant", [7, 8])
 @pytest.mark.parametrize("M,N,K", [(256, 128, 64), (200, 136, 72), (33, 17, 45), (600, 300, 512), (16384 // 64, 384, 256)])
 def test_gemm_tile_256x128_variants(variant, M, N, K):
-    """The 256 x 128 tile (mmt_gemm_set_variant 7 / 8: the ReLU forward at K >= 512 uses 7 by
-    default) on every forward and backward-data epilogue, ragged edges included."""
+    """The 256 x 128 tile (mmt_gemm_set_variant 7 / 8; MMT_GEMM_TILEM=1 puts the ReLU forward at
+    K >= 512 on 7) on every forward and backward-data epilogue, ragged edges included."""
     L = ML.lib()
     assert L.mmt_gemm_set_variant(variant) == 0
     try:

@@ -875,12 +875,13 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     const char* e = getenv("MMT_GEMM_DW_VARIANT");
     return e ? atoi(e) : -1;
   }();
-  // the bias+ReLU forward (ffn0) at K >= 512 (target / C3 shapes) takes the 256 x 128 tile (TileM, 2
-  // blocks per CU): standalone 214 -> 194 us at the target; the other short-K shapes measured slower
-  // on it (profiles/r3x_gemm_tilem.txt). MMT_GEMM_TILEM=0 turns the policy off
+  // MMT_GEMM_TILEM=1: the bias+ReLU forward (ffn0) at K >= 512 (target / C3) on the 256 x 128 tile
+  // (TileM, 2 blocks per CU). Standalone 214 -> 194 us at the target (the other short-K shapes slower:
+  // profiles/r3x_gemm_tilem.txt), but in the step beside the side stream 20.21 -> 20.37 ms at the
+  // target, C3 neutral (profiles/r3y_tilem_ab.txt): off by default
   static const int tilem = [] {
     const char* e = getenv("MMT_GEMM_TILEM");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   int kmax = 0;
   for (int g = 0; g < b.count; ++g) kmax = std::max(kmax, b.p[g].K);
