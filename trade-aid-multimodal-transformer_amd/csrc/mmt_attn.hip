@@ -123,6 +123,15 @@ struct Stager {
       v[u] = tile_chunk(isb ? b : a, rowbase, r0, cc / CH, (cc % CH) * 8, T, isb ? ldb : lda);
     }
   }
+  // operand a's chunks only (a second image of it at another stride)
+  __device__ __forceinline__ void store_a(bf16_t* la, int sa, int tid) const {
+    constexpr int CH = Geo<HS>::CH, HALF = Chunk<HS>::HALF;
+#pragma unroll
+    for (int u = 0; u < Chunk<HS>::NSTG; ++u) {
+      const int c = tid + 256 * u;
+      if (c < HALF) *reinterpret_cast<u32x4*>(la + (c / CH) * sa + (c % CH) * 8) = v[u];
+    }
+  }
   __device__ __forceinline__ void store(bf16_t* la, int sa, bf16_t* lb, int sb, int tid) const {
     constexpr int CH = Geo<HS>::CH, HALF = Chunk<HS>::HALF;
 #pragma unroll
@@ -183,6 +192,9 @@ constexpr float kTau = 8.0f;  // lazy-rescale threshold of the forward's running
 // = 64 the forward fits two without AGPRs; the dQ pass spills ~25 VGPRs there and is still faster)
 #ifndef MMT_FWD_MINB
 #define MMT_FWD_MINB(hs) 2
+#endif
+#ifndef MMT_DQ_KT2
+#define MMT_DQ_KT2 1  // hs <= 32 dQ pass: second K image for the transposed reads (0: one image)
 #endif
 #ifndef MMT_DQ_MINB
 #define MMT_DQ_MINB(hs) 2
@@ -522,9 +534,9 @@ __device__ __forceinline__ void dq_ds(f32x16& sacc, const f32x16& dpacc, const D
 // The K / V row fragments and the transposed K fragments are read once for both tiles and issued
 // up front (the transposed ones land behind the dS arithmetic)
 template <int HS, int NQ, bool DA, bool DB, bool DROP>
-__device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, int kl, int k0, DqQ<HS>& a, DqQ<HS>& b,
-                                        const uint32_t* mta, const uint32_t* mtb, float c2, const AttnProblem& P,
-                                        int lane) {
+__device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, const bf16_t* kts, int kts_ld, int kl,
+                                        int k0, DqQ<HS>& a, DqQ<HS>& b, const uint32_t* mta, const uint32_t* mtb,
+                                        float c2, const AttnProblem& P, int lane) {
   using G = Geo<HS>;
   const int r = lane & 31, h = lane >> 5;
   const uint32_t wa = DROP ? reinterpret_cast<const uint16_t*>(mta)[lane] : 0u;  // keep bits (LDS)
@@ -563,7 +575,7 @@ __device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, int 
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int dt = 0; dt < G::ND; ++dt) kt[s][dt] = tr_frag(ks + kl * G::RW, G::RW, dt, s, lane);
+      for (int dt = 0; dt < G::ND; ++dt) kt[s][dt] = tr_frag(kts + kl * kts_ld, kts_ld, dt, s, lane);
     dq_ds<HS, DA, DROP>(sa, pa, a, k0, c2, dsc, wa, h, dfa);
     dq_ds<HS, DB, DROP>(sb, pb, b, k0, c2, dsc, wb, h, dfb);
 #pragma unroll
@@ -578,7 +590,7 @@ __device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, int 
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int dt = 0; dt < G::ND; ++dt) a.dq[dt] = mfma32(tr_frag(ks + kl * G::RW, G::RW, dt, s, lane), dfa[s], a.dq[dt]);
+      for (int dt = 0; dt < G::ND; ++dt) a.dq[dt] = mfma32(tr_frag(kts + kl * kts_ld, kts_ld, dt, s, lane), dfa[s], a.dq[dt]);
   }
 }
 
@@ -610,13 +622,24 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   const int nch = (min((qmax + 1) * 32, T) + ROWS - 1) / ROWS;
   const int64_t rowbase = (int64_t)b * T;
   const float c2 = scale * kLog2e;
-  __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row + tr reads
+  __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row (+ tr at hs > 32) reads
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::RW];  // V chunk: row reads
+  // hs <= 32: a second K image at the transposed-read stride (64-B rows: its ds_read_b64_tr_b16 rows
+  // land on distinct banks; at the row-read stride they conflict 2-way — 31 % of the kernel's LDS
+  // cycles in profiles/r3final_sq_c1.txt)
+  constexpr bool KT2 = MMT_DQ_KT2 && HS <= 32;
+  __shared__ __attribute__((aligned(16))) bf16_t kt2[KT2 ? ROWS * G::TW : 8];
+  const bf16_t* kts = KT2 ? kt2 : ks;
+  constexpr int KTS_LD = KT2 ? G::TW : G::RW;
   using MS = MaskStager<HS, ROWS / 32>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // keep-bit lane words
-  if (HS % 32 != 0)  // pad columns are read only when HS is not a multiple of 32
+  if (HS % 32 != 0) {  // pad columns are read only when HS is not a multiple of 32
     for (int q = tid; q < ROWS * G::RW; q += 256)
       if (q % G::RW >= HS) { ks[q] = 0; vs[q] = 0; }
+    if (KT2)
+      for (int q = tid; q < ROWS * G::TW; q += 256)
+        if (q % G::TW >= HS) kt2[q] = 0;
+  }
   Stager<HS> st;
   MS mst;
   // lane-word record of the keep bits (AttnProblem::dmask): after the key-major one
@@ -628,6 +651,7 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
       st.load(P.k[jj] + head * P.kv_hstride, P.kv_ld, P.v[jj] + head * P.kv_hstride, P.kv_ld, rowbase,
               cc * ROWS + rr * SR, T, tid);
       st.store(ks + rr * SR * G::RW, G::RW, vs + rr * SR * G::RW, G::RW, tid);
+      if (KT2) st.store_a(kt2 + rr * SR * G::TW, G::TW, tid);
     }
     if (DROP) mst.store(msk, tid);
   };
@@ -680,10 +704,10 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
       const int kt_lo = c * (ROWS / 32);
       const int kt_hi = min(kt_lo + ROWS / 32, nt) - 1;
 #define DQ_STEP(NQ, DA, DB, KT) \
-  dq_step<HS, NQ, DA, DB, DROP>(ks, vs, ((KT) - kt_lo) * 32, (KT) * 32, A, Bq, mska + ((KT) - kt_lo) * 32, \
+  dq_step<HS, NQ, DA, DB, DROP>(ks, vs, kts, KTS_LD, ((KT) - kt_lo) * 32, (KT) * 32, A, Bq, mska + ((KT) - kt_lo) * 32, \
                                 mskb + ((KT) - kt_lo) * 32, c2, P, lane)
 #define DQ_STEP_B(DB, KT) \
-  dq_step<HS, 1, DB, false, DROP>(ks, vs, ((KT) - kt_lo) * 32, (KT) * 32, Bq, A, mskb + ((KT) - kt_lo) * 32, mska, \
+  dq_step<HS, 1, DB, false, DROP>(ks, vs, kts, KTS_LD, ((KT) - kt_lo) * 32, (KT) * 32, Bq, A, mskb + ((KT) - kt_lo) * 32, mska, \
                                   c2, P, lane)
       if (lb) {
         int kt = kt_lo;
