@@ -194,7 +194,9 @@ constexpr float kTau = 8.0f;  // lazy-rescale threshold of the forward's running
 #define MMT_FWD_MINB(hs) 2
 #endif
 #ifndef MMT_DQ_KT2
-#define MMT_DQ_KT2 1  // hs <= 32 dQ pass: second K image for the transposed reads (0: one image)
+// hs <= 32 dQ pass: 1 = a second K image for the transposed reads. Measured neutral at C1 (8.943 vs
+// 8.944 ms/step, three same-box pairs: profiles/r3k_dq_kt2_ab.txt): off
+#define MMT_DQ_KT2 0
 #endif
 #ifndef MMT_DQ_MINB
 #define MMT_DQ_MINB(hs) 2
