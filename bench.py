@@ -47,6 +47,9 @@ WORKLOADS = {"c1": "C1: 4-modality 1M-row synthetic, d256 L6 T256 (BASELINE conf
              "c3": "C3: 8-modality selective cross-attention stress, d512 L12 T1024 (BASELINE configs[3], per GPU)",
              "c4": "C4: 4-modality, d1024 L24 T4096 (BASELINE configs[4], per GPU)"}
 PEAK_TFLOPS = 2500.0  # MI355X bf16 dense MFMA (MI355X_MICROARCH.md; no sparsity)
+PEAK_TFLOPS_FP8 = 5000.0  # MX-fp8 dense MFMA (v_mfma_scale_f32_32x32x64_f8f6f4: 2x the bf16 rate)
+# forward GEMM launch labels that run on the MX-fp8 kernel under precision fp8 (mmt_engine.hip run_forward)
+FP8_LABELS = {"qkv1", "ffn0", "ffn2", "ca_q"}
 PEAK_HBM_GBS = 8000.0  # HBM3E
 METRIC = "training tokens/sec/GPU, 4-modality 1M-row synthetic, at 1/2/4/8 MI355X"
 
@@ -82,14 +85,22 @@ def pmc_traffic(config, label):
         return None
 
 
-def roofline_entry(label, ms, n, flops, nbytes, sampled_steps, config):
+def fp8_flops_per_row(M, C, L, cross):
+    """Training flops per row that run on the MX-fp8 forward GEMMs under precision fp8: the forward of
+    Q/K/V stage 1 (C x 3C/2), FFN up + down (8 C^2) per modality and the cross query (C^2) per
+    cross-enabled modality (2 flops per MAC; their backward stays bf16)."""
+    X = sum(1 for i in range(M) if cross[i]) if M > 1 else 0
+    return 2.0 * L * (M * 9.5 * C * C + X * C * C)
+
+
+def roofline_entry(label, ms, n, flops, nbytes, sampled_steps, config, peak=PEAK_TFLOPS):
     """Roofline of one probed launch family: algorithmic flops / bytes per launch (reported by the
     engine for each launch) over the live HIP-event launch time; the binding roof at the family's
-    arithmetic intensity (ridge = 2500 TFLOP/s / 8 TB/s = 312.5 flop/B)."""
+    arithmetic intensity (ridge = peak / 8 TB/s: 312.5 flop/B at bf16, 625 at MX-fp8)."""
     sec = ms * 1e-3 / n
     fl, by = flops / n, nbytes / n
-    if fl / by >= PEAK_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9):
-        r = {"bound": "mfma", "achieved": round(fl / sec / 1e12, 1), "peak": PEAK_TFLOPS, "unit": "TFLOP/s"}
+    if fl / by >= peak * 1e12 / (PEAK_HBM_GBS * 1e9):
+        r = {"bound": "mfma", "achieved": round(fl / sec / 1e12, 1), "peak": peak, "unit": "TFLOP/s"}
     else:
         r = {"bound": "hbm", "achieved": round(by / sec / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
     r["frac"] = round(r["achieved"] / r["peak"], 4)
@@ -97,8 +108,21 @@ def roofline_entry(label, ms, n, flops, nbytes, sampled_steps, config):
               "launches_per_step": round(n / sampled_steps, 2), "ms_per_step": round(ms / sampled_steps, 4),
               "avg_launch_us": round(sec * 1e6, 2), "flops_per_launch": fl, "algorithmic_bytes_per_launch": by,
               "tflops": round(fl / sec / 1e12, 1), "gbs": round(by / sec / 1e9, 1),
-              "mfma_frac": round(fl / sec / 1e12 / PEAK_TFLOPS, 4)})
+              "mfma_peak_tflops": peak, "mfma_frac": round(fl / sec / 1e12 / peak, 4)})
     return r
+
+
+def read_probes(L_, ctx, probes, sampled, config, peaks):
+    import mmt_lib as ML
+    out = []
+    for pi, label in enumerate(probes):
+        ms, n, fl, by = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_double(0), ctypes.c_double(0)
+        ML.check(L_.mmt_probe_read_at(ctx, pi, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl),
+                                      ctypes.byref(by)), ctx, "mmt_probe_read_at")
+        if n.value > 0 and by.value > 0:
+            out.append(roofline_entry(label, ms.value, n.value, fl.value, by.value, max(1, sampled), config,
+                                      peaks.get(label, PEAK_TFLOPS)))
+    return out
 
 
 def cpu_model():
@@ -198,6 +222,8 @@ def main():
                     help="compute precision (default: fp8 for c4 as BASELINE configs[4] names it, else bf16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--serial-steps", type=int, default=8,
+                    help="probed steps run with the side stream off after the main run (serial per-kernel rates)")
     ap.add_argument("--exact-steps", type=int, default=20,
                     help="steps timed with the bit-exact device get_batch (reference RNG streams) after the main run")
     args = ap.parse_args()
@@ -282,23 +308,50 @@ def main():
         tt = torch.tensor([dt], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    kernels = []
-    for pi, label in enumerate(probes):
-        ms, n, fl, by = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_double(0), ctypes.c_double(0)
-        ML.check(L_.mmt_probe_read_at(model._ctx, pi, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl),
-                                      ctypes.byref(by)), model._ctx, "mmt_probe_read_at")
-        if n.value > 0 and by.value > 0:
-            kernels.append(roofline_entry(label, ms.value, n.value, fl.value, by.value, max(1, sampled), args.config))
+    peaks = {lb: PEAK_TFLOPS_FP8 for lb in FP8_LABELS} if precision == "fp8" else {}
+    kernels = read_probes(L_, model._ctx, probes, sampled, args.config, peaks)
     L_.mmt_probe_set(model._ctx, None)
     final_loss = float(sum(l.item() for l in losses))
+    if args.serial_steps > 0 and world == 1:
+        # the same families with the side stream off (weight gradients and keep bits on the main
+        # stream): each launch has the chip to itself, so these are the per-kernel rates the live
+        # figures above are shares of (untimed for the headline; one warm step first)
+        ML.check(L_.mmt_set_side_stream(model._ctx, 0), model._ctx, "mmt_set_side_stream")
+        step()
+        torch.cuda.synchronize()
+        L_.mmt_probe_set(model._ctx, ",".join(probes).encode())
+        L_.mmt_probe_enable(model._ctx, 1)
+        for _ in range(args.serial_steps):
+            step()
+        torch.cuda.synchronize()
+        serial = {k["label"]: k for k in read_probes(L_, model._ctx, probes, args.serial_steps, args.config, peaks)}
+        L_.mmt_probe_set(model._ctx, None)
+        ML.check(L_.mmt_set_side_stream(model._ctx, 1), model._ctx, "mmt_set_side_stream")
+        for k in kernels:
+            sk = serial.get(k["label"])
+            if sk:
+                k["serial"] = {"avg_launch_us": sk["avg_launch_us"], "achieved": sk["achieved"], "frac": sk["frac"],
+                               "tflops": sk["tflops"], "mfma_frac": sk["mfma_frac"], "ms_per_step": sk["ms_per_step"]}
     nonfinite = int(model.nonfinite_loss_mask(sticky=True).item())
 
     tokens = world * B * T * M * args.steps
     value = tokens / dt
-    flops_row = train_flops_per_row(M, C, H, L, T, V, [p[8] for p in data["params"]])
+    cross = [p[8] for p in data["params"]]
+    flops_row = train_flops_per_row(M, C, H, L, T, V, cross)
     achieved_step_tflops = flops_row * B * T * args.steps / dt / 1e12  # per GPU
+    # the MFMA fraction of the step: each flop priced at the peak of the unit it runs on (MX-fp8 for
+    # the fp8 forward GEMMs under precision fp8, bf16 for the rest)
+    f8_row = fp8_flops_per_row(M, C, L, cross) if precision == "fp8" else 0.0
+    step_peak_s = (f8_row / (PEAK_TFLOPS_FP8 * 1e12) + (flops_row - f8_row) / (PEAK_TFLOPS * 1e12)) * B * T * args.steps
+    step_mfma_frac = step_peak_s / dt
     # the roofline line prices the DOMINANT probed family by measured time per step
-    roof = max(kernels, key=lambda k: k["ms_per_step"]) if kernels else None
+    roof = dict(max(kernels, key=lambda k: k["ms_per_step"])) if kernels else None
+    if roof and "serial" in roof:
+        # the live frac is this family's share of a GPU the concurrent side stream also loads; the
+        # serial one (side stream off) is the kernel's own rate
+        roof["frac_live"] = roof["frac"]
+        roof["frac_serial"] = roof["serial"]["frac"]
+        roof["achieved_serial"] = roof["serial"]["achieved"]
 
     exact = None
     if args.exact_steps > 0 and world == 1:
@@ -347,7 +400,7 @@ def main():
                    "parallelism": f"dp{world}"},
         "tokens_per_gpu_per_s": round(value / world, 1),
         "step_tflops_per_gpu": round(achieved_step_tflops, 2),
-        "step_mfma_frac": round(achieved_step_tflops / PEAK_TFLOPS, 4),
+        "step_mfma_frac": round(step_mfma_frac, 4),
         "train_flops_per_row": flops_row,
         "final_loss": round(final_loss, 4),
         "nonfinite_loss_flags": nonfinite,

@@ -148,8 +148,12 @@ int mmt_probe_read(mmt_ctx* ctx, double* total_ms, int64_t* launches);
 int mmt_probe_read_at(mmt_ctx* ctx, int32_t pattern, double* total_ms, int64_t* launches, double* flops,
                       double* bytes);
 /* Pause (on = 0) / resume (on != 0) the probe's recording without clearing it: the bench samples
- * one step in four, so the probe's event records stay out of the other steps. */
+ * one step in eight, so the probe's event records stay out of the other steps. */
 int mmt_probe_enable(mmt_ctx* ctx, int32_t on);
+/* Serial mode for measurement: on = 0 runs every launch of this context on the caller's stream (no
+ * side stream for the weight gradients and keep bits), on != 0 restores the default. Switch between
+ * training steps only. */
+int mmt_set_side_stream(mmt_ctx* ctx, int32_t on);
 
 /* ---- device-resident batcher: get_batch (training_utils.py:333-384) on HBM token streams ---- */
 /* in-place random walk of one int32 training stream (data_utils.py:342-351 as reached through
@@ -181,7 +185,8 @@ int mmt_exact_gen(void* stream, const uint32_t* mt_state, uint32_t* words, int64
 int mmt_exact_walk(void* stream, int32_t nmod, int32_t* const* data, const int64_t* n, const int32_t* rand_size,
                    const int32_t* vocab, uint32_t* mt_state, const uint32_t* words, int64_t nwords, void* scratch,
                    int64_t scratch_bytes, int32_t* status);
-/* tuning knob: bit 0 / bit 1 = the slice-streamed hs-64 attention dK/dV / dQ pass, bit 2 = dK/dV at 3 waves per SIMD (default 1); returns the old value */
+/* tuning knob: bit 0 / bit 1 = the slice-streamed hs-64 attention dK/dV / dQ pass, bit 2 = dK/dV at 3 waves
+ * per SIMD (default 7); returns the old value */
 int mmt_attn_set_ring(int v);
 
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
@@ -216,7 +221,10 @@ int mmt_op_gemm_ln_bwd(void* stream, int32_t M, int32_t N, int32_t K, const void
                        int32_t ldb, float alpha, const float* x, const float* gamma, const float* mean,
                        const float* rstd, float* dx, void* dx16, float* dgamma, float* dbeta, float* dsum,
                        uint32_t drop_key, uint32_t drop_thr, float drop_scale);
-/* causal attention over nstreams KV streams; layouts as in the engine (row = b*T + t) */
+/* causal attention over nstreams KV streams; layouts as in the engine (row = b*T + t).
+ * lse[j] (float [B*H*T] per stream, written by the forward, read by the backward) is in the LOG2
+ * domain: lse = log2(sum_k 2^(log2(e) * scale * q.k)) = ln(sum_k e^(scale q.k)) / ln 2, with scale =
+ * hs^-0.5 -- a natural-log LSE from another implementation must be divided by ln 2 first. */
 int mmt_op_attention_fwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams,
                          const void* q, int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld,
                          int32_t kv_hstride, void* o, int32_t o_ld, void* const* oj, float* const* lse);

@@ -173,6 +173,10 @@ def run(cfg, data, log=print):
             optimizer.step()
         else:
             log("Warning: Training step losses not calculated, skipping backpropagation")
+    # the device-exact batcher's last walk (the final step's get_batch) is still on the GPU: bring
+    # Python's `random` state and the training lists up to it, as the reference's loop leaves them
+    # (a no-op in the other batcher modes)
+    training_utils.sync_host_state()
     log("\nTRAINING COMPLETED SUCCESSFULLY")
     if cfg["save_model"] == 1:
         os.makedirs(os.path.dirname(model_file_name) or ".", exist_ok=True)

@@ -1,0 +1,6 @@
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+bash tools/gpu_steps.sh \
+ "200|r4a_bench_c1|python -u bench.py --steps 50 --no-cpu-baseline --exact-steps 0" \
+ "200|r4a_bench_target|python -u bench.py --config target --no-cpu-baseline --steps 10 --exact-steps 0" \
+ "200|r4a_gemm|GEMM_BENCH_ONLY=tgt_,sq4k,c4_ffn0_store python -u tools/gemm_bench.py --variants -1 --reps 20" \
+ "300|r4a_prof_ts|MMT_SIDE_STREAM=0 rocprofv3 --kernel-trace --stats -d gpurun_out/r4a_prof_ts -o run -- python3 bench.py --config target --steps 10 --warmup 3 --no-cpu-baseline --exact-steps 0"

@@ -193,11 +193,6 @@ constexpr float kTau = 8.0f;  // lazy-rescale threshold of the forward's running
 #ifndef MMT_FWD_MINB
 #define MMT_FWD_MINB(hs) 2
 #endif
-#ifndef MMT_DQ_KT2
-// hs <= 32 dQ pass: 1 = a second K image for the transposed reads. Measured neutral at C1 (8.943 vs
-// 8.944 ms/step, three same-box pairs: profiles/r3k_dq_kt2_ab.txt): off
-#define MMT_DQ_KT2 0
-#endif
 #ifndef MMT_DQ_MINB
 #define MMT_DQ_MINB(hs) 2
 #endif
@@ -626,21 +621,13 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   const float c2 = scale * kLog2e;
   __shared__ __attribute__((aligned(16))) bf16_t ks[ROWS * G::RW];  // K chunk: row (+ tr at hs > 32) reads
   __shared__ __attribute__((aligned(16))) bf16_t vs[ROWS * G::RW];  // V chunk: row reads
-  // hs <= 32: a second K image at the transposed-read stride (64-B rows: its ds_read_b64_tr_b16 rows
-  // land on distinct banks; at the row-read stride they conflict 2-way — 31 % of the kernel's LDS
-  // cycles in profiles/r3final_sq_c1.txt)
-  constexpr bool KT2 = MMT_DQ_KT2 && HS <= 32;
-  __shared__ __attribute__((aligned(16))) bf16_t kt2[KT2 ? ROWS * G::TW : 8];
-  const bf16_t* kts = KT2 ? kt2 : ks;
-  constexpr int KTS_LD = KT2 ? G::TW : G::RW;
+  const bf16_t* kts = ks;
+  constexpr int KTS_LD = G::RW;
   using MS = MaskStager<HS, ROWS / 32>;
   __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // keep-bit lane words
   if (HS % 32 != 0) {  // pad columns are read only when HS is not a multiple of 32
     for (int q = tid; q < ROWS * G::RW; q += 256)
       if (q % G::RW >= HS) { ks[q] = 0; vs[q] = 0; }
-    if (KT2)
-      for (int q = tid; q < ROWS * G::TW; q += 256)
-        if (q % G::TW >= HS) kt2[q] = 0;
   }
   Stager<HS> st;
   MS mst;
@@ -653,7 +640,6 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
       st.load(P.k[jj] + head * P.kv_hstride, P.kv_ld, P.v[jj] + head * P.kv_hstride, P.kv_ld, rowbase,
               cc * ROWS + rr * SR, T, tid);
       st.store(ks + rr * SR * G::RW, G::RW, vs + rr * SR * G::RW, G::RW, tid);
-      if (KT2) st.store_a(kt2 + rr * SR * G::TW, G::TW, tid);
     }
     if (DROP) mst.store(msk, tid);
   };
@@ -776,9 +762,6 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
   }
 }
 
-#ifndef MMT_DKDV_MINB
-#define MMT_DKDV_MINB 1
-#endif
 // dK, dV: one 32x32 (queries x keys) tile; S, dP recomputed, dV += P^T dO, dK += dS^T Q
 template <int HS, bool MASKED, bool DROP>
 __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, const float* lsl, const float* dsl,
@@ -858,162 +841,6 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
     for (int dt = 0; dt < G::ND; ++dt) {
       dv[dt] = mfma32(pf, dot[s][dt], dv[dt]);
       dk[dt] = mfma32(df, qtr[s][dt], dk[dt]);
-    }
-  }
-}
-
-// =============================================================================================
-// backward dK, dV: grid (ceil(nt/8) * B*H*nstreams, 1, G); wave w owns key tiles ka = 8*bx + w and
-// kb = 8*bx + 7 - w and walks the query tiles of both together (queries >= kb feed both, the
-// ones in [ka, kb) only ka); the Q/dO chunk of the block is staged once per chunk
-// =============================================================================================
-template <int HS, bool DROP>
-__global__ __launch_bounds__(256, MMT_DKDV_MINB) void attn_bwd_dkdv_kernel(AttnBatch batch, int T,
-                                                                                         int H, float scale) {
-  using G = Geo<HS>;
-  constexpr int ROWS = Chunk<HS>::ROWS;
-  const AttnProblem& P = batch.p[blockIdx.z];
-  const int nb = ((T + 31) / 32 + 7) / 8;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int yy = tile / nb, bx = tile % nb;
-  const int nbh = gridDim.x / nb / P.nstreams;
-  if (yy >= nbh * P.nstreams) return;
-  const int j = yy / nbh;
-  const int bh = yy % nbh;
-  const int b = bh / H, head = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int nt = (T + 31) / 32;
-  const int kt0 = bx * 8;
-  const int q_lo = kt0 * 32;
-  const int nch = (T - q_lo + ROWS - 1) / ROWS;
-  const bool ragged = (T & 31) != 0;
-  const int qlast = ragged ? nt - 1 : nt;  // the ragged last query tile (masked); nt: none
-  const int64_t rowbase = (int64_t)b * T;
-  const float c2 = scale * kLog2e;
-  __shared__ __attribute__((aligned(16))) bf16_t qs[ROWS * G::RW];   // Q chunk: row + tr reads
-  __shared__ __attribute__((aligned(16))) bf16_t dos[ROWS * G::RW];  // dO chunk: row + tr reads
-  __shared__ __attribute__((aligned(16))) float lsd[2][ROWS];        // -log2-domain LSE, -D of the chunk rows
-  using MS = MaskStager<HS>;
-  __shared__ __attribute__((aligned(16))) uint32_t msk[DROP ? MS::DWORDS : 4];  // [key tile][chunk q tile]
-  if (HS % 32 != 0)  // pad columns are read only when HS is not a multiple of 32
-    for (int q = tid; q < ROWS * G::RW; q += 256)
-      if (q % G::RW >= HS) { qs[q] = 0; dos[q] = 0; }
-
-  const bf16_t* kp = P.k[j] + head * P.kv_hstride;
-  const bf16_t* vp = P.v[j] + head * P.kv_hstride;
-  const float* lsep = P.lse[j] + (int64_t)bh * T;
-  const float* dvp = P.dvec[j] + (int64_t)bh * T;
-  const bf16_t* qp = P.q + head * HS;
-  const bf16_t* dop = P.dout + head * HS;
-  constexpr int NSL = 2 * ROWS / 256;
-  Stager<HS> st;
-  MS mst;
-  float sl[NSL];
-  auto load = [&](int r0) {
-    st.load(qp, P.q_ld, dop, P.dout_ld, rowbase, r0, T, tid);
-    if (DROP) mst.load(P.dmask[j], bh, nt, kt0, r0 / 32, false, tid);
-#pragma unroll
-    for (int u = 0; u < NSL; ++u) {
-      const int c = tid + 256 * u;
-      const int t = r0 + (c % ROWS);
-      sl[u] = t < T ? ((c < ROWS) ? -lsep[t] : -dvp[t]) : 0.f;  // negated: fma addends
-    }
-  };
-  auto store = [&]() {
-    st.store(qs, G::RW, dos, G::RW, tid);
-    if (DROP) mst.store(msk, tid);
-#pragma unroll
-    for (int u = 0; u < NSL; ++u) {
-      const int c = tid + 256 * u;
-      lsd[c / ROWS][c % ROWS] = sl[u];
-    }
-  };
-  load(q_lo);
-  store();
-  __syncthreads();
-
-  const int ka = kt0 + w, kb = kt0 + 7 - w;  // ka < kb; lb implies la
-  const bool la = ka < nt, lb = kb < nt;
-  const int tka = ka * 32 + r, tkb = kb * 32 + r;
-  const uint32_t* mska = msk + (DROP ? w * MS::KT * 32 : 0);        // keep-bit tiles of ka, kb
-  const uint32_t* mskb = msk + (DROP ? (7 - w) * MS::KT * 32 : 0);  // (chunk tile qt - qt_lo)
-  bf16x8 kfa[G::NKS], vfa[G::NKS], kfb[G::NKS], vfb[G::NKS];
-  f32x16 dka[G::ND], dva[G::ND], dkb[G::ND], dvb[G::ND];
-#pragma unroll
-  for (int s = 0; s < G::NKS; ++s) {
-    const int d0 = 16 * s + 8 * h;
-    const bool oka = la && tka < T && d0 < HS, okb = lb && tkb < T && d0 < HS;
-    kfa[s] = ld8(kp + (rowbase + tka) * P.kv_ld + d0, oka);
-    vfa[s] = ld8(vp + (rowbase + tka) * P.kv_ld + d0, oka);
-    kfb[s] = ld8(kp + (rowbase + tkb) * P.kv_ld + d0, okb);
-    vfb[s] = ld8(vp + (rowbase + tkb) * P.kv_ld + d0, okb);
-  }
-#pragma unroll
-  for (int dt = 0; dt < G::ND; ++dt) { zero16(dka[dt]); zero16(dva[dt]); zero16(dkb[dt]); zero16(dvb[dt]); }
-  for (int c = 0; c < nch; ++c) {
-    const int r0 = q_lo + c * ROWS;
-    const int qt_lo = r0 / 32, qt_hi = min(qt_lo + ROWS / 32, nt) - 1;
-    // per key tile, the diagonal query tile and a ragged last one take the masked variant, peeled
-    // off the plain loop: every accumulator set sees one straight chain of call sites (inlined
-    // variants merging inside a loop made the register allocator copy the dK/dV accumulators
-    // between AGPR sets every iteration)
-    auto tile_a = [&](auto mc, int qt) {
-      dkdv_tile<HS, decltype(mc)::value, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tka, T, kfa, vfa, dka,
-                                               dva, c2, P, mska + (qt - qt_lo) * 32, lane);
-    };
-    auto tile_b = [&](auto mc, int qt) {
-      dkdv_tile<HS, decltype(mc)::value, DROP>(qs, dos, lsd[0], lsd[1], qt * 32 - r0, qt * 32, tkb, T, kfb, vfb, dkb,
-                                               dvb, c2, P, mskb + (qt - qt_lo) * 32, lane);
-    };
-    const std::true_type msk_on;
-    const std::false_type msk_off;
-    if (la) {  // queries in [ka, kb): tile a only
-      const int s_hi = lb ? min(kb - 1, qt_hi) : qt_hi;
-      int qt = max(ka, qt_lo);
-      if (qt == ka && qt <= s_hi) tile_a(msk_on, qt++);
-      const int qe = min(s_hi, qlast - 1);
-#pragma unroll 1
-      for (; qt <= qe; ++qt) tile_a(msk_off, qt);
-      if (qt <= s_hi) tile_a(msk_on, qt);  // qt == qlast
-    }
-    if (lb) {  // queries >= kb: both tiles
-      int qt = max(kb, qt_lo);
-      if (qt == kb && qt <= qt_hi) { tile_a(msk_on, qt); tile_b(msk_on, qt++); }
-      const int qe = min(qt_hi, qlast - 1);
-#pragma unroll 1
-      for (; qt <= qe; ++qt) { tile_a(msk_off, qt); tile_b(msk_off, qt); }
-      if (qt <= qt_hi) { tile_a(msk_on, qt); tile_b(msk_on, qt); }
-    }
-    if (c + 1 < nch) {
-      __syncthreads();
-      load(q_lo + (c + 1) * ROWS);
-      store();
-      __syncthreads();
-    }
-  }
-  // dK/dV tiles: rows = key ((e&3)+8(e>>2)+4h), cols = d (lane)
-  bf16_t* dkp = P.dk[j] + head * P.dkv_hstride;
-  bf16_t* dvo = P.dv[j] + head * P.dkv_hstride;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const bool live = u == 0 ? la : lb;
-    if (!live) continue;
-    const f32x16* dk = u == 0 ? dka : dkb;
-    const f32x16* dv = u == 0 ? dva : dvb;
-    const int k0 = (u == 0 ? ka : kb) * 32;
-#pragma unroll
-    for (int dt = 0; dt < G::ND; ++dt) {
-      const int d = dt * 32 + r;
-      if (d >= HS) continue;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int key = k0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (key < T) {
-          dkp[(rowbase + key) * P.dkv_ld + d] = f2bf(dk[dt][e] * scale);
-          dvo[(rowbase + key) * P.dkv_ld + d] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
-        }
-      }
     }
   }
 }
@@ -1174,8 +1001,7 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
 }
 
 // attention variant knob (bit 0: the slice-streamed hs-64 dK/dV pass, bit 1: its dQ pass, bit 2: the
-// dK/dV pass at 3 waves per SIMD, bits 3 / 4: its 8 / 4 key tiles per workgroup at every T): MMT_ATTN_RING, or
-// mmt_attn_set_ring() for in-process A/B
+// dK/dV pass at 3 waves per SIMD): MMT_ATTN_RING, or mmt_attn_set_ring() for in-process A/B
 static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
   // both hs-64 passes on the rings (dQ: two query tiles per wave), dK/dV at 3 waves per SIMD
@@ -1189,8 +1015,23 @@ extern "C" int mmt_attn_set_ring(int v) {
   return old;
 }
 
+// the slice-streamed hs-64 kernels address a sequence's rows (and one (batch, head)'s keep-bit
+// records) with 32-bit per-lane offsets from a per-batch-row buffer base: a sequence whose span
+// reaches 2^31 bytes takes the chunked kernels (64-bit pointer math) instead
+static bool ring64_fits(const AttnBatch& bt, int T) {
+  const int64_t lim = (int64_t)1 << 31;
+  const int64_t nt = (T + 31) / 32, ntri = nt * (nt + 1) / 2;
+  if (ntri * 128 >= lim) return false;
+  for (int g = 0; g < bt.count; ++g) {
+    const AttnProblem& P = bt.p[g];
+    if ((int64_t)T * P.q_ld * 2 >= lim || (int64_t)T * P.dout_ld * 2 >= lim || (int64_t)T * P.kv_ld * 2 >= lim)
+      return false;
+  }
+  return true;
+}
+
 template <int HS>
-static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
+static hipError_t attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
   const int nb = ((T + 31) / 32 + 7) / 8;
   if (!bwd) {
     bool drop = false;
@@ -1204,34 +1045,23 @@ static void attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, b
     for (int g = 0; g < bt.count; ++g) drop = drop || bt.p[g].drop_thr != 0;
     // hs 64: the slice-streamed kernels (mmt_attn2.hip): bit 1 of the knob the dQ pass, bit 0 the
     // dK/dV pass; MMT_ATTN_RING=0 (or mmt_attn_set_ring(0)) keeps the chunked ones
-    if (HS == 64 && (g_attn_ring & 2)) (void)mmt_attn_bwd_dq_ring64(bt, B, T, H, scale, drop, s);
-    else if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, true>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
+    const bool ring = HS == 64 && ring64_fits(bt, T);
+    if (ring && (g_attn_ring & 2)) {
+      const hipError_t e = mmt_attn_bwd_dq_ring64(bt, B, T, H, scale, drop, s);
+      if (e != hipSuccess) return e;  // (hipGetLastError cleared it: report it here)
+    } else if (drop) hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, true>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<HS, false>), dim3(nb * B * H, 1, bt.count), dim3(256), 0, s, bt, T, H, scale);
-    if (HS == 64 && (g_attn_ring & 1)) {
-      (void)mmt_attn_bwd_dkdv_ring64(bt, B, T, H, scale, drop, g_attn_ring, s);
-      return;
-    }
-    // dK/dV: the paired walk needs 4 accumulator sets (1 wave per SIMD); the single-tile kernel
-    // keeps 2 waves per SIMD and measured faster at hs = 32 (C1: 103 vs 127 us) and, once it fits
-    // hs = 64 without AGPRs, there too (target step 25.9 -> 25.4 ms). MMT_DKDV_PAIR=1 forces the pair
-    static const int pair = [] {
-      const char* e = getenv("MMT_DKDV_PAIR");
-      return e ? atoi(e) : -1;
-    }();
-    const bool paired = pair > 0;
-    if (!paired && drop)
+    if (ring && (g_attn_ring & 1)) return mmt_attn_bwd_dkdv_ring64(bt, B, T, H, scale, drop, g_attn_ring, s);
+    // dK/dV: one key tile per wave at 2 waves per SIMD (a paired two-key-tile walk at one wave per
+    // SIMD measured slower: C1 103 vs 127 us, target step 25.4 vs 25.9 ms; removed in round 4)
+    if (drop)
       hipLaunchKernelGGL((attn_bwd_dkdv1_kernel<HS, true>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H,
                          scale);
-    else if (!paired)
+    else
       hipLaunchKernelGGL((attn_bwd_dkdv1_kernel<HS, false>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T,
                          H, scale);
-    else if (drop)
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HS, true>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T, H,
-                         scale);
-    else
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<HS, false>), dim3(nb * B * H * ns, 1, bt.count), dim3(256), 0, s, bt, T,
-                         H, scale);
   }
+  return hipGetLastError();
 }
 
 static hipError_t attn_dispatch(const AttnBatch& b, int B, int T, int H, int hs, float scale, bool bwd,
@@ -1262,15 +1092,14 @@ static hipError_t attn_dispatch(const AttnBatch& b, int B, int T, int H, int hs,
     }
   }
   switch (hs) {
-    case 8: attn_launch<8>(b, B, T, H, scale, bwd, s); break;
-    case 16: attn_launch<16>(b, B, T, H, scale, bwd, s); break;
-    case 24: attn_launch<24>(b, B, T, H, scale, bwd, s); break;
-    case 32: attn_launch<32>(b, B, T, H, scale, bwd, s); break;
-    case 48: attn_launch<48>(b, B, T, H, scale, bwd, s); break;
-    case 64: attn_launch<64>(b, B, T, H, scale, bwd, s); break;
+    case 8: return attn_launch<8>(b, B, T, H, scale, bwd, s);
+    case 16: return attn_launch<16>(b, B, T, H, scale, bwd, s);
+    case 24: return attn_launch<24>(b, B, T, H, scale, bwd, s);
+    case 32: return attn_launch<32>(b, B, T, H, scale, bwd, s);
+    case 48: return attn_launch<48>(b, B, T, H, scale, bwd, s);
+    case 64: return attn_launch<64>(b, B, T, H, scale, bwd, s);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s) {

@@ -99,7 +99,7 @@ __device__ __forceinline__ int key_dword(int r) { return 2 * ((r & 3) + 4 * (r >
 // Workgroups are ordered heaviest key block first (the causal walk of key block kb is nt - NWV kb
 // slices long) so the launch does not end on a tail of long blocks.
 // =============================================================================================
-template <bool DROP, int OCC, int S, int NWV, bool PAIR = false>
+template <bool DROP, int OCC, int S, int NWV>
 __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch batch, int T, int H, float scale) {
   constexpr int NKS = 4, ND = 2;  // hs 64: 4 k-steps of 16, 2 output tiles of 32
   static_assert(S >= 3 && 4 * (S - 2) <= 16, "ring slots: S - 1 slices in flight, counted waits <= 16");
@@ -160,8 +160,9 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
 
   // DMA sources: Q / dO rows of batch b (rows past T are sent out of range: zeros), the stream's
   // LSE / D rows, the key-major keep-bit records of (query tile, key tiles kt0..kt0+3) (contiguous)
-  const i32x4 rq = make_rsrc(P.q + head * 64, (rowbase + T) * (int64_t)P.q_ld * 2);
-  const i32x4 rdo = make_rsrc(P.dout + head * 64, (rowbase + T) * (int64_t)P.dout_ld * 2);
+  // (each resource starts at batch row b: the 32-bit per-lane offsets span one sequence only)
+  const i32x4 rq = make_rsrc(P.q + rowbase * P.q_ld + head * 64, (int64_t)T * P.q_ld * 2);
+  const i32x4 rdo = make_rsrc(P.dout + rowbase * P.dout_ld + head * 64, (int64_t)T * P.dout_ld * 2);
   const i32x4 rl = make_rsrc(P.lse[j] + (int64_t)bh * T, (int64_t)T * 4);
   const i32x4 rd = make_rsrc(P.dvec[j] + (int64_t)bh * T, (int64_t)T * 4);
   const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
       const int piece = PPW * w + u;  // 0..3: Q column blocks, 4..7: dO
       const int op = piece >> 2, cb = piece & 3;
       const int ld = op ? P.dout_ld : P.q_ld;
-      const int voff = grow < T ? ((int)(rowbase + grow) * ld + cb * 16 + pcol) * 2 : OOB;
+      const int voff = grow < T ? (grow * ld + cb * 16 + pcol) * 2 : OOB;
       dma16(op ? rdo : rq, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_DO + cb * SUB)), voff);
     }
     if (w < 2) {
@@ -193,14 +194,9 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
       dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
     }
   };
-  int nis = 0;  // slices issued so far (uniform)
-  if (PAIR) {
-    for (; nis < S - 1 && nis < nq; ++nis) issue(nis, kt0 + nis);
-  } else {
 #pragma unroll
-    for (int i = 0; i < S - 1; ++i)
-      if (i < nq) issue(i, kt0 + i);
-  }
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nq) issue(i, kt0 + i);
 
   // per-lane read offsets (the slot base and the k step / column block are added as immediates):
   // row reads (lane row r, half h of 16-column block s), transposed reads (tr_frag geometry: rows
@@ -296,32 +292,11 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
   const int n_diag = min(NWV, nq);
   const int n_plain_end = (ragged && nq > 4) ? nq - 1 : nq;
   int i = 0;
-  if (PAIR) {
-    // PAIR: the plain slices two per barrier (their tiles' independent S / dP chains interleave); the
-    // ring refills every slot whose slice is consumed, so slices in flight drop from S - 1 to S - 2
-    auto step_n = [&](int i0, int n, auto mc) {
-      wait_vm(per * (nis - i0 - n));  // this wave's pieces of slices i0 .. i0 + n - 1 landed
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // everyone's landed; every read of slices < i0 is done
-      for (; nis <= i0 + S - 1 && nis < nq; ++nis) issue(nis % S, kt0 + nis);
-      for (int u = 0; u < n; ++u) {
-        const int qt = kt0 + i0 + u;
-        if (live && qt >= kt) tile(lds + ((i0 + u) % S) * SLOT, qt, mc);
-      }
-    };
 #pragma unroll 1
-    for (; i < n_diag; ++i) step_n(i, 1, std::true_type{});
+  for (; i < n_diag; ++i) step(i, std::true_type{});
 #pragma unroll 1
-    for (; i + 1 < n_plain_end; i += 2) step_n(i, 2, std::false_type{});
-    if (i < n_plain_end) { step_n(i, 1, std::false_type{}); ++i; }
-    if (i < nq) step_n(i, 1, std::true_type{});
-  } else {
-#pragma unroll 1
-    for (; i < n_diag; ++i) step(i, std::true_type{});
-#pragma unroll 1
-    for (; i < n_plain_end; ++i) step(i, std::false_type{});
-    if (i < nq) step(i, std::true_type{});
-  }
+  for (; i < n_plain_end; ++i) step(i, std::false_type{});
+  if (i < nq) step(i, std::true_type{});
   __syncthreads();  // the ring is free: the epilogue transposes through it
 
   // dK / dV tiles: accumulator rows = key ((e&3)+8(e>>2)+4h), cols = d (lane); each 32-column slice
@@ -352,205 +327,6 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
   }
 }
 
-// =============================================================================================
-// dQ (and D_j = rowsum(dO * O_j)) at hs 64. grid (nqb * B*H, 1, problems), nqb = ceil(nt / 4): a
-// workgroup owns 4 query tiles (wave w: query tile 4 qb + w, its Q / dO in registers, dQ
-// accumulated in registers over every KV stream) and walks (stream j, key tile 0 .. 4 qb + 3) in
-// lockstep; each key slice (K, V, the 4 query tiles' keep-bit lane words) arrives in an LDS ring
-// slot by LDS-DMA. Per key tile a wave whose query tile is not below it computes S^T = K Q^T,
-// dP^T = V dO^T (queries on lanes), dS^T = P^T (Z dP^T - D), dQ^T += K^T dS^T. Heaviest query block
-// first. The per-stream LSE / D of the block's rows live in a small LDS table.
-// =============================================================================================
-template <bool DROP, int S>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64(AttnBatch batch, int T, int H, float scale) {
-  constexpr int NKS = 4, ND = 2;
-  static_assert(S >= 3 && 3 * (S - 2) <= 16, "ring slots: S - 1 slices in flight, counted waits <= 16");
-  constexpr int OFF_V = IMG64, OFF_M = 2 * IMG64;
-  constexpr int SLOT = OFF_M + (DROP ? 1024 : 0);
-  constexpr int TAB = S * SLOT;  // [wave][stream][query row] {lse2, D} float2
-  __shared__ __attribute__((aligned(1024))) char lds[TAB + 4 * MMT_MAX_STREAMS * 32 * 8];
-  const AttnProblem& P = batch.p[blockIdx.z];
-  const int nt = (T + 31) / 32;
-  const int nqb = (nt + 3) / 4;
-  const int ns = P.nstreams;
-  const int BH = gridDim.x / nqb;
-  const int qb = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (last) query block first
-  const int bh = blockIdx.x % BH;
-  const int b = bh / H, head = bh % H;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int qt = 4 * qb + w;
-  const bool live = qt < nt;
-  const int tq = qt * 32 + r;
-  const bool okq = live && tq < T;
-  const int nk = min(4 * qb + 4, nt);  // key tiles walked per stream
-  const int nsl = ns * nk;             // slices
-  const int64_t rowbase = (int64_t)b * T;
-  const float c2 = scale * kLog2e2;
-  const bool ragged = (T & 31) != 0;
-
-  // Q, dO of this wave's query rows (queries on lanes: the B operands of S^T and dP^T); per stream
-  // D_j = rowsum(dO * O_j) (written for the dK/dV pass) and the LSE into the LDS table
-  bf16x8 qf[NKS], dof[NKS];
-  float* tab = reinterpret_cast<float*>(lds + TAB) + w * (MMT_MAX_STREAMS * 64);
-  {
-    u32x4 qr[NKS], dr[NKS];
-    const bf16_t* qp = P.q + (rowbase + tq) * P.q_ld + head * 64;
-    const bf16_t* dp = P.dout + (rowbase + tq) * P.dout_ld + head * 64;
-    const u32x4 z = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      qr[s] = okq ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * h) : z;
-      dr[s] = okq ? *reinterpret_cast<const u32x4*>(dp + 16 * s + 8 * h) : z;
-    }
-    for (int j = 0; j < ns; ++j) {
-      const bf16_t* oj = (ns > 1 ? P.oj[j] : P.o) + (rowbase + tq) * P.o_ld + head * 64;
-      float d = 0.f;
-#pragma unroll
-      for (int s = 0; s < NKS; ++s) {
-        const u32x4 ov = okq ? *reinterpret_cast<const u32x4*>(oj + 16 * s + 8 * h) : z;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          d += bf2f(ov[e] & 0xffff) * bf2f(dr[s][e] & 0xffff);
-          d += bf2f(ov[e] >> 16) * bf2f(dr[s][e] >> 16);
-        }
-      }
-      d += __shfl_xor(d, 32, 64);
-      const float l2 = okq ? P.lse[j][(int64_t)bh * T + tq] : 0.f;
-      if (h == 0) {
-        if (okq) P.dvec[j][(int64_t)bh * T + tq] = d;
-        tab[j * 64 + 2 * r] = l2;
-        tab[j * 64 + 2 * r + 1] = d;
-      }
-    }
-    // consumed here: the compiler's wait for these loads sits before the DMA prologue
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      asm volatile("" : "+v"(qr[s]));
-      asm volatile("" : "+v"(dr[s]));
-      qf[s] = __builtin_bit_cast(bf16x8, qr[s]);
-      dof[s] = __builtin_bit_cast(bf16x8, dr[s]);
-    }
-  }
-  f32x16 dq[ND];
-#pragma unroll
-  for (int dt = 0; dt < ND; ++dt) zero16(dq[dt]);
-
-  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
-  const int64_t ntiles = (int64_t)BH * ntri;
-  // per-lane source of a sub-image piece: row L/2, half L&1 (swapped on rows with bit 3 set)
-  const int prow = lane >> 1;
-  const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
-  const int per = 2 + (DROP && w == 0 ? 1 : 0);
-  auto issue = [&](int slot, int sl) {
-    char* sb = lds + slot * SLOT;
-    const int j = sl / nk, kt = sl % nk;
-    const int grow = kt * 32 + prow;
-    const i32x4 rk = make_rsrc(P.k[j] + head * P.kv_hstride, (rowbase + T) * (int64_t)P.kv_ld * 2);
-    const i32x4 rv = make_rsrc(P.v[j] + head * P.kv_hstride, (rowbase + T) * (int64_t)P.kv_ld * 2);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int piece = 2 * w + u;  // 0..3: K column block, 4..7: V
-      const int op = piece >> 2, cb = piece & 3;
-      const int voff = grow < T ? ((int)(rowbase + grow) * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
-      dma16(op ? rv : rk, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_V + cb * SUB)), voff);
-    }
-    if (DROP && w == 0) {  // lane words of (query tile 4 qb + u, key tile kt), u = 0..3: 4 x 128 B
-      const i32x4 rm = make_rsrc(P.dmask[j], ntiles * 2 * 32 * 4);
-      const int u = lane >> 3, q_ = 4 * qb + u;
-      const int64_t t = (int64_t)bh * ntri + (int64_t)q_ * (q_ + 1) / 2 + kt;
-      const int voff = (lane < 32 && q_ < nt && kt <= q_) ? (int)((ntiles + t) * 128 + (lane & 7) * 16) : OOB;
-      dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
-    }
-  };
-#pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < nsl) issue(i, i);
-
-  const int o_row = img_off(r, 0, h);
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int o_tr0 = img_off(4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
-  const int o_tr1 = img_off(8 + 4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
-  const float dsc = DROP ? P.drop_scale : 1.f;
-  // one key tile against this wave's query tile; MASKED: the diagonal tile / a ragged tile
-  auto tile = [&](const char* sb, int j, int kt, auto mc) {
-    constexpr bool MASKED = decltype(mc)::value;
-    const uint32_t mw = DROP ? reinterpret_cast<const uint16_t*>(sb + OFF_M)[w * 64 + lane] : 0u;
-    const float l2 = tab[j * 64 + 2 * r], dsum = tab[j * 64 + 2 * r + 1];
-    f32x16 sa, pa;
-    zero16(sa);
-    zero16(pa);
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sb + o_row + s * SUB);
-      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(sb + OFF_V + o_row + s * SUB);
-      sa = mfma32(kf, qf[s], sa);    // S^T[key][q]
-      pa = mfma32(vf, dof[s], pa);   // dP^T[key][q]
-    }
-    bf16x8 ktr[2][ND];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt)
-        ktr[s][dt] = join4(lds_tr16(sb + o_tr0 + 512 * s + 2 * SUB * dt), lds_tr16(sb + o_tr1 + 512 * s + 2 * SUB * dt));
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[e], c2, -l2));
-      if (MASKED) {
-        const int key = kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (key > tq || key >= T) pv = 0.f;
-      }
-      float dp = pa[e];
-      if (DROP) dp = keep_f(dp, __builtin_amdgcn_sbfe((int)mw, (e & 1) * 8 + (e >> 1), 1));
-      sa[e] = pv * __builtin_fmaf(dp, dsc, -dsum);  // dS^T
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const u32x4 v = {pack2bf(sa[8 * s], sa[8 * s + 1]), pack2bf(sa[8 * s + 2], sa[8 * s + 3]),
-                       pack2bf(sa[8 * s + 4], sa[8 * s + 5]), pack2bf(sa[8 * s + 6], sa[8 * s + 7])};
-      const bf16x8 df = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt) dq[dt] = mfma32(ktr[s][dt], df, dq[dt]);
-    }
-  };
-  // per stream: the plain key tiles 0 .. 4 qb - 1 (all below every wave's diagonal; the last one
-  // masked when T is ragged and it is the sequence's last tile), then the block's 4 diagonal tiles
-  // masked (each wave its own diagonal; tiles above it skipped)
-  auto step = [&](int i, auto mc) {
-    wait_vm(per * min(S - 2, nsl - 1 - i));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (i + S - 1 < nsl) issue((i + S - 1) % S, i + S - 1);
-    const int j = i / nk, kt = i % nk;
-    if (live && kt <= qt) tile(lds + (i % S) * SLOT, j, kt, mc);
-  };
-  int i = 0;
-  for (int j = 0; j < ns; ++j) {
-    const int nplain = min(4 * qb, nk);
-#pragma unroll 1
-    for (int kt = 0; kt < nplain; ++kt, ++i) step(i, std::false_type{});
-#pragma unroll 1
-    for (int kt = nplain; kt < nk; ++kt, ++i) step(i, std::true_type{});
-  }
-  // 16-B stores of 8 consecutive d per lane after a v_permlane32_swap exchange of the row halves
-  // (the swaps run on every lane: both halves of a row are live or dead together)
-#pragma unroll
-  for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      const int ga = 2 * pr, gb = 2 * pr + 1;
-      const uint32_t x0 = pack2bf(dq[dt][4 * ga] * scale, dq[dt][4 * ga + 1] * scale);
-      const uint32_t x1 = pack2bf(dq[dt][4 * ga + 2] * scale, dq[dt][4 * ga + 3] * scale);
-      const uint32_t y0 = pack2bf(dq[dt][4 * gb] * scale, dq[dt][4 * gb + 1] * scale);
-      const uint32_t y1 = pack2bf(dq[dt][4 * gb + 2] * scale, dq[dt][4 * gb + 3] * scale);
-      const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
-      const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-      const int d0 = dt * 32 + 16 * pr + 8 * h;
-      if (okq)
-        *reinterpret_cast<u32x4*>(P.dq + (rowbase + tq) * P.dq_ld + head * 64 + d0) = u32x4{s0[0], s1[0], s0[1], s1[1]};
-    }
-}
-
 
 // =============================================================================================
 // dQ (and D_j) at hs 64, two query tiles per wave. grid (nqb * B*H, 1, problems), nqb = ceil(nt / 8):
@@ -558,7 +334,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64(AttnBatch batch, in
 // so every wave's causal walk is equally long) and walks (stream j, key tile 0 .. 8 qb + 7) through
 // the LDS ring; a wave reads each slice's K / V fragments (rows and K transposed) ONCE and runs both
 // of its query tiles on them: half the fragment reads, DMA pieces and barriers per MFMA of the
-// one-tile kernel above. Diagonal tiles are masked at run time (a uniform branch around the mask).
+// walk with one tile per wave. Diagonal tiles are masked at run time (a uniform branch around the mask).
 // =============================================================================================
 template <bool DROP, int S>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, int T, int H, float scale) {
@@ -646,20 +422,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
     char* sb = lds + slot * SLOT;
     const int j = sl / nk, kt = sl % nk;
     const int grow = kt * 32 + prow;
-    const i32x4 rk = make_rsrc(P.k[j] + head * P.kv_hstride, (rowbase + T) * (int64_t)P.kv_ld * 2);
-    const i32x4 rv = make_rsrc(P.v[j] + head * P.kv_hstride, (rowbase + T) * (int64_t)P.kv_ld * 2);
+    const i32x4 rk = make_rsrc(P.k[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+    const i32x4 rv = make_rsrc(P.v[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int piece = 2 * w + u;  // 0..3: K column block, 4..7: V
       const int op = piece >> 2, cb = piece & 3;
-      const int voff = grow < T ? ((int)(rowbase + grow) * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
+      const int voff = grow < T ? (grow * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
       dma16(op ? rv : rk, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_V + cb * SUB)), voff);
     }
     if (DROP && w == 0) {  // lane words of (query tile 8 qb + u, key tile kt), u = 0..7: 8 x 128 B
-      const i32x4 rm = make_rsrc(P.dmask[j], ntiles * 2 * 32 * 4);
+      const i32x4 rm = make_rsrc(P.dmask[j] + (ntiles + (int64_t)bh * ntri) * 32, ntri * 128);
       const int u = lane >> 3, q_ = 8 * qb + u;
-      const int64_t t = (int64_t)bh * ntri + (int64_t)q_ * (q_ + 1) / 2 + kt;
-      const int voff = (q_ < nt && kt <= q_) ? (int)((ntiles + t) * 128 + (lane & 7) * 16) : OOB;
+      const int voff = (q_ < nt && kt <= q_) ? (q_ * (q_ + 1) / 2 + kt) * 128 + (lane & 7) * 16 : OOB;
       dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
     }
   };
@@ -754,85 +529,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
       }
 }
 
-// ring depth knob (slots; S - 1 slices in flight): MMT_ATTN_RING_SLOTS = 4 (default) or 6
-static int ring_slots() {
-  static const int v = [] {
-    const char* e = getenv("MMT_ATTN_RING_SLOTS");
-    return e ? atoi(e) : 4;
-  }();
-  return v;
-}
-
-// dQ ring variant: MMT_ATTN_DQ_X2 = 1 (default) two query tiles per wave, 0 one
-static const int g_dq_x2 = [] {
-  const char* e = getenv("MMT_ATTN_DQ_X2");
-  return e ? atoi(e) : 1;
-}();
-
+// ring depth 4 (three slices in flight): depth 6 measured slower (target backward 294 -> 301 us, C4
+// 2315 -> 2394 us: profiles/r3e_ring_slots_ab.txt); a one-query-tile-per-wave dQ ring equal at the
+// target and slower at C3, 8 key tiles per dK/dV workgroup slower at C3 / C4
+// (profiles/r3h_dkdv_waves_ab.txt), two plain dK/dV slices per barrier slower at C3 / C4
+// (profiles/r3u_ring_ab.txt): those variants were removed in round 4.
 hipError_t mmt_attn_bwd_dq_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, hipStream_t s) {
   const int nt = (T + 31) / 32;
-  const int nqb = (nt + 3) / 4;
-  const dim3 grid(nqb * B * H, 1, bt.count);
-  const bool deep = ring_slots() >= 6;
-  if (g_dq_x2) {  // two query tiles per wave (8 per workgroup)
-    const dim3 g2(((nt + 7) / 8) * B * H, 1, bt.count);
-    if (drop) hipLaunchKernelGGL((attn_bwd_dq_ring64x2<true, 4>), g2, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dq_ring64x2<false, 4>), g2, dim3(256), 0, s, bt, T, H, scale);
-    return hipGetLastError();
-  }
-  if (drop) {
-    if (deep) hipLaunchKernelGGL((attn_bwd_dq_ring64<true, 6>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dq_ring64<true, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
-  } else {
-    if (deep) hipLaunchKernelGGL((attn_bwd_dq_ring64<false, 6>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dq_ring64<false, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
-  }
+  const dim3 g2(((nt + 7) / 8) * B * H, 1, bt.count);  // two query tiles per wave (8 per workgroup)
+  if (drop) hipLaunchKernelGGL((attn_bwd_dq_ring64x2<true, 4>), g2, dim3(256), 0, s, bt, T, H, scale);
+  else hipLaunchKernelGGL((attn_bwd_dq_ring64x2<false, 4>), g2, dim3(256), 0, s, bt, T, H, scale);
   return hipGetLastError();
 }
 
-template <int S, int NWV>
-static void dkdv_launch(const AttnBatch& bt, dim3 grid, int T, int H, float scale, bool drop, bool occ3, hipStream_t s) {
-  const dim3 blk(64 * NWV);
-  if (occ3) {  // 3 waves per SIMD (<= 168 VGPRs)
-    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 3, S, NWV>), grid, blk, 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 3, S, NWV>), grid, blk, 0, s, bt, T, H, scale);
-  } else {
-    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2, S, NWV>), grid, blk, 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2, S, NWV>), grid, blk, 0, s, bt, T, H, scale);
-  }
-}
-
-// key tiles per dK/dV workgroup: MMT_ATTN_DKDV_WAVES = 4 or 8 (8: half the query-slice DMA and L2
-// traffic per key, longer diagonal ramp); default 4: 8 measured slower (C3 cross-attention backward
-// 2483 -> 2709 us, C4 2270 -> 2364 us, C3 step +1.5 %: profiles/r3h_dkdv_waves_ab.txt); kept as a knob
-// (MMT_ATTN_DKDV8_TMIN: 8 from that T on)
-static int dkdv_waves(int T) {
-  static const int env = [] {
-    const char* e = getenv("MMT_ATTN_DKDV_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  static const int tmin = [] {
-    const char* e = getenv("MMT_ATTN_DKDV8_TMIN");
-    return e ? atoi(e) : (1 << 30);
-  }();
-  if (env == 4 || env == 8) return env;
-  return T >= tmin ? 8 : 4;
-}
-
+// variant bit 2: 3 waves per SIMD (<= 168 VGPRs; the default), else 2
 hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, int variant,
                                     hipStream_t s) {
   const int nt = (T + 31) / 32;
   const bool occ3 = (variant & 4) != 0;
-  const int nwv = (variant & 8) ? 8 : (variant & 16) ? 4 : dkdv_waves(T);
-  const int nkb = (nt + nwv - 1) / nwv;
-  const dim3 grid(nkb * B * H * bt.p[0].nstreams, 1, bt.count);
-  if (variant & 32) {  // two plain slices per barrier on a 6-slot ring
-    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2, 6, 4, true>), grid, dim3(256), 0, s, bt, T, H, scale);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2, 6, 4, true>), grid, dim3(256), 0, s, bt, T, H, scale);
-    return hipGetLastError();
+  const dim3 grid(((nt + 3) / 4) * B * H * bt.p[0].nstreams, 1, bt.count);
+  if (occ3) {
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 3, 4, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 3, 4, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
+  } else {
+    if (drop) hipLaunchKernelGGL((attn_bwd_dkdv_ring64<true, 2, 4, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_ring64<false, 2, 4, 4>), grid, dim3(256), 0, s, bt, T, H, scale);
   }
-  if (nwv == 8) dkdv_launch<4, 8>(bt, grid, T, H, scale, drop, occ3, s);
-  else if (ring_slots() >= 6) dkdv_launch<6, 4>(bt, grid, T, H, scale, drop, occ3, s);
-  else dkdv_launch<4, 4>(bt, grid, T, H, scale, drop, occ3, s);
   return hipGetLastError();
 }

@@ -155,6 +155,7 @@ struct mmt_ctx {
   // them) run there, overlapping the latency-bound data-gradient kernels; joined at stage ends
   hipStream_t side = nullptr;
   int side_device = -1;
+  bool side_off = false;  // mmt_set_side_stream(ctx, 0): this context runs everything on the caller's stream
   std::vector<hipEvent_t> evpool;
   size_t evnext = 0;
   int d16 = 0;  // rotation index of the current dres16 copy (reset at backward stage 0)
@@ -701,8 +702,9 @@ struct Runner {
     }
   }
   // fork the side stream off the main one (everything enqueued on `s` so far happens first)
+  hipStream_t side_stream() const { return c->side_off ? nullptr : c->side; }
   hipStream_t side() {
-    if (!c->side) return s;
+    if (!side_stream()) return s;
     hipEvent_t e = c->evpool[c->evnext++ % c->evpool.size()];
     ok(hipEventRecord(e, s), "event record");
     ok(hipStreamWaitEvent(c->side, e, 0), "stream wait");
@@ -711,7 +713,7 @@ struct Runner {
   // the main stream waits for everything enqueued on the side stream
   void join() {
     flush();
-    if (!c->side) return;
+    if (!side_stream()) return;
     hipEvent_t e = c->evpool[c->evnext++ % c->evpool.size()];
     ok(hipEventRecord(e, c->side), "event record");
     ok(hipStreamWaitEvent(s, e, 0), "stream wait");
@@ -723,7 +725,7 @@ struct Runner {
   std::vector<std::pair<GemmBatch, const char*>> pend;
   void flush() {
     if (pend.empty() || rc != MMT_OK) { pend.clear(); return; }
-    hipStream_t ss = c->side ? side() : s;
+    hipStream_t ss = side_stream() ? side() : s;
     // merge consecutive queued weight-gradient batches of the same tile kind into one launch (up
     // to MMT_MAX_GROUP problems): more tiles per launch -> fewer K splits -> fewer partial bytes
     std::vector<std::pair<GemmBatch, std::string>> merged;
@@ -1582,24 +1584,10 @@ void ensure_side(mmt_ctx* c) {
   // MMT_SIDE_PRIORITY (optional): HIP stream priority of the side stream (lower = higher priority,
   // clamped to the device's range); unset = default priority
   static const char* prio_env = getenv("MMT_SIDE_PRIORITY");
-  // MMT_SIDE_CUS (optional): confine the side stream to N of the device's CUs (a CU mask spread evenly
-  // over the XCDs whether the mask bits map to CUs XCD-major or round-robin), so the weight gradients
-  // and keep-bit hashing never take more than N CUs from the main stream's chain
-  static const int side_cus = [] {
-    const char* e = getenv("MMT_SIDE_CUS");
-    return e ? atoi(e) : 0;
-  }();
+  // (a CU-masked side stream measured far slower -- it cannot be created non-blocking, so it
+  // serialises against the caller's stream: profiles/r3q_side_cumask_ab.txt; removed in round 4)
   hipError_t ce;
-  int ncu = 0;
-  if (side_cus > 0) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (side_cus > 0 && ncu > 0 && side_cus < ncu && ncu % 8 == 0) {
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    const int stride = std::max(1, ncu / side_cus);
-    int set = 0;
-    for (int i = 0; i < ncu && set < side_cus; ++i)
-      if (((i % 8) + (i / 8)) % stride == 0) { mask[i / 32] |= 1u << (i % 32); ++set; }
-    ce = hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data());
-  } else if (prio_env) {
+  if (prio_env) {
     int least = 0, greatest = 0;
     (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
     const int pr = std::max(greatest, std::min(least, atoi(prio_env)));
@@ -1821,6 +1809,15 @@ extern "C" int mmt_set_dropout_seed(mmt_ctx* c, uint64_t seed) {
 // live per-kernel timing: HIP events around every launch whose label matches one of the
 // comma-separated patterns of `label` (e.g. "*_dw,attn_fwd,attn_bwd,ffn0"), recorded on the stream
 // the launch runs on, so bench.py can price kernels inside the timed region.
+// serial mode for measurement (bench.py's serial roofline leg): 0 = everything of this context on the
+// caller's stream, 1 = the side stream again; switch between steps only (a backward joins the side
+// stream its forward forked)
+extern "C" int mmt_set_side_stream(mmt_ctx* c, int32_t on) {
+  if (!c) return MMT_ERR_INVALID;
+  c->side_off = on == 0;
+  return MMT_OK;
+}
+
 extern "C" int mmt_probe_set(mmt_ctx* c, const char* label) {
   if (!c) return MMT_ERR_INVALID;
   c->probe_events.clear();

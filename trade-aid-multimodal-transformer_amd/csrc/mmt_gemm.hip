@@ -43,12 +43,6 @@ using TileL = TileCfg<2, 4, 4, 2>;
 // 128 x 512, 8 waves (1 x 8) of 128 x 64 (TileL's per-wave shape): whole 512-wide rows per block for
 // the fused LayerNorm-backward epilogue at C = 512 (BK 32 x 2 stages = 80 KiB of ring)
 using TileW = TileCfg<1, 8, 4, 2>;
-// 128 x 256, 4 waves (1 x 4) of 128 x 64: whole 256-wide rows at twice the blocks of TileL, two
-// blocks per CU, so one block's LayerNorm epilogue (HBM-bound) overlaps another's K loop
-using TileH = TileCfg<1, 4, 4, 2>;
-// 256 x 128, 4 waves (2 x 2) of 128 x 64 (TileL's per-wave shape: 0.75 fragment reads per MFMA
-// instead of TileS's 1) at two blocks per CU (variants 7 / 8 of the short-K path)
-using TileM = TileCfg<2, 2, 4, 2>;
 
 // tuning knob (mmt_gemm_set_variant): pipeline variant of the forward / backward-data GEMMs in
 // bits 0-3 and of the weight-grad (split-K, atomic) GEMMs in bits 4-7:
@@ -58,7 +52,7 @@ static int g_gemm_variant = -1;     // forward / backward-data (-1: per-epilogue
 static int g_gemm_variant_dw = 0;   // weight grad (split-K atomic)
 extern "C" int mmt_gemm_set_variant(int v) {
   if (v < 0) { g_gemm_variant = -1; g_gemm_variant_dw = 0; return 0; }  // back to the default policy
-  if ((v & 15) > 8 || ((v >> 4) & 15) > 6) return -1;
+  if ((v & 15) > 6 || ((v >> 4) & 15) > 6) return -1;
   g_gemm_variant = v & 15;
   g_gemm_variant_dw = (v >> 4) & 15;
   return 0;
@@ -875,20 +869,11 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     const char* e = getenv("MMT_GEMM_DW_VARIANT");
     return e ? atoi(e) : -1;
   }();
-  // MMT_GEMM_TILEM=1: the bias+ReLU forward (ffn0) at K >= 512 (target / C3) on the 256 x 128 tile
-  // (TileM, 2 blocks per CU). Standalone 214 -> 194 us at the target (the other short-K shapes slower:
-  // profiles/r3x_gemm_tilem.txt), but in the step beside the side stream 20.21 -> 20.37 ms at the
-  // target, C3 neutral (profiles/r3y_tilem_ab.txt): off by default
-  static const int tilem = [] {
-    const char* e = getenv("MMT_GEMM_TILEM");
-    return e ? atoi(e) : 0;
-  }();
-  int kmax = 0;
-  for (int g = 0; g < b.count; ++g) kmax = std::max(kmax, b.p[g].K);
-  const bool relu_wide = tilem && EPI == EPI_BIAS_RELU_BF16 && A_KC && B_KC && kmax >= 512;
+  // (a 256 x 128 tile at two blocks per CU won standalone on the target ffn0, 214 -> 194 us, but not in
+  // the step beside the side stream, 20.21 -> 20.37 ms: profiles/r3y_tilem_ab.txt; removed in round 4)
   const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw
                   : (!A_KC && !B_KC && env_dw >= 0) ? env_dw
-                  : (g_gemm_variant >= 0 ? g_gemm_variant : relu_wide ? 7 : occ3 ? 6 : 0);
+                  : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? 6 : 0);
   switch (var) {
     case 1: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 2: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
@@ -896,20 +881,6 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     case 4: launch_v<TileS, 64, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 5: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
     case 6: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
-    case 7:
-    case 8: {
-      if constexpr (SWAP) {  // 256 x 128 tile: its own grid
-        const int mtm = max_tiles<TileM>(b, nullptr);
-        if (mtm == 0) return hipSuccess;
-        const dim3 gm(mtm, grid.y, grid.z);
-        // two blocks per CU (8 waves): the launch bound caps the registers at 256 per lane
-        if (var == 7) launch_v<TileM, 32, 2, A_KC, B_KC, SWAP, EPI, 2>(b, gm, s);
-        else launch_v<TileM, 64, 2, A_KC, B_KC, SWAP, EPI, 2>(b, gm, s);
-      } else {
-        launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s);
-      }
-      break;
-    }
     default: launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
   }
   return hipGetLastError();
@@ -1126,42 +1097,26 @@ bool mmt_gemm_ln_bwd_ok(const GemmBatch& b) {
     const GemmProblem& P = b.p[g];
     if ((P.N != TileL::BN && P.N != TileW::BN) || P.N != b.p[0].N || !P.resid || !P.o32 || !P.ln_gamma || !P.ln_mean || !P.ln_rstd || !P.ln_dgamma ||
         !P.ln_dbeta || (P.ldc & 3) || (P.ldres & 3) || (P.o16 && (P.ldo16 & 7)) || (P.lda & 7) || (P.ldb & 7) ||
-        (((uintptr_t)P.A | (uintptr_t)P.B | (uintptr_t)P.o32 | (uintptr_t)P.resid | (uintptr_t)P.ln_gamma) & 15))
+        (((uintptr_t)P.A | (uintptr_t)P.B | (uintptr_t)P.o32 | (uintptr_t)P.resid | (uintptr_t)P.ln_gamma |
+          (uintptr_t)P.o16) & 15))  // (o16: the epilogue's 16-B dropout-masked copy stores)
       return false;
   }
   return true;
 }
 
-// tile of the fused LayerNorm backward at C = 256: MMT_LNB_TILE = 0 (default) 256 x 256, 1 128 x 256
-// (twice the blocks, two per CU: measured slower, C1 4-problem launches 63.7 -> 92.9 us, step
-// 9.11 -> 9.29 ms: profiles/r3i_lnb_tile_ab.txt)
-static const int g_lnb_tile = [] {
-  const char* e = getenv("MMT_LNB_TILE");
-  return e ? atoi(e) : 0;
-}();
-
 hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
   if (!mmt_gemm_ln_bwd_ok(b)) return hipErrorInvalidValue;
   // a tile as wide as the row, whatever K: its block owns whole rows of the LayerNorm (C = 256:
-  // 256 x 256; C = 512: 128 x 512)
+  // 256 x 256; C = 512: 128 x 512 at BK 32 x 2 stages = 80 KiB of ring; BK 64 measured neutral, a
+  // 128 x 256 tile at C = 256 slower: 63.7 -> 92.9 us per launch, profiles/r3i_lnb_tile_ab.txt)
   if (b.p[0].N == TileW::BN) {
     const int mt = max_tiles<TileW>(b, nullptr);
     if (mt == 0) return hipSuccess;
-    // K-step: 32 (80 KiB ring) or, MMT_LNB_W_BK=64, 64 (the whole 160 KiB of LDS, half the barriers)
-    static const int bk = [] {
-      const char* e = getenv("MMT_LNB_W_BK");
-      return e ? atoi(e) : 32;
-    }();
-    if (bk == 64) launch_v<TileW, 64, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
-    else launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
-  } else if (g_lnb_tile == 0) {
+    launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+  } else {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
     launch_v<TileL, 64, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
-  } else {
-    const int mt = max_tiles<TileH>(b, nullptr);
-    if (mt == 0) return hipSuccess;
-    launch_v<TileH, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
   }
   return hipGetLastError();
 }

@@ -71,6 +71,7 @@ _SIGS = {
     "mmt_probe_set": (c_i32, [c_vp, c_cp]),
     "mmt_probe_read": (c_i32, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
     "mmt_probe_enable": (c_i32, [c_vp, c_i32]),
+    "mmt_set_side_stream": (c_i32, [c_vp, c_i32]),
     "mmt_probe_count": (c_i32, [c_vp]),
     "mmt_probe_read_at": (c_i32, [c_vp, c_i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64),
                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
