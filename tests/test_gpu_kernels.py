@@ -431,6 +431,40 @@ def test_qkv2(R, H, hs):
     assert rel(dw2, wr.grad) < 1e-4
 
 
+@pytest.mark.parametrize("M,H,hs,K", [(1000, 8, 32, 256), (300, 2, 64, 72), (512, 8, 64, 1024), (77, 1, 32, 48),
+                                     (16384 // 32, 8, 64, 512)])
+def test_gemm_qkv_fused(M, H, hs, K):
+    """Q/K/V stage 1 GEMM with the per-head stage 2 fused into its epilogue (mmt_op_gemm_qkv; the
+    engine's forward at hs 32 / 64) against torch: h1 = tanh(X W1^T + b1), out = block-diagonal
+    [hs/2 -> hs] maps of bf16(h1); the 128 x 128 and (M, N >= 256, K >= 1024) 256 x 256 tiles, a
+    partial last column block (N = 48) and ragged rows."""
+    torch.manual_seed(M + H + hs + K)
+    hh = hs // 2
+    N = 3 * H * hh
+    lda = r8(K)
+    X = torch.randn(M, K, device=DEV)
+    W1 = torch.randn(N, K, device=DEV) / K ** 0.5
+    b1 = torch.randn(N, device=DEV) * 0.3
+    w2 = torch.randn(N // hh, hs, hh, device=DEV) * 0.2
+    Xb, Wb = bf(pad_cols(X, lda)), bf(pad_cols(W1, lda))
+    ldh1, ldo = r8(N), 2 * N
+    h1 = torch.zeros(M, ldh1, dtype=torch.bfloat16, device=DEV)
+    out = torch.zeros(M, ldo, dtype=torch.bfloat16, device=DEV)
+    L = ML.lib()
+    assert L.mmt_op_gemm_qkv(_s(), M, N, K, ML.ptr(Xb), lda, ML.ptr(Wb), lda, ML.ptr(b1), ML.ptr(h1), ldh1, ML.ptr(w2),
+                             hh, ML.ptr(out), ldo) == 0
+    _sync()
+    ref_h1 = torch.tanh(Xb.float()[:, :K] @ Wb.float()[:, :K].t() + b1)
+    assert rel(h1[:, :N], ref_h1) < 1e-2
+    assert (h1[:, N:] == 0).all()  # pad columns of the next GEMM's operand stay zero
+    ref = torch.einsum("rbi,boi->rbo", h1.float()[:, :N].view(M, N // hh, hh), bf(w2).float())
+    assert rel(out.view(M, N // hh, hs), ref) < 1e-2
+    # head sizes whose stage-1 block is not 16 / 32 columns are refused (the engine keeps qkv2_fwd)
+    if hs == 32:
+        assert L.mmt_op_gemm_qkv(_s(), M, 3 * H * 8, K, ML.ptr(Xb), lda, ML.ptr(Wb), lda, ML.ptr(b1), ML.ptr(h1), ldh1,
+                                 ML.ptr(w2), 8, ML.ptr(out), ldo) == -2
+
+
 @pytest.mark.parametrize("R,N,ld", [(16384, 1024, 1024), (1000, 450, 456), (77, 13, 16), (300, 6, 8)])
 def test_colsum(R, N, ld):
     x = bf(torch.randn(R, ld, device=DEV))

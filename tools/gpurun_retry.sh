@@ -4,7 +4,7 @@
 # announces ("retry in Ns"). A GPU step that ran and failed is never resubmitted.
 # usage: tools/gpurun_retry.sh <logfile> <timeout> <command>
 log="$1"; to="$2"; shift 2
-for attempt in 1 2 3 4 5 6; do
+for attempt in $(seq 1 ${GPURUN_ATTEMPTS:-30}); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@" > "$log" 2>&1
   rc=$?
   if [ $rc -ne 3 ] && ! grep -q 'status=transient rc=None' "$log"; then

@@ -871,18 +871,32 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
     std::fill(ln1_done.begin(), ln1_done.end(), 0);
     lb.count = M;
     GemmBatch g{}; g.count = M;
+    // per-head stage 2 (model.py:39, 44, 49) fused into the stage-1 GEMM's epilogue at hs 32 / 64
+    // (qkv2_fused), else its own launch; MMT_QKV2_FUSE=0 keeps the separate kernel
+    static const bool qkv2_fuse = [] {
+      const char* e = getenv("MMT_QKV2_FUSE");
+      return e ? atoi(e) != 0 : true;
+    }();
+    const bool fuse_qkv2 = qkv2_fuse && (c->hh == 16 || c->hh == 32);
     for (int i = 0; i < M; ++i) {
       g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].a8), C, r.W<uint8_t>(a[i].as8), ldsC, w8, x[i].W1, R)
                   : gp_fwd(r.W<bf16_t>(a[i].a), C, wpk, x[i].W1, R);
       g.p[i].bias = r.P(x[i].b1); g.p[i].o16 = r.W<bf16_t>(a[i].h1); g.p[i].ldo16 = ldh1;
+      if (fuse_qkv2) {
+        g.p[i].qkv2_w2 = r.P(x[i].w2); g.p[i].qkv2_out = r.W<bf16_t>(a[i].qkv);
+        g.p[i].qkv2_ld = 3 * C; g.p[i].qkv2_hh = c->hh;
+      }
     }
     if (f8) r.gemm8(g, EPI_BIAS_TANH_BF16, "qkv1");
     else r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "qkv1");
-    Qkv2Batch qb{}; qb.count = M;
-    for (int i = 0; i < M; ++i) {
-      qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].out = r.W<bf16_t>(a[i].qkv);
+    for (int i = 0; i < M; ++i) g.p[i].qkv2_out = nullptr;  // g is reused by the next GEMMs
+    if (!fuse_qkv2) {
+      Qkv2Batch qb{}; qb.count = M;
+      for (int i = 0; i < M; ++i) {
+        qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].out = r.W<bf16_t>(a[i].qkv);
+      }
+      r.ok(mmt_launch_qkv2_fwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_fwd");
     }
-    r.ok(mmt_launch_qkv2_fwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_fwd");
     AttnBatch ab{}; ab.count = M;
     for (int i = 0; i < M; ++i) {
       AttnProblem& q = ab.p[i];

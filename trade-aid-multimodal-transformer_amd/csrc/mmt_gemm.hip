@@ -144,14 +144,15 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int sb, int s, int lane)
 }
 
 // one output element; returns the value stored (the bias-gradient column sum adds it up)
-template <int EPI>
+// PRE: the activation (alpha, bias, tanh) was already applied to the accumulators (qkv2_fused)
+template <int EPI, bool PRE = false>
 __device__ __forceinline__ float epi_scalar(const GemmProblem& P, float* o32, float alpha, int m, int n, float v) {
-  float r = alpha * v;
-  if (EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
-      EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16) {
+  float r = PRE ? v : alpha * v;
+  if (!PRE && (EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
+               EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16)) {
     if (P.bias) r += P.bias[n];
   }
-  if (EPI == EPI_BIAS_TANH_BF16) r = fast_tanh(r);
+  if (!PRE && EPI == EPI_BIAS_TANH_BF16) r = fast_tanh(r);
   if (EPI == EPI_BIAS_RELU_BF16) r = fmaxf(r, 0.0f);
   if (EPI == EPI_DTANH_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r *= (1.0f - t * t); }
   if (EPI == EPI_DRELU_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r = t > 0.0f ? r : 0.0f; }
@@ -199,7 +200,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 // so every global access is 16 B per lane (bf16 x 8, or 2 x f32x4) and GBN/8 lanes cover one row
 // segment. 16-B stores halve the store instructions of the 8-B form (the epilogue of a short-K tile
 // is store-issue bound). Starts with a barrier (the caller's LDS reads of `ct` must be done).
-template <class TL, int EPI, int EPI_ROWS>
+template <class TL, int EPI, int EPI_ROWS, bool PRE = false>
 __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc)[TL::TN][TL::TM], char* lds,
                                               float* o32, float alpha, int m0, int n0, int tid, int lane, int wave) {
   constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
@@ -221,8 +222,8 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
   const int n = n0 + 8 * c8;
   constexpr bool HAS_AUX = EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
   constexpr bool HAS_RES = EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32;
-  constexpr bool HAS_BIAS = EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_RESID_F32 ||
-                            EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16;
+  constexpr bool HAS_BIAS = !PRE && (EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 ||
+                                     EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32 || EPI == EPI_STORE_BF16);
   // fused bias gradient (bf16-output epilogues): column sums of the stored values
   constexpr bool CAN_DB = EPI == EPI_STORE_BF16 || EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
   // MX-fp8 copy of a forward activation (P.o8; needs N % 32 == 0 and the vector path)
@@ -365,10 +366,10 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
         float r[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          r[e] = alpha * v0[e] + bias0[e];
-          r[e + 4] = alpha * v1[e] + bias1[e];
+          r[e] = PRE ? v0[e] : alpha * v0[e] + bias0[e];
+          r[e + 4] = PRE ? v1[e] : alpha * v1[e] + bias1[e];
         }
-        if (EPI == EPI_BIAS_TANH_BF16) {
+        if (!PRE && EPI == EPI_BIAS_TANH_BF16) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) r[e] = fast_tanh(r[e]);
         }
@@ -474,7 +475,7 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float v = ct[ml * CT + 8 * c8 + e];
-          if (n + e < N) cs[e] += epi_scalar<EPI>(P, o32, alpha, m, n + e, v);
+          if (n + e < N) cs[e] += epi_scalar<EPI, PRE>(P, o32, alpha, m, n + e, v);
           else epi_pad<EPI>(P, m, n + e);
         }
       }
@@ -506,6 +507,97 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
   if constexpr (LNB) {
     flush_colsums(cg, P.ln_dgamma);
     flush_colsums(cb, P.ln_dbeta);
+  }
+}
+
+// Per-head Q/K/V stage 2 fused into the stage-1 GEMM's epilogue (reference model.py:36-50,
+// each head's key / query / value = Linear(hs/2, hs, no bias) of tanh(Linear(C, hs/2))). acc holds
+// this wave's TN x TM 32x32 sub-tiles of h1^T (stage-1 column n on accumulator rows, row m on lanes).
+// First, in place, acc = h1 = tanh(alpha acc + bias) (what the epilogue then stores as o16, PRE).
+// Each hh-wide column block blk of h1 (hh = 16 or 32) is one head's K, Q or V stage-1 output; its
+// stage 2 out[m][blk*2hh + o] = sum_k W2[blk][o][k] h1[m][blk*hh + k] runs on MFMA straight from
+// the accumulator registers: lane (r, h) holds h1[r][4h + 0..3] and h1[r][8 + 4h + 0..3] of a
+// 16-column block (accumulator groups g and g + 1), which is a K-16 B operand with K permuted
+// (slot j <-> k = 4h + j, j < 4; 8 + 4h + j - 4, j >= 4) -- the W2 fragment takes the same
+// permutation. No LDS, no barrier; 16-B row stores after a v_permlane32_swap of the two halves.
+template <class TL>
+__device__ __forceinline__ void qkv2_fused(const GemmProblem& P, f32x16 (&acc)[TL::TN][TL::TM], float alpha, int m0,
+                                           int n0, int lane, int wave) {
+  constexpr int TM = TL::TM, TN = TL::TN;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int h = lane >> 5, r = lane & 31;
+  const int M = P.M, N = P.N, HH = P.qkv2_hh, HS = 2 * HH;
+  const int nw = n0 + wn * TN * 32;  // first stage-1 column of this wave
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n = nw + 32 * i + 8 * g + 4 * h;
+      f32x4 b = {0.f, 0.f, 0.f, 0.f};
+      if (P.bias && n + 4 <= N) b = *reinterpret_cast<const f32x4*>(P.bias + n);
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = fast_tanh(alpha * acc[i][j][4 * g + e] + b[e]);
+    }
+  }
+  // W2 fragment of block blk, output tile ot, K-16 half kh (HH = 32: two halves): lane (o, h), slot j
+  auto w2frag = [&](int blk, int ot, int kh) {
+    const float* w = P.qkv2_w2 + ((int64_t)blk * HS + ot * 32 + r) * HH + 16 * kh + 4 * h;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(w);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(w + 8);
+    const u32x4 u = {pack2bf(lo[0], lo[1]), pack2bf(lo[2], lo[3]), pack2bf(hi[0], hi[1]), pack2bf(hi[2], hi[3])};
+    return __builtin_bit_cast(bf16x8, u);
+  };
+  // accumulator elements [8q, 8q + 8) of a sub-tile as a bf16 B operand (16 columns of h1)
+  auto hfrag = [&](const f32x16& a, int q) {
+    const u32x4 u = {pack2bf(a[8 * q], a[8 * q + 1]), pack2bf(a[8 * q + 2], a[8 * q + 3]),
+                     pack2bf(a[8 * q + 4], a[8 * q + 5]), pack2bf(a[8 * q + 6], a[8 * q + 7])};
+    return __builtin_bit_cast(bf16x8, u);
+  };
+  // D[o][m] of output tile ot of block blk, m = row sub-tile j: 16-B row pieces
+  auto store = [&](const f32x16& d, int blk, int ot, int j) {
+    const int m = m0 + wm * TM * 32 + 32 * j + r;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int ga = 2 * pr, gb = 2 * pr + 1;
+      const auto s0 = __builtin_amdgcn_permlane32_swap(pack2bf(d[4 * ga], d[4 * ga + 1]), pack2bf(d[4 * gb], d[4 * gb + 1]),
+                                                       false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(pack2bf(d[4 * ga + 2], d[4 * ga + 3]),
+                                                       pack2bf(d[4 * gb + 2], d[4 * gb + 3]), false, false);
+      if (m < M)  // o = ot*32 + 16 pr + 8 h + 0..7
+        *reinterpret_cast<u32x4*>(P.qkv2_out + (int64_t)m * P.qkv2_ld + blk * HS + ot * 32 + 16 * pr + 8 * h) =
+            u32x4{s0[0], s1[0], s0[1], s1[1]};
+    }
+  };
+  f32x16 z;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) z[e] = 0.f;
+  if (HH == 16) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int nb = nw + 32 * i + 16 * q;
+        if (nb >= N) continue;  // wave-uniform
+        const int blk = nb / 16;
+        const bf16x8 a = w2frag(blk, 0, 0);
+#pragma unroll
+        for (int j = 0; j < TM; ++j) store(mfma32(a, hfrag(acc[i][j], q), z), blk, 0, j);
+      }
+  } else {  // HH == 32: one block per sub-tile, K = 32 in two halves, two output tiles
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int nb = nw + 32 * i;
+      if (nb >= N) continue;
+      const int blk = nb / 32;
+#pragma unroll
+      for (int ot = 0; ot < 2; ++ot) {
+        const bf16x8 a0 = w2frag(blk, ot, 0), a1 = w2frag(blk, ot, 1);
+#pragma unroll
+        for (int j = 0; j < TM; ++j) store(mfma32(a1, hfrag(acc[i][j], 1), mfma32(a0, hfrag(acc[i][j], 0), z)), blk, ot, j);
+      }
+    }
   }
 }
 
@@ -640,7 +732,14 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   // split-K into slabs: split s of the K loop writes its own fp32 slab (reduced by mmt_gemm_slab_reduce)
   float* o32 = P.o32 + (P.split_stride ? (int64_t)split * P.split_stride : (int64_t)0);
   const int h = lane >> 5, r = lane & 31;
-  if constexpr (SWAP) {
+  if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16) {
+    if (P.qkv2_out) {  // the per-head stage 2 of Q/K/V (uniform per problem)
+      qkv2_fused<TL>(P, acc, alpha, m0, n0, lane, wave);
+      epilogue_swap<TL, EPI, EPI_ROWS, true>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
+    } else {
+      epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
+    }
+  } else if constexpr (SWAP) {
     epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
   } else {
     // acc[i][j]: rows = m (sub-tile i), cols = n (sub-tile j)
@@ -790,6 +889,13 @@ __global__ __launch_bounds__(TL::NT) void gemm_f8_kernel(GemmBatch batch) {
   }
   float alpha = P.alpha;
   if (P.alpha_ptr) alpha *= *P.alpha_ptr;
+  if constexpr (EPI == EPI_BIAS_TANH_BF16) {
+    if (P.qkv2_out) {
+      qkv2_fused<TL>(P, acc, alpha, m0, n0, lane, wave);
+      epilogue_swap<TL, EPI, EPI_ROWS, true>(P, acc, lds, P.o32, alpha, m0, n0, tid, lane, wave);
+      return;
+    }
+  }
   epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, P.o32, alpha, m0, n0, tid, lane, wave);
 }
 
@@ -909,11 +1015,20 @@ static bool use_big(const GemmBatch& b) {
   return true;
 }
 
+// the fused per-head Q/K/V stage 2 (qkv2_fused): forward tanh epilogue only, hh 16 or 32, 16-B stores,
+// whole hh-blocks (N % hh == 0)
+static bool qkv2_ok(const GemmProblem& P, int epi, bool fwd) {
+  if (!P.qkv2_out) return true;
+  return epi == EPI_BIAS_TANH_BF16 && fwd && (P.qkv2_hh == 16 || P.qkv2_hh == 32) && P.N % P.qkv2_hh == 0 &&
+         P.qkv2_w2 && !(P.qkv2_ld & 7) && !((uintptr_t)P.qkv2_out & 15) && !((uintptr_t)P.qkv2_w2 & 15);
+}
+
 hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, int splits, hipStream_t s) {
   for (int g = 0; g < b.count; ++g) {
     const GemmProblem& P = b.p[g];
     // 16-byte LDS-DMA pieces need 8-element-aligned leading dimensions and 16-byte aligned bases
     if ((P.lda & 7) || (P.ldb & 7) || (((uintptr_t)P.A | (uintptr_t)P.B) & 15)) return hipErrorInvalidValue;
+    if (!qkv2_ok(P, epi, a_kc && b_kc)) return hipErrorInvalidValue;
   }
   const bool big = use_big(b);
   if (a_kc && b_kc) {
@@ -1148,6 +1263,7 @@ hipError_t mmt_launch_gemm_f8(const GemmBatch& b, int epi, hipStream_t s) {
         (P.lds_b & 3) || (((uintptr_t)P.sa | (uintptr_t)P.sb) & 3) || P.lds_a * 32 < P.K || P.lds_b * 32 < P.K)
       return hipErrorInvalidValue;
     if (P.o8 && ((P.N & 31) || (P.ld8 & 7) || ((uintptr_t)P.o8 & 7))) return hipErrorInvalidValue;
+    if (!qkv2_ok(P, epi, true)) return hipErrorInvalidValue;
   }
   switch (epi) {
     case EPI_STORE_BF16: return launch_f8_tile<EPI_STORE_BF16>(b, s);

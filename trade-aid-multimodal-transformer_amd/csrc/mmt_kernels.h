@@ -81,6 +81,14 @@ struct GemmProblem {
   bf16_t* lnf_y;
   float* lnf_mean;
   float* lnf_rstd;
+  // EPI_BIAS_TANH_BF16 (forward, a_kc = b_kc = 1) + the per-head Q/K/V stage 2 fused into the
+  // epilogue (model.py:39, 44, 49): o16 = h1 = tanh(alpha acc + bias) as usual, and for each
+  // qkv2_hh-wide column block blk of h1 (qkv2_hh = 16 or 32)
+  //   qkv2_out[m, blk*2hh + o] = bf16(sum_i qkv2_w2[blk][o][i] * bf16(h1[m, blk*hh + i]))
+  // (qkv2_w2 fp32 [nblk][2hh][hh], qkv2_ld % 8 == 0, 16-B aligned out); null qkv2_out: off
+  const float* qkv2_w2;
+  bf16_t* qkv2_out;
+  int qkv2_ld, qkv2_hh;
 };
 
 struct GemmBatch {

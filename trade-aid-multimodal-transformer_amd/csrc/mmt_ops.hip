@@ -26,6 +26,21 @@ int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t s
   return st(e);
 }
 
+int mmt_op_gemm_qkv(void* stream, int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, const void* B,
+                    int32_t ldb, const float* bias, void* h1, int32_t ldh1, const float* w2, int32_t hh, void* out,
+                    int32_t ld_out) {
+  if (M < 0 || N < 0 || K < 0 || !out || !w2) return MMT_ERR_INVALID;
+  GemmBatch b{};
+  b.count = 1;
+  GemmProblem& p = b.p[0];
+  p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb; p.bias = bias;
+  p.o16 = (bf16_t*)h1; p.ldo16 = ldh1; p.alpha = 1.f; p.M = M; p.N = N; p.K = K;
+  p.qkv2_w2 = w2; p.qkv2_out = (bf16_t*)out; p.qkv2_ld = ld_out; p.qkv2_hh = hh;
+  const hipError_t e = mmt_launch_gemm(b, true, true, EPI_BIAS_TANH_BF16, 1, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return MMT_ERR_UNSUPPORTED;
+  return st(e);
+}
+
 int mmt_op_gemm_wgrad(void* stream, int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, const void* B,
                       int32_t ldb, float* out, int32_t ldc, float alpha, void* slab, int64_t slab_bytes) {
   if (M < 0 || N < 0 || K < 0 || (lda & 7) || (ldb & 7) || !out) return MMT_ERR_INVALID;

@@ -276,9 +276,177 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Backward at hs 32 / 64 (hh = 16 / 32), the head sizes of C1 and the target / C3 / C4 shapes. The op
+// is HBM-bound (read dout and h1, write dh1), so the dh1 product takes its operands straight from
+// global memory: a wave owns 32-row tiles of one block blk, lane (r, h) loads dout[r][16 s + 8 h ..
+// + 8] as the K = o slice of an MFMA B operand and h1[r][8 h .. + 8] (and [16 + 8 h ..] at hh 32) with
+// one 16-B load each. The A operand is W2^T with its rows permuted (physical row p <-> i = p with bits
+// 2 and 3 swapped) so the accumulator hands lane (r, h) exactly dh1[r][8 h + 0..7] (+ [16 + 8 h ..]):
+// tanh' from the h1 registers, one 16-B store, column sums for the stage-1 bias gradient in registers.
+// dW2 (K = rows) needs the tile transposed: the wave writes its dout / h1 registers into its own LDS
+// images (32 rows x 32 columns, 64-B rows, 16-B chunk c of row r at c ^ ((r >> 2) & 3): conflict-free
+// for the 8-lane ds_write_b128 groups and the 4-row ds_read_b64_tr_b16 groups alike) and reads
+// them back transposed. No block barrier in the row loop; the next tile's loads are in flight while
+// the current one computes.
+// ---------------------------------------------------------------------------------------------
+constexpr int QKV2B_TILES = 8;  // 32-row tiles per wave (a block of 4 waves: 1024 rows)
+__device__ __forceinline__ int q2_swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+template <int HS>
+__global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
+  constexpr int HH = HS / 2;
+  constexpr int NOT = HS / 32;  // 32-column output tiles of dout (o)
+  constexpr int KSO = HS / 16;  // k-steps over o for dh1
+  constexpr int NI = HH / 16;   // 16-column slices of h1 per lane group (1 or 2)
+  constexpr int RPB = 4 * 32 * QKV2B_TILES;
+  const Qkv2Problem& P = batch.p[blockIdx.z];
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int nblk = gridDim.x / ((R + RPB - 1) / RPB);
+  const int blk = tile % nblk, rb = tile / nblk;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  // per-wave images: NOT dout sub-images + one h1 image, each 32 x 32 bf16 (2 KiB)
+  __shared__ __attribute__((aligned(16))) char lds[4 * (NOT + 1) * 2048];
+  char* img = lds + w * (NOT + 1) * 2048;
+  char* himg = img + NOT * 2048;
+  if (HH == 16)  // h1 image columns 16..31 stay zero (the dW2 B operand's unused half)
+    *reinterpret_cast<u32x4*>(himg + q2_swz(r, 2 + h)) = u32x4{0u, 0u, 0u, 0u};
+  // A operand of dh1^T = W2^T dout^T: lane (p, h), k-step s -> W2[o = 16 s + 8 h + j][i = pi(p)]
+  const float* w2 = P.w2 + (int64_t)blk * HS * HH;
+  const int ip = (r & 16) | ((r & 4) << 1) | ((r & 8) >> 1) | (r & 3);  // bits 2 and 3 of p swapped
+  bf16x8 wa[KSO];
+#pragma unroll
+  for (int s = 0; s < KSO; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wa[s][j] = (__bf16)(ip < HH ? w2[(16 * s + 8 * h + j) * HH + ip] : 0.f);
+  f32x16 dw[NOT];
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dw[ot][e] = 0.f;
+  float cs[8 * NI];
+#pragma unroll
+  for (int e = 0; e < 8 * NI; ++e) cs[e] = 0.f;
+  f32x16 z;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) z[e] = 0.f;
+
+  u32x4 dv[KSO], hv[NI];
+  auto load = [&](int row) {
+    const bool ok = row < R;
+    const u32x4 zz = {0u, 0u, 0u, 0u};
+    const bf16_t* d = P.dout + (int64_t)row * ld_out + blk * HS + 8 * h;
+    const bf16_t* hp = P.h1 + (int64_t)row * ld_h1 + blk * HH + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KSO; ++s) dv[s] = ok ? *reinterpret_cast<const u32x4*>(d + 16 * s) : zz;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) hv[q] = ok ? *reinterpret_cast<const u32x4*>(hp + 16 * q) : zz;
+  };
+  const int r0 = rb * RPB + w * 32 * QKV2B_TILES;
+  load(r0 + r);
+#pragma unroll 1
+  for (int t = 0; t < QKV2B_TILES; ++t) {
+    const int row = r0 + 32 * t + r;
+    if (r0 + 32 * t >= R) break;  // wave-uniform
+    u32x4 dc[KSO], hc[NI];
+#pragma unroll
+    for (int s = 0; s < KSO; ++s) dc[s] = dv[s];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) hc[q] = hv[q];
+    if (t + 1 < QKV2B_TILES) load(row + 32);  // the next tile's loads fly while this one computes
+    // dh1 (accumulator rows = i in the permuted order: lane (r, h) gets i = 8 h + e, 16 + 8 h + e - 8)
+    f32x16 acc = z;
+#pragma unroll
+    for (int s = 0; s < KSO; ++s) acc = mfma32(wa[s], __builtin_bit_cast(bf16x8, dc[s]), acc);
+    u32x4 dz[NI];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      float t8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t wd = hc[q][e >> 1];
+        const float x = bf2f((bf16_t)((e & 1) ? (wd >> 16) : (wd & 0xffff)));
+        t8[e] = acc[8 * q + e] * (1.f - x * x);
+      }
+      dz[q] = u32x4{pack2bf(t8[0], t8[1]), pack2bf(t8[2], t8[3]), pack2bf(t8[4], t8[5]), pack2bf(t8[6], t8[7])};
+      if (row < R) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[8 * q + e] += t8[e];
+        *reinterpret_cast<u32x4*>(P.dh1 + (int64_t)row * ld_h1 + blk * HH + 16 * q + 8 * h) = dz[q];
+      }
+    }
+    // dW2 over this tile's 32 rows: LDS images (rows past R hold zeros: their loads returned 0)
+#pragma unroll
+    for (int s = 0; s < KSO; ++s)  // dout columns 16 s + 8 h: sub-image s / 2, chunk 2 (s & 1) + h
+      *reinterpret_cast<u32x4*>(img + (s >> 1) * 2048 + q2_swz(r, 2 * (s & 1) + h)) = dc[s];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) *reinterpret_cast<u32x4*>(himg + q2_swz(r, 2 * q + h)) = hc[q];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own wave's writes visible to its reads
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {  // rows 16 ks .. 16 ks + 15
+      // tr read: lane gets column (l & 31) and rows 16 ks + 8 h + 0..7 of an image
+      auto trd = [&](const char* im) {
+        const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+        const int col = 16 * (g & 1) + 4 * pp;
+        const int kr = 16 * ks + 8 * (g >> 1) + qq;
+        const s16x4 lo = lds_tr16(im + q2_swz(kr, col >> 3) + (col & 7) * 2);
+        const s16x4 hi = lds_tr16(im + q2_swz(kr + 4, col >> 3) + (col & 7) * 2);
+        return join4(lo, hi);
+      };
+      const bf16x8 bh = trd(himg);
+#pragma unroll
+      for (int ot = 0; ot < NOT; ++ot) dw[ot] = mfma32(trd(img + ot * 2048), bh, dw[ot]);
+    }
+  }
+  // block reductions: db1 (column sums) and dW2, then one atomic per element per block
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds);  // [HS][HH] floats over the (now dead) images
+  if (P.db1) {
+#pragma unroll
+    for (int e = 0; e < 8 * NI; ++e) {
+      float v = cs[e];
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+      cs[e] = v;
+    }
+  }
+  __shared__ float dbr[4][32];
+  if (P.db1 && r == 0) {
+#pragma unroll
+    for (int q = 0; q < NI; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dbr[w][16 * q + 8 * h + e] = cs[8 * q + e];
+  }
+  __syncthreads();
+  if (P.db1 && tid < HH) atomicAdd(P.db1 + (int64_t)blk * HH + tid, (dbr[0][tid] + dbr[1][tid]) + (dbr[2][tid] + dbr[3][tid]));
+  // dW2 partials: D[o][i], o = ot*32 + (e&3) + 8(e>>2) + 4h, i = lane r (< HH valid)
+  static_assert(HS * HH * 4 <= 4 * (NOT + 1) * 2048, "dW2 reduction fits the images");
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int o = ot * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (r < HH) {
+            float* q = red + o * HH + r;
+            *q = (ww == 0 ? 0.f : *q) + dw[ot][e];
+          }
+        }
+    }
+    __syncthreads();
+  }
+  for (int q = tid; q < HS * HH; q += 256) atomicAdd(P.dw2 + (int64_t)blk * HS * HH + q, red[q]);
+}
+
 template <int HS>
 static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_out, bool bwd, hipStream_t s) {
-  if (bwd)
+  constexpr int RPB = 4 * 32 * QKV2B_TILES;
+  if (bwd && (HS == 32 || HS == 64))
+    hipLaunchKernelGGL(qkv2_bwd_v2<HS == 64 ? 64 : 32>, dim3((R + RPB - 1) / RPB * nblk, 1, b.count), dim3(256), 0, s, b,
+                       R, ld_h1, ld_out);
+  else if (bwd)
     hipLaunchKernelGGL(qkv2_bwd_mfma<HS>, dim3((R + QKV2_BWD_ROWS - 1) / QKV2_BWD_ROWS * nblk, 1, b.count), dim3(256), 0, s,
                        b, R, ld_h1, ld_out);
   else

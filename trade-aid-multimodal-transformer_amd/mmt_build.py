@@ -48,10 +48,14 @@ def build(force=False, verbose=True):
     with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), 8)) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs
+        # link to a temporary name, then rename: a snapshot of the tree taken meanwhile (gpurun) never
+        # sees a half-written library
+        tmp = LIB + ".tmp"
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, LIB)
     if verbose:
         print(f"[mmt_build] {LIB}")
     return LIB

@@ -88,6 +88,8 @@ _SIGS = {
     "mmt_gemm_set_variant": (c_i32, [ctypes.c_int]),
     "mmt_op_gemm": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp,
                             c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32]),
+    "mmt_op_gemm_qkv": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp, c_i32,
+                                c_vp, c_i32]),
     "mmt_op_gemm_wgrad": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32, c_vp, c_i64]),
     "mmt_op_gemm_ln_bwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp,
                                    c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint32, ctypes.c_uint32, c_f32]),
