@@ -203,8 +203,9 @@ int mmt_op_gemm(void* stream, int32_t a_kc, int32_t b_kc, int32_t epi, int32_t s
 /* Q/K/V projection of the engine's forward (reference model.py:36-50, every head's key / query /
  * value MLP at once): h1[M, N] = bf16(tanh(A[M, K] B[N, K]^T + bias)) (stage 1, N = 3 H hh) and, fused
  * into the same GEMM's epilogue, stage 2 out[m, blk*2hh + o] = bf16(sum_i w2[blk][o][i] h1[m, blk*hh + i])
- * (w2 fp32 [N/hh][2hh][hh]). hh must be 16 or 32 (MMT_ERR_UNSUPPORTED otherwise: the engine then runs
- * stage 2 as mmt_op_qkv2_fwd's separate kernel); ld_out % 8 == 0, 16-B aligned out. */
+ * (w2 fp32 [N/hh][2hh][hh]). hh must be 16 or 32 and the GEMM must run on the 128 x 128 tile (not M,
+ * N >= 256 with K >= 1024), else MMT_ERR_UNSUPPORTED (the engine then runs stage 2 as mmt_op_qkv2_fwd's
+ * separate kernel); ld_out % 8 == 0, 16-B aligned out. */
 int mmt_op_gemm_qkv(void* stream, int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, const void* B,
                     int32_t ldb, const float* bias, void* h1, int32_t ldh1, const float* w2, int32_t hh, void* out,
                     int32_t ld_out);

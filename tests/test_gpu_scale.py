@@ -231,7 +231,11 @@ def test_full_size_training_property(name):
     assert torch.isfinite(h).all()
     assert int(m.nonfinite_loss_mask(sticky=True).item()) == 0
     assert torch.isfinite(m.flat_params).all()
-    # the total falls by > 10 % and no modality's loss rises (the narrow output heads of the small
-    # vocabularies, Linear(C, V//2) -> tanh, move slowly at lr 3e-4: V = 13 and 5 fall by 1-4 %)
+    # the total falls by > 10 % and no modality's loss rises by more than 0.5 %: the narrow output
+    # heads of the small vocabularies (Linear(C, V//2) -> tanh) move slowly at lr 3e-4, and in 20
+    # steps of the 24-layer fp8 C4 model the V = 5 stream ends anywhere between -1 % and +0.2 % of
+    # its start depending on the accumulation order of the backward kernels (round 4: 1.6068 ->
+    # 1.5940 / 1.5966 / 1.6096 with three numerically equivalent attention / Q/K/V backward
+    # variants), so "strictly below" would test rounding, not learning
     last = h[-3:].mean(0)
-    assert last.sum() < 0.9 * h[0].sum() and (last < h[0]).all(), (h[0], h[-1])
+    assert last.sum() < 0.9 * h[0].sum() and (last < 1.005 * h[0]).all(), (h[0], h[-1])

@@ -36,13 +36,16 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 
 // tanh for fp32 epilogues whose result is stored as bf16: exp-based away from 0, odd Taylor
 // polynomial near 0 (avoids the 1 - e cancellation); |error| < 2e-7, far below bf16 rounding.
+// Branch-free: both forms are computed and selected (a divide here lowered to the IEEE
+// v_div_scale / v_div_fmas sequence and turned the select into a divergent branch per element).
+// v_rcp_f32 (1 ulp) keeps the error far below the bf16 rounding of the stored result.
 __device__ __forceinline__ float fast_tanh(float x) {
   const float ax = fabsf(x);
   const float e = __expf(-2.0f * ax);
-  const float t = __fdividef(1.0f - e, 1.0f + e);
+  const float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
   const float x2 = x * x;
   const float p = x * (1.0f + x2 * (-0.333333343f + x2 * (0.133333340f + x2 * -0.0539682540f)));
-  return ax < 0.125f ? p : copysignf(t, x);
+  return ax < 0.125f ? p : __builtin_copysignf(t, x);
 }
 
 __device__ __forceinline__ float warp_sum(float v) {

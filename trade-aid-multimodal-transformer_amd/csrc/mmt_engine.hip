@@ -82,13 +82,17 @@ struct Plan {
   std::vector<ActLM> act;  // [L*M]
   size_t xemb[MAXM];
   size_t lnf16[MAXM], meanf[MAXM], rstdf[MAXM], hh[MAXM], dlog[MAXM];
-  // backward scratch, per modality
-  size_t dres[MAXM], dln[MAXM], gbig[MAXM], gdo[MAXM], gq[MAXM], gqkv[MAXM], gh1[MAXM], gp[MAXM], gpc[MAXM];
-  // bf16 residual-gradient copies, rotated over 4 buffers (one per LayerNorm-backward / copy launch):
-  // a side-stream weight-gradient GEMM still reading one does not block the next write
-  size_t dres16[4][MAXM];
+  // backward scratch, per modality. The data gradients a side-stream weight-gradient GEMM reads
+  // (gbig, gq, gh1, gp, gpc, dkv) have two copies, one per backward-stage parity, so the main
+  // stream may run a whole stage ahead of the side stream (mmt_backward joins once, at its end)
+  size_t dres[MAXM], dln[MAXM], gdo[MAXM], gqkv[MAXM];
+  size_t gbig[2][MAXM], gq[2][MAXM], gh1[2][MAXM], gp[2][MAXM], gpc[2][MAXM];
+  // bf16 residual-gradient copies, rotated over 8 buffers (one per LayerNorm-backward / copy launch,
+  // three per layer stage): a side-stream weight-gradient GEMM up to one stage behind still reads
+  // its copy when the main stream writes the next ones
+  size_t dres16[8][MAXM];
   size_t dvec[MAXM][MAXM];
-  size_t dkv[MAXM][MAXM];
+  size_t dkv[2][MAXM][MAXM];
   // KV-cache decode (generate): compact [B, *] rows of ONE new position per sequence
   struct Dec {
     size_t x0, a16, mean, rstd, h1, qkv, o16, p1, f, x2h, d16, qc, oc, pc, lnf16, hh;
@@ -156,6 +160,12 @@ struct mmt_ctx {
   hipStream_t side = nullptr;
   int side_device = -1;
   bool side_off = false;  // mmt_set_side_stream(ctx, 0): this context runs everything on the caller's stream
+  // mmt_backward (all stages in one call): no join per stage; the side stream's work of stage t is
+  // recorded in stage_ev[t & 1] and the main stream waits for it only at the start of stage t + 2,
+  // the first stage that rewrites that parity's scratch (Plan). mmt_backward_stage called alone (the
+  // data-parallel path: each stage's gradient range must be final for its all-reduce) joins per stage.
+  bool defer_join = false;
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> evpool;
   size_t evnext = 0;
   int d16 = 0;  // rotation index of the current dres16 copy (reset at backward stage 0)
@@ -428,14 +438,17 @@ void make_plan(mmt_ctx* c, int B) {
   }
   for (int i = 0; i < M; ++i) {
     p.dres[i] = A(R * C * f4); p.dln[i] = A(R * C * f4);
-    for (int k = 0; k < 4; ++k) p.dres16[k][i] = A(R * C * b2);
-    p.gbig[i] = A(R * std::max(4 * C, maxvh) * b2);
-    p.gdo[i] = A(R * C * b2); p.gq[i] = A(R * C * b2); p.gqkv[i] = A(R * 3 * C * b2);
-    p.gh1[i] = A(R * ldh1 * b2); p.gp[i] = A(R * ldp * b2);
-    p.gpc[i] = (c->any_cross && c->cfg.cross_attention[i]) ? A(R * ldp * b2) : p.gp[i];
+    for (int k = 0; k < 8; ++k) p.dres16[k][i] = A(R * C * b2);
+    p.gdo[i] = A(R * C * b2); p.gqkv[i] = A(R * 3 * C * b2);
+    for (int k = 0; k < 2; ++k) {
+      p.gbig[k][i] = A(R * std::max(4 * C, maxvh) * b2);
+      p.gq[k][i] = A(R * C * b2);
+      p.gh1[k][i] = A(R * ldh1 * b2); p.gp[k][i] = A(R * ldp * b2);
+      p.gpc[k][i] = (c->any_cross && c->cfg.cross_attention[i]) ? A(R * ldp * b2) : p.gp[k][i];
+      if (c->any_cross && c->cfg.cross_attention[i])
+        for (int j = 0; j < M - 1; ++j) p.dkv[k][i][j] = A(R * 2 * C * b2);
+    }
     for (int j = 0; j < M; ++j) p.dvec[i][j] = A(bhT * f4);
-    if (c->any_cross && c->cfg.cross_attention[i])
-      for (int j = 0; j < M - 1; ++j) p.dkv[i][j] = A(R * 2 * C * b2);
   }
   // weight-gradient split-K slabs: room for 16 splits of the largest grouped dW launch
   {
@@ -877,11 +890,14 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       const char* e = getenv("MMT_QKV2_FUSE");
       return e ? atoi(e) != 0 : true;
     }();
-    const bool fuse_qkv2 = qkv2_fuse && (c->hh == 16 || c->hh == 32);
     for (int i = 0; i < M; ++i) {
       g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].a8), C, r.W<uint8_t>(a[i].as8), ldsC, w8, x[i].W1, R)
                   : gp_fwd(r.W<bf16_t>(a[i].a), C, wpk, x[i].W1, R);
       g.p[i].bias = r.P(x[i].b1); g.p[i].o16 = r.W<bf16_t>(a[i].h1); g.p[i].ldo16 = ldh1;
+    }
+    // (the 128 x 128 bf16 tile only: not on the fp8 kernel, not where the GEMM takes the 256 x 256 tile)
+    const bool fuse_qkv2 = qkv2_fuse && (c->hh == 16 || c->hh == 32) && !f8 && !mmt_gemm_wgrad_big(g);
+    for (int i = 0; i < M; ++i) {
       if (fuse_qkv2) {
         g.p[i].qkv2_w2 = r.P(x[i].w2); g.p[i].qkv2_out = r.W<bf16_t>(a[i].qkv);
         g.p[i].qkv2_ld = 3 * C; g.p[i].qkv2_hh = c->hh;
@@ -1269,7 +1285,7 @@ void colsum_add(Runner& r, ColsumBatch& cb, int u, const bf16_t* x, int ld, floa
 // sums are that branch's output-bias gradient. Modalities whose copy is rebuilt later (non-cross
 // modalities of a cross model) and lprev < 0 (embeddings) get no copy.
 // current dres16 copy (the last one written), and the next one in the rotation (for a writer)
-inline bf16_t* d16_cur(mmt_ctx* c, Runner& r, int i) { return r.W<bf16_t>(c->plan.dres16[c->d16 & 3][i]); }
+inline bf16_t* d16_cur(mmt_ctx* c, Runner& r, int i) { return r.W<bf16_t>(c->plan.dres16[c->d16 & 7][i]); }
 inline void d16_advance(mmt_ctx* c) { ++c->d16; }
 
 void set_dres16_consumer(mmt_ctx* c, Runner& r, LnProblem& lp, int i, int lprev, float* grads) {
@@ -1294,6 +1310,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   const float scale = 1.0f / std::sqrt((float)hs);
   Plan& p = c->plan;
   const bf16_t* wpk = r.W<bf16_t>(p.pack);
+  const int par = stage & 1;  // copy of the side-stream-read scratch this stage writes (Plan)
   if (stage == 0) {
     c->d16 = 0;
     HIPCHK(c, hipMemsetAsync(grads, 0, sizeof(float) * c->nactive, r.s));  // the active prefix only
@@ -1310,7 +1327,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       dx.p[i] = gp_dx(dl, c->ldv[i], wpk, q.H2, R);
       dx.p[i].alpha_ptr = loss_grads + i; dx.p[i].alpha = invR;
       dx.p[i].aux = r.W<bf16_t>(p.hh[i]); dx.p[i].ldaux = c->ldvh[i];
-      dx.p[i].o16 = r.W<bf16_t>(p.gbig[i]); dx.p[i].ldo16 = c->ldvh[i];
+      dx.p[i].o16 = r.W<bf16_t>(p.gbig[par][i]); dx.p[i].ldo16 = c->ldvh[i];
     }
     r.dwgemm(dw, "head2_dw");
     r.ok(mmt_launch_colsum(cs, R, r.s), "head2_db");
@@ -1318,7 +1335,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "head2_dx");
     for (int i = 0; i < M; ++i) {
       const PostM& q = c->post[i];
-      const bf16_t* g = r.W<bf16_t>(p.gbig[i]);
+      const bf16_t* g = r.W<bf16_t>(p.gbig[par][i]);
       dw.p[i] = gp_dw(g, c->ldvh[i], r.W<bf16_t>(p.lnf16[i]), C, grads, q.H0, R);
       dx.p[i] = gp_dx(g, c->ldvh[i], wpk, q.H0, R);
       dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
@@ -1364,14 +1381,14 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       const bf16_t* g = d16_cur(c, r, i);
       dw.p[u] = gp_dw(g, C, r.W<bf16_t>(a[i].pc), ldp, grads, x[i].C2, R);
       dx.p[u] = gp_dx(g, C, wpk, x[i].C2, R);
-      dx.p[u].aux = r.W<bf16_t>(a[i].pc); dx.p[u].ldaux = ldp; dx.p[u].o16 = r.W<bf16_t>(p.gpc[i]); dx.p[u].ldo16 = ldp;
+      dx.p[u].aux = r.W<bf16_t>(a[i].pc); dx.p[u].ldaux = ldp; dx.p[u].o16 = r.W<bf16_t>(p.gpc[par][i]); dx.p[u].ldo16 = ldp;
       dx.p[u].dbias = grads + x[i].bc0;
     }
     r.dwgemm(dw, "ca_proj2_dw");
     r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "ca_proj2_dx");
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
-      const bf16_t* g = r.W<bf16_t>(p.gpc[i]);
+      const bf16_t* g = r.W<bf16_t>(p.gpc[par][i]);
       dw.p[u] = gp_dw(g, ldp, r.W<bf16_t>(a[i].oc), C, grads, x[i].C0, R);
       dx.p[u] = gp_dx(g, ldp, wpk, x[i].C0, R);
       dx.p[u].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[u].ldo16 = C;
@@ -1388,11 +1405,11 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
         bf16_t* kv = r.W<bf16_t>(a[i].kv[j]);
         q.k[j] = kv; q.v[j] = kv + hs; q.oj[j] = r.W<bf16_t>(a[i].ocj[j]); q.lse[j] = r.W<float>(a[i].lsej[j]);
         q.dvec[j] = r.W<float>(p.dvec[i][j]);
-        bf16_t* dkv = r.W<bf16_t>(p.dkv[i][j]);
+        bf16_t* dkv = r.W<bf16_t>(p.dkv[par][i][j]);
         q.dk[j] = dkv; q.dv[j] = dkv + hs;
       }
       q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(a[i].oc); q.o_ld = C; q.nstreams = M - 1;
-      q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dq = r.W<bf16_t>(p.gq[i]); q.dq_ld = C;
+      q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dq = r.W<bf16_t>(p.gq[par][i]); q.dq_ld = C;
       q.dkv_ld = 2 * C; q.dkv_hstride = 2 * hs;
       r.set_drop(q, l, i, DS_CA_PROB);
       if (r.drop)
@@ -1401,7 +1418,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     r.attn(ab, true, scale, "ca_attn_bwd");
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
-      const bf16_t* g = r.W<bf16_t>(p.gq[i]);
+      const bf16_t* g = r.W<bf16_t>(p.gq[par][i]);
       dw.p[u] = gp_dw(g, C, r.W<bf16_t>(a[i].d), C, grads, x[i].Wq, R);
       dx.p[u] = gp_dx(g, C, wpk, x[i].Wq, R);
       dx.p[u].o32 = r.W<float>(p.dln[i]); dx.p[u].ldc = C;
@@ -1423,7 +1440,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       int jj = 0;
       for (int j = 0; j < M; ++j) {
         if (j == i) continue;
-        const bf16_t* g = r.W<bf16_t>(p.dkv[i][jj]);
+        const bf16_t* g = r.W<bf16_t>(p.dkv[par][i][jj]);
         kw.p[kw.count++] = gp_dw(g, 2 * C, r.W<bf16_t>(a[j].x2h), C, grads, x[i].Wkv[jj], R);
         GemmProblem d = gp_dx(g, 2 * C, wpk, x[i].Wkv[jj], R);
         d.o32 = r.W<float>(p.dres[j]); d.ldc = C;
@@ -1456,13 +1473,13 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     const bf16_t* g = d16_cur(c, r, i);
     dw.p[i] = gp_dw(g, C, r.W<bf16_t>(a[i].f), 4 * C, grads, x[i].F2, R);
     dx.p[i] = gp_dx(g, C, wpk, x[i].F2, R);
-    dx.p[i].aux = r.W<bf16_t>(a[i].f); dx.p[i].ldaux = 4 * C; dx.p[i].o16 = r.W<bf16_t>(p.gbig[i]); dx.p[i].ldo16 = 4 * C;
+    dx.p[i].aux = r.W<bf16_t>(a[i].f); dx.p[i].ldaux = 4 * C; dx.p[i].o16 = r.W<bf16_t>(p.gbig[par][i]); dx.p[i].ldo16 = 4 * C;
     dx.p[i].dbias = grads + x[i].bf0;
   }
   r.dwgemm(dw, "ffn2_dw");
   r.gemm(dx, true, false, EPI_DRELU_BF16, 1, "ffn2_dx");
   for (int i = 0; i < M; ++i) {
-    const bf16_t* g = r.W<bf16_t>(p.gbig[i]);
+    const bf16_t* g = r.W<bf16_t>(p.gbig[par][i]);
     dw.p[i] = gp_dw(g, 4 * C, r.W<bf16_t>(a[i].c), C, grads, x[i].F0, R);
     dx.p[i] = gp_dx(g, 4 * C, wpk, x[i].F0, R);
     dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
@@ -1483,13 +1500,13 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     const bf16_t* g = d16_cur(c, r, i);
     dw.p[i] = gp_dw(g, C, r.W<bf16_t>(a[i].p1), ldp, grads, x[i].P2, R);
     dx.p[i] = gp_dx(g, C, wpk, x[i].P2, R);
-    dx.p[i].aux = r.W<bf16_t>(a[i].p1); dx.p[i].ldaux = ldp; dx.p[i].o16 = r.W<bf16_t>(p.gp[i]); dx.p[i].ldo16 = ldp;
+    dx.p[i].aux = r.W<bf16_t>(a[i].p1); dx.p[i].ldaux = ldp; dx.p[i].o16 = r.W<bf16_t>(p.gp[par][i]); dx.p[i].ldo16 = ldp;
     dx.p[i].dbias = grads + x[i].bp0;
   }
   r.dwgemm(dw, "proj2_dw");
   r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "proj2_dx");
   for (int i = 0; i < M; ++i) {
-    const bf16_t* g = r.W<bf16_t>(p.gp[i]);
+    const bf16_t* g = r.W<bf16_t>(p.gp[par][i]);
     dw.p[i] = gp_dw(g, ldp, r.W<bf16_t>(a[i].o), C, grads, x[i].P0, R);
     dx.p[i] = gp_dx(g, ldp, wpk, x[i].P0, R);
     dx.p[i].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[i].ldo16 = C;
@@ -1513,12 +1530,12 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   Qkv2Batch qb{}; qb.count = M;
   for (int i = 0; i < M; ++i) {
     qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].dout = r.W<bf16_t>(p.gqkv[i]);
-    qb.p[i].dh1 = r.W<bf16_t>(p.gh1[i]); qb.p[i].dw2 = grads + x[i].w2;
+    qb.p[i].dh1 = r.W<bf16_t>(p.gh1[par][i]); qb.p[i].dw2 = grads + x[i].w2;
     qb.p[i].db1 = grads + x[i].b1;  // stage-1 bias gradient: column sums of dh1, fused
   }
   r.ok(mmt_launch_qkv2_bwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_bwd");
   for (int i = 0; i < M; ++i) {
-    const bf16_t* g = r.W<bf16_t>(p.gh1[i]);
+    const bf16_t* g = r.W<bf16_t>(p.gh1[par][i]);
     dw.p[i] = gp_dw(g, ldh1, r.W<bf16_t>(a[i].a), C, grads, x[i].W1, R);
     dx.p[i] = gp_dx(g, ldh1, wpk, x[i].W1, R);
     dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
@@ -1616,7 +1633,15 @@ void ensure_side(mmt_ctx* c) {
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) break;
     c->evpool.push_back(e);
   }
-  if (c->evpool.empty() && c->side) { (void)hipStreamDestroy(c->side); c->side = nullptr; }
+  for (auto& e : c->stage_ev) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+    if (c->side && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+  }
+  if ((c->evpool.empty() || !c->stage_ev[0] || !c->stage_ev[1]) && c->side) {
+    (void)hipStreamDestroy(c->side);
+    c->side = nullptr;
+  }
 }
 
 }  // namespace
@@ -1654,6 +1679,7 @@ void mmt_destroy(mmt_ctx* c) {
   if (c->d_mxsegs) (void)hipFree(c->d_mxsegs);
   for (auto& e : c->probe_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
+  for (auto& e : c->stage_ev) if (e) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
 }
@@ -1773,19 +1799,32 @@ int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* los
     r.ok(mmt_launch_embed_bwd(eb, r.B, c->T, c->C, r.s), "embed_bwd");
     return r.rc;
   }
+  const bool defer = c->defer_join && r.side_stream();
+  if (defer && stage >= 2)  // the side stream's work of stage - 2 read this stage's scratch copies
+    r.ok(hipStreamWaitEvent(r.s, c->stage_ev[stage & 1], 0), "stream wait");
   const int rc = run_backward_stage(c, r, stage, loss_grads, grads);
-  r.join();  // the stage's gradient range is complete on the caller's stream (DP all-reduce order)
+  if (defer) {
+    r.flush();
+    r.ok(hipEventRecord(c->stage_ev[stage & 1], c->side), "event record");
+  } else {
+    r.join();  // the stage's gradient range is complete on the caller's stream (DP all-reduce order)
+  }
   return rc ? rc : r.rc;
 }
 
 int mmt_backward(mmt_ctx* c, void* stream, const float* loss_grads, const float* params, float* grads,
                  void* workspace) {
   if (!c) return MMT_ERR_INVALID;
-  for (int s = 0; s < c->L + 2; ++s) {
-    const int rc = mmt_backward_stage(c, stream, s, loss_grads, params, grads, workspace);
-    if (rc) return rc;
-  }
-  return MMT_OK;
+  // one join at the end instead of one per stage (mmt_ctx::defer_join); the embedding stage is the
+  // last and runs on the caller's stream only, so the join closes over every weight gradient
+  c->defer_join = true;
+  int rc = MMT_OK;
+  for (int s = 0; s < c->L + 2 && rc == MMT_OK; ++s) rc = mmt_backward_stage(c, stream, s, loss_grads, params, grads, workspace);
+  c->defer_join = false;
+  if (rc) return rc;
+  Runner r{c, (hipStream_t)stream, workspace, params, nullptr, c->plan.B, c->plan.B * c->T};
+  r.join();
+  return r.rc;
 }
 
 int mmt_adamw_step(mmt_ctx* c, void* stream, float* params, const float* grads, float* m, float* v, int64_t n,

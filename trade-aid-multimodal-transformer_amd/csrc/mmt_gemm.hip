@@ -49,12 +49,14 @@ using TileW = TileCfg<1, 8, 4, 2>;
 //   0 = BK 64 x 2 stages, 1 = BK 32 x 2, 2 = BK 32 x 3, 3 = BK 32 x 4, 4 = BK 64 x 3,
 //   5 = BK 32 x 3 and 6 = BK 32 x 2 at 3 blocks per CU (64-row epilogue passes)
 static int g_gemm_variant = -1;     // forward / backward-data (-1: per-epilogue policy, launch_t)
+static int g_gemm_big_variant_rt = 0;  // bits 8-11 of mmt_gemm_set_variant: 256x256 pipeline (0: env / default)
 static int g_gemm_variant_dw = 0;   // weight grad (split-K atomic)
 extern "C" int mmt_gemm_set_variant(int v) {
   if (v < 0) { g_gemm_variant = -1; g_gemm_variant_dw = 0; return 0; }  // back to the default policy
-  if ((v & 15) > 6 || ((v >> 4) & 15) > 6) return -1;
+  if ((v & 15) > 8 || ((v >> 4) & 15) > 8) return -1;
   g_gemm_variant = v & 15;
   g_gemm_variant_dw = (v >> 4) & 15;
+  g_gemm_big_variant_rt = (v >> 8) & 15;
   return 0;
 }
 
@@ -121,6 +123,41 @@ __device__ __forceinline__ void issue_tile(const i32x4& rsrc, char* img, int ld,
     }
     dma16(rsrc, __builtin_amdgcn_readfirstlane(lds_u32(img + i * 1024)), voff);
   }
+}
+
+// per-piece source geometry, computed once per tile: the byte offset of the piece's row (K-contiguous
+// operand) or column (MN-contiguous) -- negative when that row / column is past the operand -- and
+// its K offset within a K-step. issue_pre then costs ~4 VALU per piece instead of ~12.
+struct PieceSrc {
+  int base, kk;
+};
+template <int BK, bool KC, int ROWS, int NW>
+__device__ __forceinline__ PieceSrc piece_src(int ld, int rows_total, int r0, int wave, int lane, int u) {
+  constexpr int PPW = ROWS * BK / 512 / NW;
+  constexpr int CPR = BK / 8;
+  constexpr int CPK = ROWS / 8;
+  const int i = wave * PPW + u;
+  PieceSrc p;
+  if (KC) {
+    const int row = (64 / CPR) * i + lane / CPR;
+    const int chunk = kc_swz<BK>(lane % CPR, row);
+    p.base = r0 + row < rows_total ? (r0 + row) * ld * 2 : -1;
+    p.kk = chunk * 8;
+  } else {
+    const int kr = (64 / CPK) * i + lane / CPK;
+    const int chunk = (lane % CPK) ^ ((kr & 3) << 2);
+    p.base = r0 + chunk * 8 < rows_total ? (r0 + chunk * 8) * 2 : -1;
+    p.kk = kr;
+  }
+  return p;
+}
+template <int BK, bool KC, int ROWS, int NW>
+__device__ __forceinline__ void issue_pre(const i32x4& rsrc, char* img, const PieceSrc& ps, int ld, int K, int k0,
+                                          int wave, int u) {
+  constexpr int PPW = ROWS * BK / 512 / NW;
+  const int gk = k0 + ps.kk;
+  const int voff = (ps.base >= 0 && gk < K) ? ps.base + (KC ? gk * 2 : gk * ld * 2) : 0x7fffffff;
+  dma16(rsrc, __builtin_amdgcn_readfirstlane(lds_u32(img + (wave * PPW + u) * 1024)), voff);
 }
 
 // fragment for "lane row = sb + (lane&31), k = 16*s + 8*(lane>>5) + j" from a staged image
@@ -528,19 +565,6 @@ __device__ __forceinline__ void qkv2_fused(const GemmProblem& P, f32x16 (&acc)[T
   const int h = lane >> 5, r = lane & 31;
   const int M = P.M, N = P.N, HH = P.qkv2_hh, HS = 2 * HH;
   const int nw = n0 + wn * TN * 32;  // first stage-1 column of this wave
-#pragma unroll
-  for (int i = 0; i < TN; ++i) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = nw + 32 * i + 8 * g + 4 * h;
-      f32x4 b = {0.f, 0.f, 0.f, 0.f};
-      if (P.bias && n + 4 <= N) b = *reinterpret_cast<const f32x4*>(P.bias + n);
-#pragma unroll
-      for (int j = 0; j < TM; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = fast_tanh(alpha * acc[i][j][4 * g + e] + b[e]);
-    }
-  }
   // W2 fragment of block blk, output tile ot, K-16 half kh (HH = 32: two halves): lane (o, h), slot j
   auto w2frag = [&](int blk, int ot, int kh) {
     const float* w = P.qkv2_w2 + ((int64_t)blk * HS + ot * 32 + r) * HH + 16 * kh + 4 * h;
@@ -573,37 +597,43 @@ __device__ __forceinline__ void qkv2_fused(const GemmProblem& P, f32x16 (&acc)[T
   f32x16 z;
 #pragma unroll
   for (int e = 0; e < 16; ++e) z[e] = 0.f;
-  if (HH == 16) {
+  // one 32x32 sub-tile at a time (activation, then its stage-2 MFMAs and stores): every value is
+  // produced right before its use, so the epilogue stays inside the main loop's register budget
 #pragma unroll
-    for (int i = 0; i < TN; ++i)
+  for (int i = 0; i < TN; ++i) {
+    const int nb = nw + 32 * i;
+    f32x4 bv[4];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int nb = nw + 32 * i + 16 * q;
-        if (nb >= N) continue;  // wave-uniform
-        const int blk = nb / 16;
-        const bf16x8 a = w2frag(blk, 0, 0);
+    for (int g = 0; g < 4; ++g) {
+      const int n = nb + 8 * g + 4 * h;
+      bv[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (P.bias && n + 4 <= N) bv[g] = *reinterpret_cast<const f32x4*>(P.bias + n);
+    }
 #pragma unroll
-        for (int j = 0; j < TM; ++j) store(mfma32(a, hfrag(acc[i][j], q), z), blk, 0, j);
+    for (int j = 0; j < TM; ++j) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = fast_tanh(alpha * acc[i][j][e] + bv[e >> 2][e & 3]);
+      if (HH == 16) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          if (nb + 16 * q < N) store(mfma32(w2frag((nb + 16 * q) / 16, 0, 0), hfrag(acc[i][j], q), z), (nb + 16 * q) / 16, 0, j);
+      } else if (nb < N) {  // HH == 32: K = 32 in two halves, two output tiles
+        const bf16x8 h0 = hfrag(acc[i][j], 0), h1 = hfrag(acc[i][j], 1);
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot)
+          store(mfma32(w2frag(nb / 32, ot, 1), h1, mfma32(w2frag(nb / 32, ot, 0), h0, z)), nb / 32, ot, j);
       }
-  } else {  // HH == 32: one block per sub-tile, K = 32 in two halves, two output tiles
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int nb = nw + 32 * i;
-      if (nb >= N) continue;
-      const int blk = nb / 32;
-#pragma unroll
-      for (int ot = 0; ot < 2; ++ot) {
-        const bf16x8 a0 = w2frag(blk, ot, 0), a1 = w2frag(blk, ot, 1);
-#pragma unroll
-        for (int j = 0; j < TM; ++j) store(mfma32(a1, hfrag(acc[i][j], 1), mfma32(a0, hfrag(acc[i][j], 0), z)), blk, ot, j);
-      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 
 // MINB > 1 (128x128 tile only): a launch-bounds hint of MINB blocks per CU, with the epilogue staged in
 // 64-row passes so the LDS footprint leaves room for them (variants 5 and 6)
-template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1>
+// PIPE = 1: software-pipelined K-step (the fragments of sub-step s + 1 read while sub-step s's MFMAs
+// issue, and the next stage's LDS-DMA pieces issued one at a time between MFMAs instead of as a burst
+// ahead of them: a piece's issue costs a wave ~60-100 cycles, MI355X_MICROARCH.md)
+template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1, int PIPE = 0>
 __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
   constexpr int IMG_A = GBM * BK * 2, IMG_B = GBN * BK * 2;  // per operand per stage (both layouts)
@@ -708,6 +738,60 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
           }
       }
     };
+    PieceSrc psrc[PIPE == 1 ? PIECES : 1];
+    if constexpr (PIPE == 1) {
+      constexpr int PA = GBM * BK / 512 / NW;
+#pragma unroll
+      for (int u = 0; u < PIECES; ++u)
+        psrc[u] = u < PA ? piece_src<BK, A_KC, GBM, NW>(P.lda, M, m0, wave, lane, u)
+                         : piece_src<BK, B_KC, GBN, NW>(P.ldb, N, n0, wave, lane, u - PA);
+    }
+    // PIPE 1: one K-step with the fragment reads one sub-step ahead (two fragment register sets) and
+    // the prefetch pieces spread over the first half of the step's MFMAs (the second half covers their
+    // landing before the next step's wait)
+    auto step_p = [&](int tt, auto UC) {
+      constexpr int U = decltype(UC)::value;
+      constexpr int NS = BK / 16, NMF = NS * AI * AJ;
+      constexpr int PA = GBM * BK / 512 / NW;  // this wave's A pieces; then PIECES - PA B pieces
+      static_assert(PA <= PIECES, "pieces");
+      wait_vm(PIECES * min(ST - 2, nk - 1 - tt));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const bool pre = tt + ST - 1 < nk;
+      char* stn = lds + ((U + ST - 1) % ST) * STAGE_BYTES;
+      const int k0n = (ks0 + tt + ST - 1) * BK;
+      const char* imgA = lds + U * STAGE_BYTES;
+      const char* imgB = imgA + IMG_A;
+      bf16x8 fa[2][TM], fb[2][TN];
+#pragma unroll
+      for (int j = 0; j < TM; ++j) fa[0][j] = frag<BK, A_KC, GBM>(imgA, wm * TM * 32 + 32 * j, 0, lane);
+#pragma unroll
+      for (int i = 0; i < TN; ++i) fb[0][i] = frag<BK, B_KC, GBN>(imgB, wn * TN * 32 + 32 * i, 0, lane);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int c = s & 1;
+        if (s + 1 < NS) {
+#pragma unroll
+          for (int j = 0; j < TM; ++j) fa[c ^ 1][j] = frag<BK, A_KC, GBM>(imgA, wm * TM * 32 + 32 * j, s + 1, lane);
+#pragma unroll
+          for (int i = 0; i < TN; ++i) fb[c ^ 1][i] = frag<BK, B_KC, GBN>(imgB, wn * TN * 32 + 32 * i, s + 1, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < AI; ++i)
+#pragma unroll
+          for (int j = 0; j < AJ; ++j) {
+            if (SWAP) acc[i][j] = mfma32(fb[c][i], fa[c][j], acc[i][j]);
+            else acc[i][j] = mfma32(fa[c][i], fb[c][j], acc[i][j]);
+            const int q = (s * AI + i) * AJ + j;  // MFMA index within the step
+#pragma unroll
+            for (int u = 0; u < PIECES; ++u)
+              if (q == (u * NMF) / (2 * PIECES) && pre) {  // first half of the step: time to land
+                if (u < PA) issue_pre<BK, A_KC, GBM, NW>(ra, stn, psrc[u], P.lda, K, k0n, wave, u);
+                else issue_pre<BK, B_KC, GBN, NW>(rb, stn + IMG_A, psrc[u], P.ldb, K, k0n, wave, u - PA);
+              }
+          }
+      }
+    };
 #pragma unroll
     for (int t = 0; t < ST - 1; ++t)
       if (t < nk) {
@@ -716,15 +800,27 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
         issue_tile<BK, B_KC, GBN, NW>(rb, st + IMG_A, P.ldb, N, K, n0, (ks0 + t) * BK, wave, lane);
       }
     int t = 0;
-    for (; t + ST <= nk; t += ST) {
-      step(t, std::integral_constant<int, 0>{});
-      step(t + 1, std::integral_constant<int, 1>{});
-      if constexpr (ST > 2) step(t + 2, std::integral_constant<int, (ST > 2 ? 2 : 0)>{});
-      if constexpr (ST > 3) step(t + 3, std::integral_constant<int, (ST > 3 ? 3 : 0)>{});
+    if constexpr (PIPE == 1) {
+      for (; t + ST <= nk; t += ST) {
+        step_p(t, std::integral_constant<int, 0>{});
+        step_p(t + 1, std::integral_constant<int, 1>{});
+        if constexpr (ST > 2) step_p(t + 2, std::integral_constant<int, (ST > 2 ? 2 : 0)>{});
+        if constexpr (ST > 3) step_p(t + 3, std::integral_constant<int, (ST > 3 ? 3 : 0)>{});
+      }
+      if (t < nk) step_p(t, std::integral_constant<int, 0>{});
+      if (ST > 2 && t + 1 < nk) step_p(t + 1, std::integral_constant<int, 1>{});
+      if constexpr (ST > 3) { if (t + 2 < nk) step_p(t + 2, std::integral_constant<int, (ST > 3 ? 2 : 0)>{}); }
+    } else {
+      for (; t + ST <= nk; t += ST) {
+        step(t, std::integral_constant<int, 0>{});
+        step(t + 1, std::integral_constant<int, 1>{});
+        if constexpr (ST > 2) step(t + 2, std::integral_constant<int, (ST > 2 ? 2 : 0)>{});
+        if constexpr (ST > 3) step(t + 3, std::integral_constant<int, (ST > 3 ? 3 : 0)>{});
+      }
+      if (t < nk) step(t, std::integral_constant<int, 0>{});
+      if (ST > 2 && t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
+      if constexpr (ST > 3) { if (t + 2 < nk) step(t + 2, std::integral_constant<int, (ST > 3 ? 2 : 0)>{}); }
     }
-    if (t < nk) step(t, std::integral_constant<int, 0>{});
-    if (ST > 2 && t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
-    if constexpr (ST > 3) { if (t + 2 < nk) step(t + 2, std::integral_constant<int, (ST > 3 ? 2 : 0)>{}); }
   }
 
   float alpha = P.alpha;
@@ -732,7 +828,9 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   // split-K into slabs: split s of the K loop writes its own fp32 slab (reduced by mmt_gemm_slab_reduce)
   float* o32 = P.o32 + (P.split_stride ? (int64_t)split * P.split_stride : (int64_t)0);
   const int h = lane >> 5, r = lane & 31;
-  if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16) {
+  // the fused per-head Q/K/V stage 2 on the 128 x 128 tile only: next to the 256 x 256 tile's 128
+  // accumulators it spills (the launcher refuses qkv2_out there; the engine then runs qkv2_fwd)
+  if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4) {
     if (P.qkv2_out) {  // the per-head stage 2 of Q/K/V (uniform per problem)
       qkv2_fused<TL>(P, acc, alpha, m0, n0, lane, wave);
       epilogue_swap<TL, EPI, EPI_ROWS, true>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
@@ -889,19 +987,12 @@ __global__ __launch_bounds__(TL::NT) void gemm_f8_kernel(GemmBatch batch) {
   }
   float alpha = P.alpha;
   if (P.alpha_ptr) alpha *= *P.alpha_ptr;
-  if constexpr (EPI == EPI_BIAS_TANH_BF16) {
-    if (P.qkv2_out) {
-      qkv2_fused<TL>(P, acc, alpha, m0, n0, lane, wave);
-      epilogue_swap<TL, EPI, EPI_ROWS, true>(P, acc, lds, P.o32, alpha, m0, n0, tid, lane, wave);
-      return;
-    }
-  }
   epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, P.o32, alpha, m0, n0, tid, lane, wave);
 }
 
-template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1>
+template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1, int PIPE = 0>
 static void launch_v(const GemmBatch& b, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI, MINB>), grid, dim3(TL::NT), 0, s, b);
+  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI, MINB, PIPE>), grid, dim3(TL::NT), 0, s, b);
 }
 
 template <class TL>
@@ -955,9 +1046,11 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
     dim3 grid(mt, EPI == EPI_ATOMIC_F32 ? auto_splits<TileL>(b, splits) : std::max(1, splits), b.count);
-    switch (g_big_variant) {
+    switch (g_gemm_big_variant_rt ? g_gemm_big_variant_rt : g_big_variant) {
       case 1: launch_v<TileL, 32, 4, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
       case 2: launch_v<TileL, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+      case 3: launch_v<TileL, 64, 2, A_KC, B_KC, SWAP, EPI, 1, 1>(b, grid, s); break;
+      case 4: launch_v<TileL, 32, 4, A_KC, B_KC, SWAP, EPI, 1, 1>(b, grid, s); break;
       default: launch_v<TileL, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     }
     return hipGetLastError();
@@ -987,6 +1080,8 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     case 4: launch_v<TileS, 64, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 5: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
     case 6: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
+    case 7: launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI, 1, 1>(b, grid, s); break;
+    case 8: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI, 3, 1>(b, grid, s); break;
     default: launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
   }
   return hipGetLastError();
@@ -1031,6 +1126,8 @@ hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, in
     if (!qkv2_ok(P, epi, a_kc && b_kc)) return hipErrorInvalidValue;
   }
   const bool big = use_big(b);
+  for (int g = 0; g < b.count; ++g)
+    if (big && b.p[g].qkv2_out) return hipErrorInvalidValue;  // fused stage 2: 128 x 128 tile only
   if (a_kc && b_kc) {
     switch (epi) {
       case EPI_STORE_BF16: return launch_t<true, true, true, EPI_STORE_BF16>(b, 1, big, s);
@@ -1263,7 +1360,7 @@ hipError_t mmt_launch_gemm_f8(const GemmBatch& b, int epi, hipStream_t s) {
         (P.lds_b & 3) || (((uintptr_t)P.sa | (uintptr_t)P.sb) & 3) || P.lds_a * 32 < P.K || P.lds_b * 32 < P.K)
       return hipErrorInvalidValue;
     if (P.o8 && ((P.N & 31) || (P.ld8 & 7) || ((uintptr_t)P.o8 & 7))) return hipErrorInvalidValue;
-    if (!qkv2_ok(P, epi, true)) return hipErrorInvalidValue;
+    if (P.qkv2_out) return hipErrorInvalidValue;  // (no fused Q/K/V stage 2 on the fp8 kernel)
   }
   switch (epi) {
     case EPI_STORE_BF16: return launch_f8_tile<EPI_STORE_BF16>(b, s);

@@ -116,7 +116,8 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
 // with E8M0 exponents per 32 K elements; K % 32 == 0) via v_mfma_scale_f32_32x32x64_f8f6f4, any
 // of the bf16 GEMM's forward epilogues; fp32 accumulation
 hipError_t mmt_launch_gemm_f8(const GemmBatch& b, int epi, hipStream_t s);
-// whether a weight-gradient batch runs on the 256x256 tile (launches can only be merged when equal)
+// whether a batch runs on the 256x256 tile (weight-gradient launches can only be merged when equal;
+// the fused Q/K/V stage 2 needs the 128x128 tile)
 bool mmt_gemm_wgrad_big(const GemmBatch& b);
 
 // ------------------------------------------------------------------------------------------
