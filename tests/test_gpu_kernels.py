@@ -118,6 +118,24 @@ def test_gemm_backward_data(M, N, K, epi):
         assert rel(o32, base + ref) < 1e-5
 
 
+@pytest.mark.parametrize("variant", [0x500 | 0x10000, 0x300 | 0x10000, 8, 7])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 512), (300, 264, 520), (768, 520, 136), (256, 1024, 64)])
+def test_gemm_pipelined_and_persistent(variant, M, N, K):
+    """The software-pipelined K-step (128 x 128 variants 7 / 8, 256 x 256 variant 3) and the
+    persistent 256 x 256 kernel (variant 5: one block per CU walks the tiles, the last K-step
+    prefetches the next tile's first stage) on the forward and backward-data epilogues, the 256 x 256
+    tile forced at every K (bit 16), ragged edges and several tiles per block included."""
+    L = ML.lib()
+    assert L.mmt_gemm_set_variant(variant) == 0
+    try:
+        for epi in ["store_bf16", "bias_tanh_bf16", "bias_relu_bf16", "bias_resid_f32", "store_f32"]:
+            test_gemm_forward_linear(M, N, K, epi)
+        for epi in ["store_bf16", "dtanh_bf16", "drelu_bf16", "store_f32", "acc_f32"]:
+            test_gemm_backward_data(M, N, K, epi)
+    finally:
+        L.mmt_gemm_set_variant(-1)
+
+
 @pytest.mark.parametrize("M,N,R", [(384, 256, 4096), (1024, 256, 2048), (900, 450, 1000), (6, 32, 300), (32, 16, 77)])
 @pytest.mark.parametrize("splits", [1, 4, 0])
 def test_gemm_weight_grad(M, N, R, splits):

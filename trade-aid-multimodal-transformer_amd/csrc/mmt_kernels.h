@@ -95,6 +95,8 @@ struct GemmBatch {
   GemmProblem p[MMT_MAX_GROUP];
   int count;
   int xcd_plane;  // split-K launches: 1 = XCD-major remap of the whole (tile, split) plane
+  // diagnostic builds only (-DMMT_GEMM_STAMPS, tools/gemm_stamps.py): per-block s_memtime stamps
+  unsigned long long* stamps;
 };
 
 hipError_t mmt_launch_gemm(const GemmBatch& b, bool a_kc, bool b_kc, int epi, int splits, hipStream_t s);

@@ -296,7 +296,7 @@ constexpr int QKV2B_TILES = 8;  // 32-row tiles per wave (a block of 4 waves: 10
 __device__ __forceinline__ int q2_swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
 template <int HS>
-__global__ __launch_bounds__(256, HS == 64 ? 3 : 4) void qkv2_bwd_v2(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
+__global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
   constexpr int HH = HS / 2;
   constexpr int NOT = HS / 32;  // 32-column output tiles of dout (o)
   constexpr int KSO = HS / 16;  // k-steps over o for dh1
@@ -334,35 +334,34 @@ __global__ __launch_bounds__(256, HS == 64 ? 3 : 4) void qkv2_bwd_v2(Qkv2Batch b
 #pragma unroll
   for (int e = 0; e < 16; ++e) z[e] = 0.f;
 
-  // every tile's dout / h1 pieces are loaded QKV2B_AHEAD tiles ahead of its compute (registers, fully
-  // unrolled): with ~one 32-row tile of work per load round trip, a single tile in flight left the
-  // kernel latency-bound at half the HBM rate (C1: 63 us for 201 MB)
-  constexpr int AHEAD = HS == 32 ? 4 : 2;
-  u32x4 dv[QKV2B_TILES][KSO], hv[QKV2B_TILES][NI];
-  const int r0 = rb * RPB + w * 32 * QKV2B_TILES;
-  auto load = [&](int t) {
-    const int row = r0 + 32 * t + r;
+  u32x4 dv[KSO], hv[NI];
+  auto load = [&](int row) {
     const bool ok = row < R;
     const u32x4 zz = {0u, 0u, 0u, 0u};
     const bf16_t* d = P.dout + (int64_t)row * ld_out + blk * HS + 8 * h;
     const bf16_t* hp = P.h1 + (int64_t)row * ld_h1 + blk * HH + 8 * h;
 #pragma unroll
-    for (int s = 0; s < KSO; ++s) dv[t][s] = ok ? *reinterpret_cast<const u32x4*>(d + 16 * s) : zz;
+    for (int s = 0; s < KSO; ++s) dv[s] = ok ? *reinterpret_cast<const u32x4*>(d + 16 * s) : zz;
 #pragma unroll
-    for (int q = 0; q < NI; ++q) hv[t][q] = ok ? *reinterpret_cast<const u32x4*>(hp + 16 * q) : zz;
+    for (int q = 0; q < NI; ++q) hv[q] = ok ? *reinterpret_cast<const u32x4*>(hp + 16 * q) : zz;
   };
-#pragma unroll
-  for (int t = 0; t < AHEAD; ++t) load(t);
-#pragma unroll
+  const int r0 = rb * RPB + w * 32 * QKV2B_TILES;
+  load(r0 + r);
+#pragma unroll 1
   for (int t = 0; t < QKV2B_TILES; ++t) {
     const int row = r0 + 32 * t + r;
-    if (t + AHEAD < QKV2B_TILES) load(t + AHEAD);
-    const u32x4* dc = dv[t];
-    const u32x4* hc = hv[t];
+    if (r0 + 32 * t >= R) break;  // wave-uniform
+    u32x4 dc[KSO], hc[NI];
+#pragma unroll
+    for (int s = 0; s < KSO; ++s) dc[s] = dv[s];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) hc[q] = hv[q];
+    if (t + 1 < QKV2B_TILES) load(row + 32);  // the next tile's loads fly while this one computes
     // dh1 (accumulator rows = i in the permuted order: lane (r, h) gets i = 8 h + e, 16 + 8 h + e - 8)
     f32x16 acc = z;
 #pragma unroll
     for (int s = 0; s < KSO; ++s) acc = mfma32(wa[s], __builtin_bit_cast(bf16x8, dc[s]), acc);
+    u32x4 dz[NI];
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       float t8[8];
@@ -372,11 +371,11 @@ __global__ __launch_bounds__(256, HS == 64 ? 3 : 4) void qkv2_bwd_v2(Qkv2Batch b
         const float x = bf2f((bf16_t)((e & 1) ? (wd >> 16) : (wd & 0xffff)));
         t8[e] = acc[8 * q + e] * (1.f - x * x);
       }
-      const u32x4 dz = {pack2bf(t8[0], t8[1]), pack2bf(t8[2], t8[3]), pack2bf(t8[4], t8[5]), pack2bf(t8[6], t8[7])};
+      dz[q] = u32x4{pack2bf(t8[0], t8[1]), pack2bf(t8[2], t8[3]), pack2bf(t8[4], t8[5]), pack2bf(t8[6], t8[7])};
       if (row < R) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[8 * q + e] += t8[e];
-        *reinterpret_cast<u32x4*>(P.dh1 + (int64_t)row * ld_h1 + blk * HH + 16 * q + 8 * h) = dz;
+        *reinterpret_cast<u32x4*>(P.dh1 + (int64_t)row * ld_h1 + blk * HH + 16 * q + 8 * h) = dz[q];
       }
     }
     // dW2 over this tile's 32 rows: LDS images (rows past R hold zeros: their loads returned 0)
@@ -401,7 +400,6 @@ __global__ __launch_bounds__(256, HS == 64 ? 3 : 4) void qkv2_bwd_v2(Qkv2Batch b
 #pragma unroll
       for (int ot = 0; ot < NOT; ++ot) dw[ot] = mfma32(trd(img + ot * 2048), bh, dw[ot]);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's image writes
   }
   // block reductions: db1 (column sums) and dW2, then one atomic per element per block
   __syncthreads();
