@@ -1,5 +1,6 @@
 # Round profile set: benches (C1 with the CPU baseline, target shape), kernel traces (side stream on
-# and off; C3, C4), PMC HBM bytes (FETCH_SIZE / WRITE_SIZE, separate passes) at C1 and the target shape.
+# and off; C3, C4), PMC HBM bytes (FETCH_SIZE / WRITE_SIZE, separate passes) at every config, SQ
+# counters (two passes) at C1 and the target shape with the side stream off.
 # usage: bash tools/gpu_prof_round.sh <tag>     (outputs under gpurun_out/<tag>_*)
 T=${1:-v}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
@@ -8,12 +9,20 @@ bash tools/gpu_steps.sh \
  "200|${T}_bench_target|python -u bench.py --config target --no-cpu-baseline --steps 10" \
  "200|${T}_bench_c3|python -u bench.py --config c3 --no-cpu-baseline --steps 10" \
  "300|${T}_bench_c4|python -u bench.py --config c4 --no-cpu-baseline --steps 6 --warmup 2" \
- "300|${T}_prof_c1|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c1 -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline" \
- "300|${T}_prof_c1s|MMT_SIDE_STREAM=0 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c1s -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline" \
- "300|${T}_prof_ts|MMT_SIDE_STREAM=0 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_ts -o run -- python3 bench.py --config target --steps 10 --warmup 3 --no-cpu-baseline" \
- "300|${T}_prof_c3|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c3 -o run -- python3 bench.py --config c3 --steps 4 --warmup 2 --no-cpu-baseline --exact-steps 0" \
- "300|${T}_prof_c4|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c4 -o run -- python3 bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline --exact-steps 0" \
- "180|${T}_pmc_fetch|timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${T}_pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline" \
- "180|${T}_pmc_write|timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${T}_pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline" \
- "180|${T}_pmc_fetch_t|timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${T}_pmc_fetch_t -o run -- python3 bench.py --config target --steps 2 --warmup 1 --no-cpu-baseline" \
- "180|${T}_pmc_write_t|timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${T}_pmc_write_t -o run -- python3 bench.py --config target --steps 2 --warmup 1 --no-cpu-baseline"
+ "300|${T}_prof_c1|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c1 -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "300|${T}_prof_c1s|MMT_SIDE_STREAM=0 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c1s -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "300|${T}_prof_ts|MMT_SIDE_STREAM=0 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_ts -o run -- python3 bench.py --config target --steps 10 --warmup 3 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "300|${T}_prof_c3|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c3 -o run -- python3 bench.py --config c3 --steps 4 --warmup 2 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "300|${T}_prof_c4|rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof_c4 -o run -- python3 bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "180|${T}_pmc_fetch|timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${T}_pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "180|${T}_pmc_write|timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${T}_pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "180|${T}_pmc_fetch_t|timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${T}_pmc_fetch_t -o run -- python3 bench.py --config target --steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "180|${T}_pmc_write_t|timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${T}_pmc_write_t -o run -- python3 bench.py --config target --steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "180|${T}_pmc_fetch_c3|timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${T}_pmc_fetch_c3 -o run -- python3 bench.py --config c3 --steps 1 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "180|${T}_pmc_write_c3|timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${T}_pmc_write_c3 -o run -- python3 bench.py --config c3 --steps 1 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "180|${T}_pmc_fetch_c4|timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${T}_pmc_fetch_c4 -o run -- python3 bench.py --config c4 --steps 1 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "180|${T}_pmc_write_c4|timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${T}_pmc_write_c4 -o run -- python3 bench.py --config c4 --steps 1 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "150|${T}_sq_c1_pmc1|MMT_SIDE_STREAM=0 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS --output-format csv -d gpurun_out/${T}_sq_c1_pmc1 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "150|${T}_sq_c1_pmc2|MMT_SIDE_STREAM=0 timeout -s KILL 140 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/${T}_sq_c1_pmc2 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "150|${T}_sq_t_pmc1|MMT_SIDE_STREAM=0 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS --output-format csv -d gpurun_out/${T}_sq_t_pmc1 -o run -- python3 bench.py --config target --steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0" \
+ "150|${T}_sq_t_pmc2|MMT_SIDE_STREAM=0 timeout -s KILL 140 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/${T}_sq_t_pmc2 -o run -- python3 bench.py --config target --steps 2 --warmup 1 --no-cpu-baseline --exact-steps 0 --serial-steps 0"

@@ -7,6 +7,7 @@ s_waitcnt/barrier), WAIT_INST_ANY (issue stalls), ACTIVE_INST_ANY; MFMA busy per
 LDS bank-conflict share; instruction counts per wave.
 """
 import csv
+import gzip
 import sys
 from collections import defaultdict
 
@@ -15,7 +16,7 @@ def main():
     d = defaultdict(lambda: defaultdict(float))
     n = defaultdict(int)
     for path in sys.argv[1:]:
-        for r in csv.DictReader(open(path)):
+        for r in csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)):
             k = r["Kernel_Name"][:70]
             d[k][r["Counter_Name"]] += float(r["Counter_Value"])
             if r["Counter_Name"] in ("SQ_WAVE_CYCLES", "SQ_INSTS_VALU"):

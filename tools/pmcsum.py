@@ -7,13 +7,14 @@ FETCH_SIZE counts 64 B per 128-B request of a wide coalesced read, so it is doub
 is exact for 16-B-per-lane stores. Prints MB per dispatch (mean over dispatches) per kernel.
 """
 import csv
+import gzip
 import sys
 from collections import defaultdict
 
 
 def load(path):
     d = defaultdict(list)
-    for r in csv.DictReader(open(path)):
+    for r in csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)):
         d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     return d
 
