@@ -405,13 +405,15 @@ def test_attention_fwd_bwd(B, T, H, hs, ns):
         assert rel(heads(got_v[j]), vf[j].grad) < 2e-2, (j, rel(heads(got_v[j]), vf[j].grad))
 
 
-@pytest.mark.parametrize("ring", [0, 1, 3, 7])
-@pytest.mark.parametrize("B,T,H,ns", [(2, 100, 2, 1), (1, 520, 2, 2), (1, 1024, 1, 1), (2, 300, 2, 3), (1, 33, 2, 1)])
+@pytest.mark.parametrize("ring", [0, 1, 3, 7, 8, 15])
+@pytest.mark.parametrize("B,T,H,ns", [(2, 100, 2, 1), (1, 520, 2, 2), (1, 1024, 1, 1), (2, 300, 2, 3), (1, 33, 2, 1),
+                                      (3, 64, 2, 7)])
 def test_attention_hs64_backward_variants(B, T, H, ns, ring):
-    """Every hs-64 backward variant (mmt_attn_set_ring: 0 the chunked dQ and dK/dV passes, 1 the
-    slice-streamed dK/dV ring, 3 both rings with two query tiles per wave in the dQ ring, 7 (the
-    default) that with the dK/dV ring at 3 waves per SIMD) against the same torch reference, ragged T
-    and multi-stream included."""
+    """Every hs-64 attention variant (mmt_attn_set_ring: 0 the chunked dQ and dK/dV passes, 1 the
+    slice-streamed dK/dV ring, 3 both rings with two query tiles per wave in the dQ ring, 7 that with
+    the dK/dV ring at 3 waves per SIMD; bit 3 the slice-streamed forward: 8 with the chunked
+    backward, 15 everything on the rings) against the same torch reference, ragged T and
+    multi-stream (up to 7 KV streams) included."""
     L = ML.lib()
     old = L.mmt_attn_set_ring(ring)
     try:
@@ -537,3 +539,4 @@ def test_embedding(B, T, C, V):
     ref_tok = torch.zeros(V, C, device=DEV).index_add_(0, idx.view(-1), dx)
     torch.testing.assert_close(dtok, ref_tok, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dpos, dx.view(B, T, C).sum(0), rtol=1e-5, atol=1e-5)
+

@@ -64,6 +64,15 @@ def main():
     torch.cuda.synchronize()
     eager = (time.perf_counter() - t0) / a.steps * 1e3
     print(f"eager  {eager:.3f} ms/step", flush=True)
+    # host launch cost: enqueue a few steps without waiting (the GPU trails behind)
+    for n in (1, 3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+        host = (time.perf_counter() - t0) / n * 1e3
+        torch.cuda.synchronize()
+        print(f"host   {host:.3f} ms/step to enqueue ({n} steps)", flush=True)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         step()

@@ -1001,7 +1001,8 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
 }
 
 // attention variant knob (bit 0: the slice-streamed hs-64 dK/dV pass, bit 1: its dQ pass, bit 2: the
-// dK/dV pass at 3 waves per SIMD): MMT_ATTN_RING, or mmt_attn_set_ring() for in-process A/B
+// dK/dV pass at 3 waves per SIMD, bit 3: the slice-streamed hs-64 forward): MMT_ATTN_RING, or
+// mmt_attn_set_ring() for in-process A/B
 static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
   // both hs-64 passes on the rings (dQ: two query tiles per wave), dK/dV at 3 waves per SIMD
@@ -1036,6 +1037,8 @@ static hipError_t attn_launch(const AttnBatch& bt, int B, int T, int H, float sc
   if (!bwd) {
     bool drop = false;
     for (int g = 0; g < bt.count; ++g) drop = drop || bt.p[g].drop_thr != 0;
+    // hs 64, knob bit 3: the forward on the LDS-DMA slice ring (mmt_attn2.hip)
+    if (HS == 64 && (g_attn_ring & 8) && ring64_fits(bt, T)) return mmt_attn_fwd_ring64(bt, B, T, H, scale, drop, s);
     const dim3 grid(nb * B * H, 1, bt.count);
     if (drop) hipLaunchKernelGGL((attn_fwd_kernel<HS, true>), grid, dim3(256), 0, s, bt, T, H, scale);
     else hipLaunchKernelGGL((attn_fwd_kernel<HS, false>), grid, dim3(256), 0, s, bt, T, H, scale);

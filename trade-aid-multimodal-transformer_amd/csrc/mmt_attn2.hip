@@ -87,6 +87,35 @@ __device__ __forceinline__ void zero16(f32x16& a) {
 __device__ __forceinline__ float keep_f(float v, int m) { return __int_as_float(__float_as_int(v) & m); }
 __device__ __forceinline__ int key_dword(int r) { return 2 * ((r & 3) + 4 * (r >> 3)) + ((r >> 2) & 1); }
 
+// forward helpers (as mmt_attn.hip): cross-half reductions in one v_permlane32_swap, and the
+// accumulator registers 8s..8s+7 as a bf16 operand fragment with the keep bits of a lane word applied
+__device__ __forceinline__ float xh_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xh_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t keep_spread2(uint32_t w16) { return __builtin_amdgcn_perm(0u, w16, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t pair_keep2(uint32_t w32, int i) {
+  s16x2 v = __builtin_bit_cast(s16x2, w32 << (15 - i));
+  v = v >> (s16x2){15, 15};
+  return __builtin_bit_cast(uint32_t, v);
+}
+template <bool DROP>
+__device__ __forceinline__ bf16x8 p_frag(const f32x16& a, int s, uint32_t w32) {
+  u32x4 v = {pack2bf(a[8 * s], a[8 * s + 1]), pack2bf(a[8 * s + 2], a[8 * s + 3]), pack2bf(a[8 * s + 4], a[8 * s + 5]),
+             pack2bf(a[8 * s + 6], a[8 * s + 7])};
+  if (DROP) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] &= pair_keep2(w32, 4 * s + q);
+  }
+  return __builtin_bit_cast(bf16x8, v);
+}
+constexpr float kTauR = 8.0f;  // lazy-rescale threshold of the running max (log2 units), as mmt_attn.hip
+
 }  // namespace
 
 // =============================================================================================
@@ -527,6 +556,242 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
         if (okq[u])
           *reinterpret_cast<u32x4*>(P.dq + (rowbase + tq[u]) * P.dq_ld + head * 64 + d0) = u32x4{s0[0], s1[0], s0[1], s1[1]};
       }
+}
+
+// =============================================================================================
+// Forward at hs 64, two query tiles per wave, on the same LDS-DMA slice ring as the dQ pass: grid
+// (nqb * B*H, 1, problems); a workgroup owns query tiles 8 qb .. 8 qb + 7 (wave w: A = 8 qb + w,
+// B = 8 qb + 7 - w) and walks (stream j, key tile 0 .. 8 qb + 7); each slice brings the key tile's K
+// and V images and the keep-bit lane words of the block's 8 query tiles. Per slice a wave reads K
+// rows (S^T = K Q^T, keys on accumulator rows, queries on lanes) and V transposed (O^T += V^T P^T)
+// once for both of its tiles. Online softmax in the log2 domain with the lazy rescale of
+// mmt_attn.hip (threshold kTauR); at the last key tile of a stream the outputs are normalised and
+// stored with the stream's LSE. The chunked forward (mmt_attn.hip) re-staged 128-row chunks through
+// VGPRs behind two barriers per chunk; its register prefetch of the next chunk does not fit at hs 64.
+// =============================================================================================
+template <bool DROP, int S>
+__global__ __launch_bounds__(256, 2) void attn_fwd_ring64x2(AttnBatch batch, int T, int H, float scale) {
+  constexpr int NKS = 4, ND = 2;
+  static_assert(S >= 3 && 3 * (S - 2) <= 16, "ring slots: S - 1 slices in flight, counted waits <= 16");
+  constexpr int OFF_V = IMG64, OFF_M = 2 * IMG64;
+  constexpr int SLOT = OFF_M + (DROP ? 1024 : 0);
+  __shared__ __attribute__((aligned(1024))) char lds[S * SLOT];
+  const AttnProblem& P = batch.p[blockIdx.z];
+  const int nt = (T + 31) / 32;
+  const int nqb = (nt + 7) / 8;
+  const int ns = P.nstreams;
+  const int BH = gridDim.x / nqb;
+  const int qb = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (last) query block first
+  const int bh = blockIdx.x % BH;
+  const int b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int qt[2] = {8 * qb + w, 8 * qb + 7 - w};
+  const bool live[2] = {qt[0] < nt, qt[1] < nt};
+  const int tq[2] = {qt[0] * 32 + r, qt[1] * 32 + r};
+  const bool okq[2] = {live[0] && tq[0] < T, live[1] && tq[1] < T};
+  const int nk = min(8 * qb + 8, nt);  // key tiles walked per stream
+  const int nsl = ns * nk;             // slices
+  const int64_t rowbase = (int64_t)b * T;
+  const float c2 = scale * kLog2e2;
+
+  // Q of both query tiles (queries on lanes: the B operand of S^T)
+  bf16x8 qf[2][NKS];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const bf16_t* qp = P.q + (rowbase + tq[u]) * P.q_ld + head * 64;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      u32x4 v = okq[u] ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * h) : z;
+      asm volatile("" : "+v"(v));  // consumed here: the wait for these loads sits before the DMA prologue
+      qf[u][s] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  f32x16 o[2][ND];
+  float m[2], l[2];
+
+  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+  const int64_t ntiles = (int64_t)BH * ntri;
+  const int prow = lane >> 1;
+  const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
+  const int per = 2 + (DROP && w == 0 ? 1 : 0);
+  auto issue = [&](int slot, int sl) {
+    char* sb = lds + slot * SLOT;
+    const int j = sl / nk, kt = sl % nk;
+    const int grow = kt * 32 + prow;
+    const i32x4 rk = make_rsrc(P.k[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+    const i32x4 rv = make_rsrc(P.v[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int piece = 2 * w + u;  // 0..3: K column block, 4..7: V
+      const int op = piece >> 2, cb = piece & 3;
+      const int voff = grow < T ? (grow * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
+      dma16(op ? rv : rk, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_V + cb * SUB)), voff);
+    }
+    if (DROP && w == 0) {  // lane words of (query tile 8 qb + u, key tile kt), u = 0..7: 8 x 128 B
+      const i32x4 rm = make_rsrc(P.dmask[j] + (ntiles + (int64_t)bh * ntri) * 32, ntri * 128);
+      const int u = lane >> 3, q_ = 8 * qb + u;
+      const int voff = (q_ < nt && kt <= q_) ? (q_ * (q_ + 1) / 2 + kt) * 128 + (lane & 7) * 16 : OOB;
+      dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nsl) issue(i, i);
+
+  const int o_row = img_off(r, 0, h);
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int o_tr0 = img_off(4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
+  const int o_tr1 = img_off(8 + 4 * (g >> 1) + q, g & 1, p >> 1) + 8 * (p & 1);
+  // online softmax of one S^T tile of query tile u (masked: the causal diagonal)
+  auto softmax = [&](f32x16& sa, int u, int kt, bool masked) {
+    if (masked) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int key = kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (key > tq[u]) sa[e] = -INFINITY;
+      }
+    }
+    float tmax = sa[0];
+#pragma unroll
+    for (int e = 1; e < 16; ++e) tmax = fmaxf(tmax, sa[e]);
+    tmax = xh_max(tmax) * c2;
+    const bool up = tmax > m[u] + kTauR;
+    if (__builtin_amdgcn_ballot_w64(up)) {  // wave-uniform
+      const float alpha = up ? __builtin_amdgcn_exp2f(m[u] - tmax) : 1.f;
+      m[u] = up ? tmax : m[u];
+      l[u] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[u][dt][e] *= alpha;
+    }
+    const float nm = -m[u];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sa[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[e], c2, nm));
+    float r0 = sa[0] + sa[1], r1 = sa[2] + sa[3], r2 = sa[4] + sa[5], r3 = sa[6] + sa[7];
+    r0 += sa[8] + sa[9]; r1 += sa[10] + sa[11]; r2 += sa[12] + sa[13]; r3 += sa[14] + sa[15];
+    l[u] += (r0 + r1) + (r2 + r3);
+  };
+  const float dsc = DROP ? P.drop_scale : 1.f;
+  // normalise and store stream j's outputs of query tile u (and its LSE, log2 domain)
+  auto finish = [&](int u, int j) {
+    const float lt = xh_sum(l[u]);
+    const float inv = lt > 0.f ? dsc / lt : 0.f;
+    u32x4 ov[ND][2];
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int ga = 2 * pr, gb = 2 * pr + 1;
+        const uint32_t x0 = pack2bf(o[u][dt][4 * ga] * inv, o[u][dt][4 * ga + 1] * inv);
+        const uint32_t x1 = pack2bf(o[u][dt][4 * ga + 2] * inv, o[u][dt][4 * ga + 3] * inv);
+        const uint32_t y0 = pack2bf(o[u][dt][4 * gb] * inv, o[u][dt][4 * gb + 1] * inv);
+        const uint32_t y1 = pack2bf(o[u][dt][4 * gb + 2] * inv, o[u][dt][4 * gb + 3] * inv);
+        const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        ov[dt][pr] = u32x4{s0[0], s1[0], s0[1], s1[1]};  // d = dt*32 + 16 pr + 8 h + 0..7
+      }
+    if (okq[u]) {
+      if (h == 0) P.lse[j][(int64_t)bh * T + tq[u]] = m[u] + __log2f(lt);
+      bf16_t* dst = (ns > 1 ? P.oj[j] : P.o) + (rowbase + tq[u]) * P.o_ld + head * 64;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) *reinterpret_cast<u32x4*>(dst + dt * 32 + 16 * pr + 8 * h) = ov[dt][pr];
+    }
+  };
+#pragma unroll 1
+  for (int i = 0; i < nsl; ++i) {
+    wait_vm(per * min(S - 2, nsl - 1 - i));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (i + S - 1 < nsl) issue((i + S - 1) % S, i + S - 1);
+    const int j = i / nk, kt = i % nk;
+    if (kt == 0) {  // a stream's walk starts
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        m[u] = -INFINITY;
+        l[u] = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) zero16(o[u][dt]);
+      }
+    }
+    // tile B (the later one) may need a key tile that A does not (or lie past the sequence)
+    const bool needA = live[0] && kt <= qt[0], needB = live[1] && kt <= qt[1];
+    if (needA || needB) {
+      const char* sb = lds + (i % S) * SLOT;
+      bf16x8 kf[NKS], vtr[2][ND];
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(sb + o_row + s * SUB);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+          vtr[s][dt] = join4(lds_tr16(sb + OFF_V + o_tr0 + 512 * s + 2 * SUB * dt),
+                             lds_tr16(sb + OFF_V + o_tr1 + 512 * s + 2 * SUB * dt));
+      const uint32_t wa = DROP ? keep_spread2(reinterpret_cast<const uint16_t*>(sb + OFF_M)[w * 64 + lane]) : 0u;
+      const uint32_t wb = DROP ? keep_spread2(reinterpret_cast<const uint16_t*>(sb + OFF_M)[(7 - w) * 64 + lane]) : 0u;
+      f32x16 sa, sb2;
+      zero16(sa);
+      zero16(sb2);
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        if (needA) sa = mfma32(kf[s], qf[0][s], sa);
+        if (needB) sb2 = mfma32(kf[s], qf[1][s], sb2);
+      }
+      if (needA) softmax(sa, 0, kt, kt == qt[0]);
+      if (needB) softmax(sb2, 1, kt, kt == qt[1]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (needA) {
+          const bf16x8 pa = p_frag<DROP>(sa, s, wa);
+#pragma unroll
+          for (int dt = 0; dt < ND; ++dt) o[0][dt] = mfma32(vtr[s][dt], pa, o[0][dt]);
+        }
+        if (needB) {
+          const bf16x8 pb = p_frag<DROP>(sb2, s, wb);
+#pragma unroll
+          for (int dt = 0; dt < ND; ++dt) o[1][dt] = mfma32(vtr[s][dt], pb, o[1][dt]);
+        }
+      }
+    }
+    if (kt == nk - 1) {
+      if (live[0]) finish(0, j);
+      if (live[1]) finish(1, j);
+    }
+  }
+  // several streams: the output is the sum of the per-stream outputs this lane just wrote
+  if (ns > 1) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!okq[u]) continue;
+      const int64_t off = (rowbase + tq[u]) * P.o_ld + head * 64;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const int d0 = dt * 32 + 16 * pr + 8 * h;
+          float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          for (int jj = 0; jj < ns; ++jj) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(P.oj[jj] + off + d0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { t[2 * e] += bf2f(v[e] & 0xffff); t[2 * e + 1] += bf2f(v[e] >> 16); }
+          }
+          *reinterpret_cast<u32x4*>(P.o + off + d0) =
+              u32x4{pack2bf(t[0], t[1]), pack2bf(t[2], t[3]), pack2bf(t[4], t[5]), pack2bf(t[6], t[7])};
+        }
+    }
+  }
+}
+
+hipError_t mmt_attn_fwd_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, hipStream_t s) {
+  const int nt = (T + 31) / 32;
+  const dim3 g2(((nt + 7) / 8) * B * H, 1, bt.count);
+  if (drop) hipLaunchKernelGGL((attn_fwd_ring64x2<true, 4>), g2, dim3(256), 0, s, bt, T, H, scale);
+  else hipLaunchKernelGGL((attn_fwd_ring64x2<false, 4>), g2, dim3(256), 0, s, bt, T, H, scale);
+  return hipGetLastError();
 }
 
 // ring depth 4 (three slices in flight): depth 6 measured slower (target backward 294 -> 301 us, C4

@@ -858,13 +858,14 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   // LayerNorm forwards already done by the previous residual GEMM's epilogue (lnf_fused: the post
   // block's); fused only in bf16 at C == 256 (whole rows per 256x256 tile), MMT_LN_FUSE=0 or
   // MMT_LN_FUSE_FWD=0 disables
-  static const bool ln_fuse = [] {
+  static const int ln_fuse = [] {
     const char* e = getenv("MMT_LN_FUSE");
     const char* f = getenv("MMT_LN_FUSE_FWD");
-    return (e ? atoi(e) != 0 : true) && (f ? atoi(f) != 0 : true);
+    return (e ? atoi(e) != 0 : true) ? (f ? atoi(f) : 1) : 0;
   }();
-  // (C = 512 on the 128 x 512 tile measured slower: target 20.09 -> 20.43 ms, profiles/r3u_ab.txt)
-  const bool fuse_fwd = ln_fuse && !f8 && C == 256;
+  // C = 512 (128 x 512 tile) only with MMT_LN_FUSE_FWD=2: measured slower on the 2-stage ring
+  // (target 20.09 -> 20.43 ms, profiles/r3u_ab.txt)
+  const bool fuse_fwd = ln_fuse && !f8 && (C == 256 || (C == 512 && ln_fuse == 2));
   std::vector<char> ln1_done(M, 0), lnf_done(M, 0);
   for (int l = 0; l < c->L && r.rc == MMT_OK; ++l) {
     const LM* x = &c->lm[(size_t)l * M];

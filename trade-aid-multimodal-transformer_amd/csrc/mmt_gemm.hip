@@ -582,22 +582,51 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, f32x16 (&acc
 // the accumulator registers: lane (r, h) holds h1[r][4h + 0..3] and h1[r][8 + 4h + 0..3] of a
 // 16-column block (accumulator groups g and g + 1), which is a K-16 B operand with K permuted
 // (slot j <-> k = 4h + j, j < 4; 8 + 4h + j - 4, j >= 4) -- the W2 fragment takes the same
-// permutation. No LDS, no barrier; 16-B row stores after a v_permlane32_swap of the two halves.
+// permutation. A 32 x 32 stage-1 sub-tile yields 64 consecutive output columns (2 n0 + ...) of 32
+// rows: they cross a wave-private LDS slot (no block barrier) so they leave as 128-B row segments,
+// 8 rows per store instruction (storing the MFMA layout directly touches 32 rows x 32 B per store
+// and ran the target's qkv1 launch 169 us against 78 + 65 for the unfused pair).
+// The W2 fragments of the tile's stage-1 column blocks, converted to bf16 and permuted once per block
+// into LDS at kernel start (before the K loop; the epilogue reads them with one ds_read_b128 each):
+// fragment (b, ot, kh) of local block b = lane-ordered 16-B pieces at ((b * 2 + ot) * 2 + kh) KiB
+// (HH = 16: ot = kh = 0, fragment b at b KiB). Fetching them from global fp32 inside the epilogue
+// put two dependent global loads in front of every sub-tile's MFMAs.
+constexpr int QKV2_W2_LDS = 16384;
 template <class TL>
-__device__ __forceinline__ void qkv2_fused(const GemmProblem& P, f32x16 (&acc)[TL::TN][TL::TM], float alpha, int m0,
-                                           int n0, int lane, int wave) {
+__device__ __forceinline__ void qkv2_stage_w2(const GemmProblem& P, char* w2l, int n0, int tid) {
+  const int HH = P.qkv2_hh, HS = 2 * HH;
+  const int nfrag = HH == 32 ? (TL::BN / 32) * 4 : TL::BN / 16;  // 16 (HH 32) or 8 (HH 16)
+  const int blk0 = n0 / HH, nblk = P.N / HH;
+  for (int q = tid; q < nfrag * 64; q += TL::NT) {
+    const int f = q >> 6, ln = q & 63, r = ln & 31, h = ln >> 5;
+    const int b = HH == 32 ? f >> 2 : f, ot = HH == 32 ? (f >> 1) & 1 : 0, kh = HH == 32 ? f & 1 : 0;
+    u32x4 u = {0u, 0u, 0u, 0u};
+    if (blk0 + b < nblk) {
+      const float* w = P.qkv2_w2 + ((int64_t)(blk0 + b) * HS + ot * 32 + r) * HH + 16 * kh + 4 * h;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(w);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(w + 8);
+      u = u32x4{pack2bf(lo[0], lo[1]), pack2bf(lo[2], lo[3]), pack2bf(hi[0], hi[1]), pack2bf(hi[2], hi[3])};
+    }
+    *reinterpret_cast<u32x4*>(w2l + f * 1024 + ln * 16) = u;
+  }
+}
+
+template <class TL>
+__device__ __forceinline__ void qkv2_fused(const GemmProblem& P, f32x16 (&acc)[TL::TN][TL::TM], char* lds, char* w2l,
+                                           float alpha, int m0, int n0, int lane, int wave) {
   constexpr int TM = TL::TM, TN = TL::TN;
+  constexpr int SROW = 144;  // slot row pitch (128 B of bf16 + 16 B pad)
   const int wm = wave / TL::WN, wn = wave % TL::WN;
   const int h = lane >> 5, r = lane & 31;
   const int M = P.M, N = P.N, HH = P.qkv2_hh, HS = 2 * HH;
   const int nw = n0 + wn * TN * 32;  // first stage-1 column of this wave
+  char* slot = lds + wave * 32 * SROW;
   // W2 fragment of block blk, output tile ot, K-16 half kh (HH = 32: two halves): lane (o, h), slot j
+  // (staged in LDS by qkv2_stage_w2)
+  const int blk0 = n0 / HH;
   auto w2frag = [&](int blk, int ot, int kh) {
-    const float* w = P.qkv2_w2 + ((int64_t)blk * HS + ot * 32 + r) * HH + 16 * kh + 4 * h;
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(w);
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(w + 8);
-    const u32x4 u = {pack2bf(lo[0], lo[1]), pack2bf(lo[2], lo[3]), pack2bf(hi[0], hi[1]), pack2bf(hi[2], hi[3])};
-    return __builtin_bit_cast(bf16x8, u);
+    const int f = HH == 32 ? ((blk - blk0) * 2 + ot) * 2 + kh : blk - blk0;
+    return *reinterpret_cast<const bf16x8*>(w2l + f * 1024 + lane * 16);
   };
   // accumulator elements [8q, 8q + 8) of a sub-tile as a bf16 B operand (16 columns of h1)
   auto hfrag = [&](const f32x16& a, int q) {
@@ -605,9 +634,9 @@ __device__ __forceinline__ void qkv2_fused(const GemmProblem& P, f32x16 (&acc)[T
                      pack2bf(a[8 * q + 4], a[8 * q + 5]), pack2bf(a[8 * q + 6], a[8 * q + 7])};
     return __builtin_bit_cast(bf16x8, u);
   };
-  // D[o][m] of output tile ot of block blk, m = row sub-tile j: 16-B row pieces
-  auto store = [&](const f32x16& d, int blk, int ot, int j) {
-    const int m = m0 + wm * TM * 32 + 32 * j + r;
+  // D[o][m] (32 output columns c0 + o of the sub-tile's 64, rows m = lanes) into the slot: 16-B row
+  // pieces after a v_permlane32_swap of the two halves
+  auto put = [&](const f32x16& d, int c0) {
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
       const int ga = 2 * pr, gb = 2 * pr + 1;
@@ -615,39 +644,46 @@ __device__ __forceinline__ void qkv2_fused(const GemmProblem& P, f32x16 (&acc)[T
                                                        false, false);
       const auto s1 = __builtin_amdgcn_permlane32_swap(pack2bf(d[4 * ga + 2], d[4 * ga + 3]),
                                                        pack2bf(d[4 * gb + 2], d[4 * gb + 3]), false, false);
-      if (m < M)  // o = ot*32 + 16 pr + 8 h + 0..7
-        *reinterpret_cast<u32x4*>(P.qkv2_out + (int64_t)m * P.qkv2_ld + blk * HS + ot * 32 + 16 * pr + 8 * h) =
-            u32x4{s0[0], s1[0], s0[1], s1[1]};
+      *reinterpret_cast<u32x4*>(slot + r * SROW + (c0 + 16 * pr + 8 * h) * 2) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    }
+  };
+  // the slot's 32 rows x 64 columns to out[m0j + row][2 nb + col]: 8 rows of 128 B per store
+  auto drain = [&](int nb, int j) {
+    const int mj = m0 + wm * TM * 32 + 32 * j;
+    const int cc = (lane & 7) * 8, cg = 2 * nb + cc;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int row = 8 * it + (lane >> 3);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(slot + row * SROW + cc * 2);
+      if (mj + row < M && cg < 2 * N)
+        *reinterpret_cast<u32x4*>(P.qkv2_out + (int64_t)(mj + row) * P.qkv2_ld + cg) = v;
     }
   };
   f32x16 z;
 #pragma unroll
   for (int e = 0; e < 16; ++e) z[e] = 0.f;
-  // one 32x32 sub-tile at a time (activation, then its stage-2 MFMAs and stores): every value is
+  __syncthreads();  // the slots overlay the stage ring: every wave's last K-step reads are done
+  // one 32x32 sub-tile at a time (activation, then its stage-2 MFMAs, slot, stores): every value is
   // produced right before its use, so the epilogue stays inside the main loop's register budget
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
     const int nb = nw + 32 * i;
-    f32x4 bv[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = nb + 8 * g + 4 * h;
-      bv[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (P.bias && n + 4 <= N) bv[g] = *reinterpret_cast<const f32x4*>(P.bias + n);
-    }
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
+      // (the bias is already in the accumulators: gemm_kernel starts them at bias / alpha)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = fast_tanh(alpha * acc[i][j][e] + bv[e >> 2][e & 3]);
-      if (HH == 16) {
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = fast_tanh(alpha * acc[i][j][e]);
+      if (nb < N) {
+        if (HH == 16) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
-          if (nb + 16 * q < N) store(mfma32(w2frag((nb + 16 * q) / 16, 0, 0), hfrag(acc[i][j], q), z), (nb + 16 * q) / 16, 0, j);
-      } else if (nb < N) {  // HH == 32: K = 32 in two halves, two output tiles
-        const bf16x8 h0 = hfrag(acc[i][j], 0), h1 = hfrag(acc[i][j], 1);
+          for (int q = 0; q < 2; ++q)
+            if (nb + 16 * q < N) put(mfma32(w2frag((nb + 16 * q) / 16, 0, 0), hfrag(acc[i][j], q), z), 32 * q);
+        } else {  // HH == 32: K = 32 in two halves, two output tiles
+          const bf16x8 h0 = hfrag(acc[i][j], 0), h1 = hfrag(acc[i][j], 1);
 #pragma unroll
-        for (int ot = 0; ot < 2; ++ot)
-          store(mfma32(w2frag(nb / 32, ot, 1), h1, mfma32(w2frag(nb / 32, ot, 0), h0, z)), nb / 32, ot, j);
+          for (int ot = 0; ot < 2; ++ot) put(mfma32(w2frag(nb / 32, ot, 1), h1, mfma32(w2frag(nb / 32, ot, 0), h0, z)), 32 * ot);
+        }
+        drain(nb, j);  // (LDS ops of one wave complete in order: the next put cannot pass these reads)
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -712,7 +748,9 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   constexpr int EPI_ROWS = (GBN >= 512 || (GBM == 128 && GBN == 256)) ? 32 : (GBM == 128 && MINB == 1) ? 128 : 64;
   constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
   constexpr int LDS_MAIN = RING > CTILE ? RING : CTILE;
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN];
+  // + the fused Q/K/V stage 2's W2 fragments (qkv2_stage_w2)
+  constexpr int LDS_W2 = (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4) ? QKV2_W2_LDS : 0;
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN + LDS_W2];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -726,6 +764,24 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
     for (int j = 0; j < AJ; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+  if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4) {
+    // fused Q/K/V stage 2: the accumulators start at bias / alpha, so the epilogue (short of
+    // registers at 3 blocks per CU) holds no bias values
+    if (P.qkv2_out) qkv2_stage_w2<TL>(P, lds + LDS_MAIN, n0, tid);  // read after the epilogue's barrier
+    if (P.qkv2_out && P.bias) {
+      const float ia = 1.0f / P.alpha;
+      const int hh = (tid & 63) >> 5;
+#pragma unroll
+      for (int i = 0; i < AI; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int n = n0 + wn * TL::TN * 32 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          const float bv = n < N ? P.bias[n] * ia : 0.0f;
+#pragma unroll
+          for (int j = 0; j < AJ; ++j) acc[i][j][e] = bv;
+        }
+    }
+  }
 
   if (ks0 < ks1) {
     // buffer descriptors over each operand's whole extent (range-checked: OOB pieces read 0)
@@ -866,7 +922,7 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   // accumulators it spills (the launcher refuses qkv2_out there; the engine then runs qkv2_fwd)
   if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4) {
     if (P.qkv2_out) {  // the per-head stage 2 of Q/K/V (uniform per problem)
-      qkv2_fused<TL>(P, acc, alpha, m0, n0, lane, wave);
+      qkv2_fused<TL>(P, acc, lds, lds + LDS_MAIN, alpha, m0, n0, lane, wave);
       epilogue_swap<TL, EPI, EPI_ROWS, true>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
     } else {
       epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
@@ -1315,7 +1371,9 @@ static bool use_big(const GemmBatch& b) {
 // whole hh-blocks (N % hh == 0)
 static bool qkv2_ok(const GemmProblem& P, int epi, bool fwd) {
   if (!P.qkv2_out) return true;
+  // (no alpha_ptr, alpha != 0: the accumulators start at bias / alpha)
   return epi == EPI_BIAS_TANH_BF16 && fwd && (P.qkv2_hh == 16 || P.qkv2_hh == 32) && P.N % P.qkv2_hh == 0 &&
+         !P.alpha_ptr && P.alpha != 0.0f &&
          P.qkv2_w2 && !(P.qkv2_ld & 7) && !((uintptr_t)P.qkv2_out & 15) && !((uintptr_t)P.qkv2_w2 & 15);
 }
 
@@ -1488,6 +1546,13 @@ bool mmt_gemm_resid_ln_ok(const GemmBatch& b) {
   return true;
 }
 
+// ring depth of the 128 x 512 row-wide GEMMs (LayerNorm backward / forward fused): 3 stages of BK 32
+// (120 KiB, one block per CU) against 2 (80 KiB, two blocks per CU): target step 20.39 -> 19.64 ms
+// with the LayerNorm-backward GEMMs on it, 4 stages equal to 3 (profiles/r4k_ab.txt); at 2 stages the
+// next K-step's DMA had one 32-deep step of MFMAs to hide under
+#ifndef MMT_GEMM_W_ST
+#define MMT_GEMM_W_ST 3
+#endif
 hipError_t mmt_launch_gemm_resid_ln(const GemmBatch& b, hipStream_t s) {
   if (!mmt_gemm_resid_ln_ok(b)) return hipErrorInvalidValue;
   // a tile as wide as the row whatever K (its block owns whole rows): 256 x 256 (as launch_t's big
@@ -1496,7 +1561,7 @@ hipError_t mmt_launch_gemm_resid_ln(const GemmBatch& b, hipStream_t s) {
     const int mt = max_tiles<TileW>(b, nullptr);
     if (mt == 0) return hipSuccess;
     if (g_pipe) launch_v<TileW, 32, 2, true, true, true, EPI_BIAS_RESID_F32, 1, 1>(b, dim3(mt, 1, b.count), s);
-    else launch_v<TileW, 32, 2, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
+    else launch_v<TileW, 32, MMT_GEMM_W_ST, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
   } else {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
@@ -1528,7 +1593,7 @@ hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
     const int mt = max_tiles<TileW>(b, nullptr);
     if (mt == 0) return hipSuccess;
     if (g_pipe) launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32, 1, 1>(b, dim3(mt, 1, b.count), s);
-    else launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+    else launch_v<TileW, 32, MMT_GEMM_W_ST, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
   } else {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;

@@ -211,6 +211,7 @@ hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& b, int B, int T, int H, flo
                                     hipStream_t s);
 // hs 64 dQ pass (and D_j) streaming the key slices through an LDS-DMA ring (mmt_attn2.hip)
 hipError_t mmt_attn_bwd_dq_ring64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, hipStream_t s);
+hipError_t mmt_attn_fwd_ring64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, hipStream_t s);
 // fill dmask[j] (j < nstreams) of every problem with drop_thr != 0 from its counter hash
 hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStream_t s);
 

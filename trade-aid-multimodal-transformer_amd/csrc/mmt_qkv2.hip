@@ -5,7 +5,6 @@
 // backward  dh1^T[i][r] = (sum_o W2[o][i] dout[r][o]) * (1 - h1[r][i]^2)
 //           dW2[o][i]  += sum_r dout[r][o] h1[r][i]        K = rows, operands by transposed LDS reads
 // blk = kind*H + head; h1 / dh1 rows hold nblk*hs/2 columns, out / dout rows nblk*hs columns.
-#include <stdlib.h>
 
 #include <type_traits>
 
@@ -445,8 +444,8 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
 template <int HS>
 static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_out, bool bwd, hipStream_t s) {
   constexpr int RPB = 4 * 32 * QKV2B_TILES;
-  static const bool v1 = getenv("MMT_QKV2_BWD_V1") && atoi(getenv("MMT_QKV2_BWD_V1"));  // (diagnostic)
-  if (bwd && (HS == 32 || HS == 64) && !v1)
+  // (v2 against qkv2_bwd_mfma in the step: C1 8.818 vs 8.832 ms, target 20.39 vs 20.48: profiles/r4k_ab.txt)
+  if (bwd && (HS == 32 || HS == 64))
     hipLaunchKernelGGL(qkv2_bwd_v2<HS == 64 ? 64 : 32>, dim3((R + RPB - 1) / RPB * nblk, 1, b.count), dim3(256), 0, s, b,
                        R, ld_h1, ld_out);
   else if (bwd)
