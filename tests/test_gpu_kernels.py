@@ -258,7 +258,10 @@ def test_layernorm(R, C):
 
 @pytest.mark.parametrize("M,N,K,drop", [(1000, 256, 1024, 0.0), (256, 256, 384, 0.1), (300, 256, 72, 0.1),
                                          (4096, 256, 256, 0.0), (2, 256, 450, 0.1), (1000, 512, 2048, 0.0),
-                                         (300, 512, 768, 0.1), (130, 512, 72, 0.1)])
+                                         (300, 512, 768, 0.1), (130, 512, 72, 0.1),
+                                         # every CU busy with the 128 x 512 tile's 3-stage ring (5 DMA
+                                         # pieces per stage: the counted waits must be exact)
+                                         (65536, 512, 2048, 0.0)])
 def test_gemm_ln_bwd_fused(M, N, K, drop):
     """Backward-data GEMM with the LayerNorm backward fused into its epilogue (the engine's path at
     C = 256) against torch: dy = alpha A B in fp32, F.layer_norm's autograd for dx / dgamma / dbeta,

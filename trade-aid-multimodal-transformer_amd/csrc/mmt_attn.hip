@@ -1007,8 +1007,9 @@ static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
   // both hs-64 passes on the rings (dQ: two query tiles per wave), dK/dV at 3 waves per SIMD
   // (standalone backward: target 277 -> 273 us, C3 cross-attention 2461 -> 2298, C4 2237 -> 2116;
-  // C3 step -1.5 %: profiles/r3u_ring_ab.txt)
-  return e ? atoi(e) : 7;
+  // C3 step -1.5 %: profiles/r3u_ring_ab.txt), and the forward on the ring too (round 4: target
+  // 20.42 -> 20.34 ms, C3 157.3 -> 153.8 ms same box, profiles/r4m_ab.txt)
+  return e ? atoi(e) : 15;
 }();
 extern "C" int mmt_attn_set_ring(int v) {
   const int old = g_attn_ring;

@@ -248,12 +248,26 @@ __device__ __forceinline__ void epi_pad(const GemmProblem& P, int m, int n) {
 }
 
 __device__ __forceinline__ void wait_vm(int n) {
-  // counted wait on this wave's outstanding LDS-DMA pieces (immediate operand: one case each)
+  // counted wait on this wave's outstanding LDS-DMA pieces (immediate operand: one case each; every
+  // count up to 16 exact — the 128 x 512 tile issues 5 pieces per stage — and above it vmcnt(16),
+  // which waits for more, never for less)
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
   }
 }
@@ -1282,6 +1296,16 @@ static int g_big_variant = [] {
   return e ? atoi(e) : (g_pipe ? 3 : 0);
 }();
 
+// default 128 x 128 pipelines (build-time, tools/build_variant.py A/B): bf16-output epilogues at 3
+// blocks per CU (variant 6: BK 32 x 2), the others at 2 (variant 0: BK 64 x 2). Deeper rings lose
+// in the step (round 4, profiles/r4m_ab.txt: variant 5 for the former C1 +0.6 %, variants 2 / 4 for
+// the latter C1 +0.6 / +5.5 %, target +0.5 / +5.3 %)
+#ifndef MMT_OCC3_VARIANT
+#define MMT_OCC3_VARIANT 6
+#endif
+#ifndef MMT_DEF_VARIANT
+#define MMT_DEF_VARIANT 0
+#endif
 template <bool A_KC, bool B_KC, bool SWAP, int EPI>
 static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t s) {
   if (b.count == 0) return hipSuccess;
@@ -1329,7 +1353,7 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
   // the step beside the side stream, 20.21 -> 20.37 ms: profiles/r3y_tilem_ab.txt; removed in round 4)
   const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw
                   : (!A_KC && !B_KC && env_dw >= 0) ? env_dw
-                  : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? (g_pipe ? 8 : 6) : (g_pipe ? 7 : 0));
+                  : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? (g_pipe ? 8 : MMT_OCC3_VARIANT) : (g_pipe ? 7 : MMT_DEF_VARIANT));
   switch (var) {
     case 1: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 2: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
