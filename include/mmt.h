@@ -256,6 +256,11 @@ int mmt_op_embedding_fwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t 
                          const float* tok, const float* pos, float* x);
 int mmt_op_embedding_bwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx,
                          const float* dx, float* dtok, float* dpos);
+/* the same with a caller scratch of >= B*T*C floats (the engine passes a free backward buffer): each
+ * row chunk's LDS-privatised token-table slabs are stored there and one reduce pass adds them into
+ * dtok, so the rows split into short chunks without global atomics; dtok is accumulated (+=) */
+int mmt_op_embedding_bwd_ws(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx,
+                            const float* dx, float* dtok, float* dpos, float* scratch);
 
 /* ---- MX-fp8 primitives (C4's fp8 path; BASELINE configs[4]) --------------------------------
  * MX-fp8 = OCP e4m3fn bytes + one E8M0 exponent byte (bias 127) per 32 consecutive K elements of a

@@ -543,3 +543,27 @@ def test_embedding(B, T, C, V):
     torch.testing.assert_close(dtok, ref_tok, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dpos, dx.view(B, T, C).sum(0), rtol=1e-5, atol=1e-5)
 
+
+@pytest.mark.parametrize("B,T,C,V", [(2, 256, 256, 900), (64, 256, 256, 900), (16, 1024, 512, 5), (64, 256, 256, 13),
+                                     (8, 512, 256, 144), (3, 4, 32, 3), (1, 64, 64, 200), (4, 256, 1024, 900),
+                                     (2, 96, 64, 5000)])
+def test_embedding_bwd_scratch(B, T, C, V):
+    """Token-table gradient with per-chunk partial tables (mmt_op_embedding_bwd_ws: the engine's
+    path) against torch index_add, accumulating into a non-zero dtok. (1, 64, 64, 200): the tables
+    do not fit B*T*C floats, so the atomic flush runs; (2, 96, 64, 5000): a table too large for a
+    4-float LDS slab takes direct atomics."""
+    torch.manual_seed(B + T + C + V)
+    idx = torch.randint(0, V, (B, T), device=DEV)
+    dx = torch.randn(B * T, C, device=DEV)
+    dtok0 = torch.randn(V, C, device=DEV)
+    dtok = dtok0.clone()
+    dpos = torch.zeros(T, C, device=DEV)
+    scratch = torch.full((B * T * C,), float("nan"), device=DEV)
+    L = ML.lib()
+    assert L.mmt_op_embedding_bwd_ws(_s(), B, T, C, V, ML.ptr(idx), ML.ptr(dx), ML.ptr(dtok), ML.ptr(dpos),
+                                     ML.ptr(scratch)) == 0
+    _sync()
+    ref_tok = dtok0.clone().index_add_(0, idx.view(-1), dx)
+    torch.testing.assert_close(dtok, ref_tok, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(dpos, dx.view(B, T, C).sum(0), rtol=1e-5, atol=1e-4)
+

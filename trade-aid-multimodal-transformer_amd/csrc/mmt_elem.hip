@@ -239,35 +239,50 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbBatch batch, int R, i
   reinterpret_cast<f32x4*>(P.x + (int64_t)r * C)[c4] = a + p;
 }
 
-// token-table gradient, privatised in LDS: a block owns one column slab (SLAB floats, the
-// widest power of two with V * SLAB floats <= 16 K = 64 KiB) of one modality's table and a chunk
-// of rows; it scatter-adds its rows into the LDS slab (ds_add_f32) and flushes the touched
-// entries with one global atomic each. Rows per block scale with V (>= 4 V) so the flush stays
-// small against the rows read; a vocabulary too large for a 4-float slab takes direct atomics.
-#define EMB_LDS_FLOATS 16384
+// token-table gradient, privatised in LDS: a block owns one column slab (SLAB floats, the widest
+// power of two with V * SLAB floats <= EMB_LDS_FLOATS) of one modality's table and a chunk of rows;
+// it scatter-adds its rows into the LDS slab (ds_add_f32) and flushes the slab. Two flush forms:
+//  * with a scratch buffer (EmbProblem::part, the engine's path): plain stores of the whole slab into
+//    the chunk's partial table [chunk][V][C], then embed_tok_reduce_kernel adds the partial tables
+//    into dtok. Chunks are then short (two passes of EMB_U loads per thread): the launch is bound by
+//    its row loads' latency, and at C1 / the target it ends the step after the side stream has
+//    drained (round 4: 174 us live at C1 with 64 blocks per modality of 16 dependent load rounds);
+//  * without one: one global atomic per touched entry, rows per block >= 4 V so the atomics stay few.
+// A vocabulary too large for a 4-float slab takes direct atomics.
+#define EMB_LDS_FLOATS 8192
 __host__ __device__ __forceinline__ int emb_slab(int V, int C) {
   if ((int64_t)V * C <= EMB_LDS_FLOATS) return C;
   int p = 256;  // largest power-of-two slab dividing C that fits (4 always divides C)
   while (p > 4 && (C % p != 0 || (int64_t)V * p > EMB_LDS_FLOATS)) p >>= 1;
   return p;
 }
-#ifndef EMB_CHUNK_MUL
-#define EMB_CHUNK_MUL 4
-#endif
 #ifndef EMB_U
-#define EMB_U 4
+#define EMB_U 8
 #endif
-__host__ __device__ __forceinline__ int emb_chunk(int V, int R) {
+// rows per chunk: with partial tables two load rounds per thread (as long as the [chunk][V][C]
+// tables fit the B*T*C-float scratch), else >= 4 V rows (atomic flush)
+__host__ __device__ __forceinline__ int emb_chunk(const EmbProblem& P, int R, int C) {
+  const int rpp = 256 / (emb_slab(P.V, C) >> 2);
+  if (P.part && (int64_t)P.V * emb_slab(P.V, C) <= EMB_LDS_FLOATS) {
+    int ch = rpp * EMB_U * 2;
+    while ((int64_t)((R + ch - 1) / ch) * P.V > R && ch < R) ch <<= 1;
+    if ((int64_t)((R + ch - 1) / ch) * P.V <= R) return ch;
+  }
   int ch = 256;
-  while (ch < EMB_CHUNK_MUL * V && ch < R) ch <<= 1;
+  while (ch < 4 * P.V && ch < R) ch <<= 1;
   return ch;
+}
+__host__ __device__ __forceinline__ bool emb_use_part(const EmbProblem& P, int R, int C) {
+  if (!P.part || (int64_t)P.V * emb_slab(P.V, C) > EMB_LDS_FLOATS) return false;
+  const int ch = emb_chunk(P, R, C);
+  return (int64_t)((R + ch - 1) / ch) * P.V <= R;
 }
 __global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int R, int C) {
   const EmbProblem& P = batch.p[blockIdx.z];
   const int V = P.V;
   const int slab = emb_slab(V, C);
   const int nslab = C / slab;
-  const int chunk = emb_chunk(V, R);
+  const int chunk = emb_chunk(P, R, C);
   const int nchunk = (R + chunk - 1) / chunk;
   if ((int)blockIdx.x >= nslab * nchunk) return;
   const int sl = blockIdx.x % nslab, ck = blockIdx.x / nslab;
@@ -312,9 +327,39 @@ __global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int 
   }
   if (priv) {
     __syncthreads();
-    for (int q = threadIdx.x; q < V * slab; q += 256)
-      if (acc[q] != 0.f) atomicAdd(P.dtok + (int64_t)(q / slab) * C + c0 + (q % slab), acc[q]);
+    if (emb_use_part(P, R, C)) {  // the whole slab into this chunk's partial table
+      float* pt = P.part + (int64_t)ck * V * C + c0;
+      for (int q = threadIdx.x; q < V * slab; q += 256) pt[(int64_t)(q / slab) * C + (q % slab)] = acc[q];
+    } else {
+      for (int q = threadIdx.x; q < V * slab; q += 256)
+        if (acc[q] != 0.f) atomicAdd(P.dtok + (int64_t)(q / slab) * C + c0 + (q % slab), acc[q]);
+    }
   }
+}
+
+// dtok += the sum over the row chunks of the partial tables (embed_tok_bwd_kernel with P.part):
+// thread (float4 i of the table, group y of EMB_RED chunks) sums its group with all loads in flight
+// and adds it with four atomics (a thread looping over every chunk ran 256 dependent loads deep for
+// the small vocabularies: 68 us at C1)
+#define EMB_RED 16
+__global__ __launch_bounds__(256) void embed_tok_reduce_kernel(EmbBatch batch, int R, int C) {
+  const EmbProblem& P = batch.p[blockIdx.z];
+  if (!emb_use_part(P, R, C)) return;
+  const int V = P.V, C4 = C >> 2;
+  const int ch = emb_chunk(P, R, C);
+  const int nchunk = (R + ch - 1) / ch;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int k0 = blockIdx.y * EMB_RED;
+  if (i >= (int64_t)V * C4 || k0 >= nchunk) return;
+  f32x4 t[EMB_RED];
+#pragma unroll
+  for (int k = 0; k < EMB_RED; ++k)
+    t[k] = k0 + k < nchunk ? reinterpret_cast<const f32x4*>(P.part + (int64_t)(k0 + k) * V * C)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 1; k < EMB_RED; ++k) t[0] += t[k];
+  float* d = P.dtok + 4 * i;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) atomicAdd(d + e, t[0][e]);
 }
 
 // positional-table gradient, shared by all modalities: dpos[t] += sum_m sum_b dx_m[b*T + t].
@@ -362,12 +407,28 @@ hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStrea
   const int R = B * T;
   if (C % 4 || C > 1024) return hipErrorInvalidValue;
   // grid: the largest (slabs x row chunks) over the problems
-  int maxblocks = 1;
+  int maxblocks = 1, maxv = 1;
+  bool any_part = false;
   for (int g = 0; g < b.count; ++g) {
-    const int nb = (C / emb_slab(b.p[g].V, C)) * ((R + emb_chunk(b.p[g].V, R) - 1) / emb_chunk(b.p[g].V, R));
+    const int ch = emb_chunk(b.p[g], R, C);
+    const int nb = (C / emb_slab(b.p[g].V, C)) * ((R + ch - 1) / ch);
     maxblocks = nb > maxblocks ? nb : maxblocks;
+    maxv = b.p[g].V > maxv ? b.p[g].V : maxv;
+    any_part = any_part || emb_use_part(b.p[g], R, C);
   }
   hipLaunchKernelGGL(embed_tok_bwd_kernel, dim3(maxblocks, 1, b.count), dim3(256), 0, s, b, R, C);
+  if (any_part) {
+    int maxg = 1;
+    for (int g = 0; g < b.count; ++g) {
+      if (!emb_use_part(b.p[g], R, C)) continue;
+      const int ch = emb_chunk(b.p[g], R, C);
+      const int ng = ((R + ch - 1) / ch + EMB_RED - 1) / EMB_RED;
+      maxg = ng > maxg ? ng : maxg;
+    }
+    const int64_t n4 = (int64_t)maxv * (C / 4);
+    hipLaunchKernelGGL(embed_tok_reduce_kernel, dim3((unsigned)((n4 + 255) / 256), maxg, b.count), dim3(256), 0, s, b, R,
+                       C);
+  }
   // all problems of one batch must share the positional table (one model): dpos of p[0]
   for (int g = 1; g < b.count; ++g)
     if (b.p[g].dpos != b.p[0].dpos) return hipErrorInvalidValue;

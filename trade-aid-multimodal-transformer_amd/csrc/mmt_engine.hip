@@ -1796,6 +1796,7 @@ int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* los
     for (int i = 0; i < c->M; ++i) {
       eb.p[i].idx = c->last_idx[i]; eb.p[i].dx = r.W<float>(c->plan.dres[i]);
       eb.p[i].dtok = grads + c->post[i].tok; eb.p[i].dpos = grads + c->pos_off; eb.p[i].V = c->V[i];
+      eb.p[i].part = r.W<float>(c->plan.dln[i]);  // R x C fp32, free once the layers are done
     }
     r.ok(mmt_launch_embed_bwd(eb, r.B, c->T, c->C, r.s), "embed_bwd");
     return r.rc;

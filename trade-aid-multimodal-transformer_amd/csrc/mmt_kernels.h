@@ -257,8 +257,12 @@ struct EmbProblem {
   const float* pos;     // [T, C]
   float* x;             // [B*T, C]
   const float* dx;      // backward: [B*T, C]
-  float* dtok;          // atomic
+  float* dtok;          // accumulated (+=)
   float* dpos;          // atomic
+  // optional scratch of >= B*T*C floats: the token-table blocks store their LDS-privatised slabs
+  // there as per-chunk partial tables and one reduce pass adds them into dtok (short row chunks,
+  // no global atomics); nullptr: atomic flush
+  float* part;
   int V;
 };
 struct EmbBatch { EmbProblem p[MMT_MAX_GROUP]; int count; };

@@ -188,6 +188,14 @@ int mmt_op_embedding_bwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t 
   return st(mmt_launch_embed_bwd(b, B, T, C, (hipStream_t)stream));
 }
 
+int mmt_op_embedding_bwd_ws(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx,
+                            const float* dx, float* dtok, float* dpos, float* scratch) {
+  EmbBatch b{};
+  b.count = 1;
+  b.p[0].idx = idx; b.p[0].dx = dx; b.p[0].dtok = dtok; b.p[0].dpos = dpos; b.p[0].V = V; b.p[0].part = scratch;
+  return st(mmt_launch_embed_bwd(b, B, T, C, (hipStream_t)stream));
+}
+
 }  // extern "C"
 
 // ---- MX-fp8 (C4's fp8 path) -------------------------------------------------------------------

@@ -108,6 +108,7 @@ _SIGS = {
     "mmt_op_cross_entropy": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "mmt_op_embedding_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mmt_op_embedding_bwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "mmt_op_embedding_bwd_ws": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mmt_op_mx_quant": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32]),
     "mmt_op_gemm_f8": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32,
                                c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32]),
@@ -130,6 +131,8 @@ def lib():
             f"`python trade-aid-multimodal-transformer_amd/mmt_build.py` (there is no CPU fallback)")
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
+        if os.environ.get("MMT_LIB_PATH") and not hasattr(L, name):
+            continue  # an older experimental build (A/B base) lacks an entry point added since
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
