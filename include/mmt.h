@@ -186,7 +186,7 @@ int mmt_exact_walk(void* stream, int32_t nmod, int32_t* const* data, const int64
                    const int32_t* vocab, uint32_t* mt_state, const uint32_t* words, int64_t nwords, void* scratch,
                    int64_t scratch_bytes, int32_t* status);
 /* tuning knob: bit 0 / bit 1 = the slice-streamed hs-64 attention dK/dV / dQ pass, bit 2 = dK/dV at 3 waves
- * per SIMD (default 7); returns the old value */
+ * per SIMD, bit 3 = the slice-streamed hs-64 forward (default 15); returns the old value */
 int mmt_attn_set_ring(int v);
 
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
