@@ -1306,9 +1306,6 @@ static int g_big_variant = [] {
 #ifndef MMT_DEF_VARIANT
 #define MMT_DEF_VARIANT 0
 #endif
-#ifndef MMT_QKV2_MINB2
-#define MMT_QKV2_MINB2 0
-#endif
 template <bool A_KC, bool B_KC, bool SWAP, int EPI>
 static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t s) {
   if (b.count == 0) return hipSuccess;
@@ -1357,15 +1354,6 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
   const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw
                   : (!A_KC && !B_KC && env_dw >= 0) ? env_dw
                   : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? (g_pipe ? 8 : MMT_OCC3_VARIANT) : (g_pipe ? 7 : MMT_DEF_VARIANT));
-#if MMT_QKV2_MINB2
-  // build-time experiment: the fused Q/K/V stage 2 (5 VGPR spills at 3 blocks per CU) at 2 blocks per CU
-  if constexpr (EPI == EPI_BIAS_TANH_BF16 && SWAP) {
-    if (g_gemm_variant < 0 && b.p[0].qkv2_out) {
-      launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI, 2>(b, grid, s);
-      return hipGetLastError();
-    }
-  }
-#endif
   switch (var) {
     case 1: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 2: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
