@@ -5,7 +5,7 @@
 # usage: bash tools/prof_post.sh <tag>
 T=${1:?tag}
 cd $GRAFT_REPO_ROOT
-for d in gpurun_out/${T}_prof_*/; do
+for d in gpurun_out/${T}_prof_*/ gpurun_out/${T}_prof/; do
   [ -d "$d" ] || continue
   db=$(ls "$d"*.db 2>/dev/null | head -1)
   [ -n "$db" ] || continue
