@@ -579,25 +579,42 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackSeg* __restrict__ s
   const int row0 = task_seg[2 * blockIdx.x + 1];
   const PackSeg S = segs[seg];
   const int chunks = S.dld / 8;
-  for (int q = threadIdx.x; q < 32 * chunks; q += 256) {
-    const int r = row0 + q / chunks;
-    const int c = (q % chunks) * 8;
-    if (r >= S.rows) break;
-    const float* s = src + S.src_off + (int64_t)r * S.cols;
-    uint32_t w[4];
-    if (c + 8 <= S.cols && ((S.cols | S.src_off) & 3) == 0) {  // interior chunk: two 16-B loads
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(s + c), hi = *reinterpret_cast<const f32x4*>(s + c + 4);
-      w[0] = pack2bf(lo[0], lo[1]); w[1] = pack2bf(lo[2], lo[3]);
-      w[2] = pack2bf(hi[0], hi[1]); w[3] = pack2bf(hi[2], hi[3]);
-    } else {
+  const int n = 32 * chunks;
+  const bool vec = ((S.cols | S.src_off) & 3) == 0;
+  // up to PK chunks per thread with every load issued before the first store (the one-chunk-at-a-time
+  // loop ran the launch at half the HBM rate: 124 us for 540 MB at the target shape)
+  constexpr int PK = 8;
+  for (int q0 = threadIdx.x; q0 < n; q0 += 256 * PK) {
+    f32x4 lo[PK], hi[PK];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a = (c + 2 * e < S.cols) ? s[c + 2 * e] : 0.f;
-        const float b = (c + 2 * e + 1 < S.cols) ? s[c + 2 * e + 1] : 0.f;
-        w[e] = pack2bf(a, b);
+    for (int k = 0; k < PK; ++k) {
+      const int q = q0 + 256 * k;
+      const int r = row0 + q / chunks, c = (q % chunks) * 8;
+      lo[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      hi[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (q < n && r < S.rows) {
+        const float* sp = src + S.src_off + (int64_t)r * S.cols;
+        if (vec && c + 8 <= S.cols) {  // interior chunk: two 16-B loads
+          lo[k] = *reinterpret_cast<const f32x4*>(sp + c);
+          hi[k] = *reinterpret_cast<const f32x4*>(sp + c + 4);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            lo[k][e] = (c + e < S.cols) ? sp[c + e] : 0.f;
+            hi[k][e] = (c + 4 + e < S.cols) ? sp[c + 4 + e] : 0.f;
+          }
+        }
       }
     }
-    *reinterpret_cast<u32x4*>(dst + S.dst_off + (int64_t)r * S.dld + c) = u32x4{w[0], w[1], w[2], w[3]};
+#pragma unroll
+    for (int k = 0; k < PK; ++k) {
+      const int q = q0 + 256 * k;
+      const int r = row0 + q / chunks, c = (q % chunks) * 8;
+      if (q < n && r < S.rows)
+        *reinterpret_cast<u32x4*>(dst + S.dst_off + (int64_t)r * S.dld + c) =
+            u32x4{pack2bf(lo[k][0], lo[k][1]), pack2bf(lo[k][2], lo[k][3]), pack2bf(hi[k][0], hi[k][1]),
+                  pack2bf(hi[k][2], hi[k][3])};
+    }
   }
 }
 
