@@ -118,13 +118,12 @@ def test_gemm_backward_data(M, N, K, epi):
         assert rel(o32, base + ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [0x500 | 0x10000, 0x300 | 0x10000, 8, 7])
+@pytest.mark.parametrize("variant", [0x100 | 0x10000, 0x200 | 0x10000, 0x10000, 5, 2, 4])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 512), (300, 264, 520), (768, 520, 136), (256, 1024, 64)])
-def test_gemm_pipelined_and_persistent(variant, M, N, K):
-    """The software-pipelined K-step (128 x 128 variants 7 / 8, 256 x 256 variant 3) and the
-    persistent 256 x 256 kernel (variant 5: one block per CU walks the tiles, the last K-step
-    prefetches the next tile's first stage) on the forward and backward-data epilogues, the 256 x 256
-    tile forced at every K (bit 16), ragged edges and several tiles per block included."""
+def test_gemm_pipeline_variants(variant, M, N, K):
+    """The 256 x 256 tile's rings (BK 32 x 4, BK 32 x 3, BK 64 x 2: bits 8-11, forced at every K by bit
+    16) and the deeper 128 x 128 rings (variants 5 / 2 / 4) on the forward and backward-data epilogues,
+    ragged edges included (the rings' vmcnt counts depend on the stages left in flight)."""
     L = ML.lib()
     assert L.mmt_gemm_set_variant(variant) == 0
     try:

@@ -58,7 +58,7 @@ extern "C" int mmt_gemm_set_variant(int v) {
     g_gemm_variant = -1; g_gemm_variant_dw = 0; g_gemm_big_variant_rt = 0; g_force_big_rt = 0;
     return 0;
   }
-  if ((v & 15) > 8 || ((v >> 4) & 15) > 8) return -1;
+  if ((v & 15) > 6 || ((v >> 4) & 15) > 6 || ((v >> 8) & 15) > 2) return -1;
   g_gemm_variant = v & 15;
   g_gemm_variant_dw = (v >> 4) & 15;
   g_gemm_big_variant_rt = (v >> 8) & 15;
@@ -149,41 +149,6 @@ __device__ __forceinline__ void issue_tile(const i32x4& rsrc, char* img, int ld,
     }
     dma16(rsrc, __builtin_amdgcn_readfirstlane(lds_u32(img + i * 1024)), voff);
   }
-}
-
-// per-piece source geometry, computed once per tile: the byte offset of the piece's row (K-contiguous
-// operand) or column (MN-contiguous) -- negative when that row / column is past the operand -- and
-// its K offset within a K-step. issue_pre then costs ~4 VALU per piece instead of ~12.
-struct PieceSrc {
-  int base, kk;
-};
-template <int BK, bool KC, int ROWS, int NW>
-__device__ __forceinline__ PieceSrc piece_src(int ld, int rows_total, int r0, int wave, int lane, int u) {
-  constexpr int PPW = ROWS * BK / 512 / NW;
-  constexpr int CPR = BK / 8;
-  constexpr int CPK = ROWS / 8;
-  const int i = wave * PPW + u;
-  PieceSrc p;
-  if (KC) {
-    const int row = (64 / CPR) * i + lane / CPR;
-    const int chunk = kc_swz<BK>(lane % CPR, row);
-    p.base = r0 + row < rows_total ? (r0 + row) * ld * 2 : -1;
-    p.kk = chunk * 8;
-  } else {
-    const int kr = (64 / CPK) * i + lane / CPK;
-    const int chunk = (lane % CPK) ^ ((kr & 3) << 2);
-    p.base = r0 + chunk * 8 < rows_total ? (r0 + chunk * 8) * 2 : -1;
-    p.kk = kr;
-  }
-  return p;
-}
-template <int BK, bool KC, int ROWS, int NW>
-__device__ __forceinline__ void issue_pre(const i32x4& rsrc, char* img, const PieceSrc& ps, int ld, int K, int k0,
-                                          int wave, int u) {
-  constexpr int PPW = ROWS * BK / 512 / NW;
-  const int gk = k0 + ps.kk;
-  const int voff = (ps.base >= 0 && gk < K) ? ps.base + (KC ? gk * 2 : gk * ld * 2) : 0x7fffffff;
-  dma16(rsrc, __builtin_amdgcn_readfirstlane(lds_u32(img + (wave * PPW + u) * 1024)), voff);
 }
 
 // fragment for "lane row = sb + (lane&31), k = 16*s + 8*(lane>>5) + j" from a staged image
@@ -707,10 +672,7 @@ __device__ __forceinline__ void qkv2_fused(const GemmProblem& P, f32x16 (&acc)[T
 
 // MINB > 1 (128x128 tile only): a launch-bounds hint of MINB blocks per CU, with the epilogue staged in
 // 64-row passes so the LDS footprint leaves room for them (variants 5 and 6)
-// PIPE = 1: software-pipelined K-step (the fragments of sub-step s + 1 read while sub-step s's MFMAs
-// issue, and the next stage's LDS-DMA pieces issued one at a time between MFMAs instead of as a burst
-// ahead of them: a piece's issue costs a wave ~60-100 cycles, MI355X_MICROARCH.md)
-template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1, int PIPE = 0>
+template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1>
 __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, NT = TL::NT, TM = TL::TM, TN = TL::TN;
   constexpr int IMG_A = GBM * BK * 2, IMG_B = GBN * BK * 2;  // per operand per stage (both layouts)
@@ -839,61 +801,6 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
           }
       }
     };
-    PieceSrc psrc[PIPE == 1 ? PIECES : 1];
-    if constexpr (PIPE == 1) {
-      constexpr int PA = GBM * BK / 512 / NW;
-#pragma unroll
-      for (int u = 0; u < PIECES; ++u)
-        psrc[u] = u < PA ? piece_src<BK, A_KC, GBM, NW>(P.lda, M, m0, wave, lane, u)
-                         : piece_src<BK, B_KC, GBN, NW>(P.ldb, N, n0, wave, lane, u - PA);
-    }
-    // PIPE 1: one K-step with the fragment reads one sub-step ahead (two fragment register sets) and
-    // the prefetch pieces spread over the first half of the step's MFMAs (the second half covers their
-    // landing before the next step's wait)
-    auto step_p = [&](int tt, auto UC) {
-      constexpr int U = decltype(UC)::value;
-      constexpr int NS = BK / 16, NMF = NS * AI * AJ;
-      constexpr int PA = GBM * BK / 512 / NW;  // this wave's A pieces; then PIECES - PA B pieces
-      static_assert(PA <= PIECES, "pieces");
-      wait_vm(PIECES * min(ST - 2, nk - 1 - tt));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (tt == 0) GEMM_STAMP(2);
-      const bool pre = tt + ST - 1 < nk;
-      char* stn = lds + ((U + ST - 1) % ST) * STAGE_BYTES;
-      const int k0n = (ks0 + tt + ST - 1) * BK;
-      const char* imgA = lds + U * STAGE_BYTES;
-      const char* imgB = imgA + IMG_A;
-      bf16x8 fa[2][TM], fb[2][TN];
-#pragma unroll
-      for (int j = 0; j < TM; ++j) fa[0][j] = frag<BK, A_KC, GBM>(imgA, wm * TM * 32 + 32 * j, 0, lane);
-#pragma unroll
-      for (int i = 0; i < TN; ++i) fb[0][i] = frag<BK, B_KC, GBN>(imgB, wn * TN * 32 + 32 * i, 0, lane);
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const int c = s & 1;
-        if (s + 1 < NS) {
-#pragma unroll
-          for (int j = 0; j < TM; ++j) fa[c ^ 1][j] = frag<BK, A_KC, GBM>(imgA, wm * TM * 32 + 32 * j, s + 1, lane);
-#pragma unroll
-          for (int i = 0; i < TN; ++i) fb[c ^ 1][i] = frag<BK, B_KC, GBN>(imgB, wn * TN * 32 + 32 * i, s + 1, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < AI; ++i)
-#pragma unroll
-          for (int j = 0; j < AJ; ++j) {
-            if (SWAP) acc[i][j] = mfma32(fb[c][i], fa[c][j], acc[i][j]);
-            else acc[i][j] = mfma32(fa[c][i], fb[c][j], acc[i][j]);
-            const int q = (s * AI + i) * AJ + j;  // MFMA index within the step
-#pragma unroll
-            for (int u = 0; u < PIECES; ++u)
-              if (q == (u * NMF) / (2 * PIECES) && pre) {  // first half of the step: time to land
-                if (u < PA) issue_pre<BK, A_KC, GBM, NW>(ra, stn, psrc[u], P.lda, K, k0n, wave, u);
-                else issue_pre<BK, B_KC, GBN, NW>(rb, stn + IMG_A, psrc[u], P.ldb, K, k0n, wave, u - PA);
-              }
-          }
-      }
-    };
 #pragma unroll
     for (int t = 0; t < ST - 1; ++t)
       if (t < nk) {
@@ -903,27 +810,15 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
       }
     GEMM_STAMP(1);
     int t = 0;
-    if constexpr (PIPE == 1) {
-      for (; t + ST <= nk; t += ST) {
-        step_p(t, std::integral_constant<int, 0>{});
-        step_p(t + 1, std::integral_constant<int, 1>{});
-        if constexpr (ST > 2) step_p(t + 2, std::integral_constant<int, (ST > 2 ? 2 : 0)>{});
-        if constexpr (ST > 3) step_p(t + 3, std::integral_constant<int, (ST > 3 ? 3 : 0)>{});
-      }
-      if (t < nk) step_p(t, std::integral_constant<int, 0>{});
-      if (ST > 2 && t + 1 < nk) step_p(t + 1, std::integral_constant<int, 1>{});
-      if constexpr (ST > 3) { if (t + 2 < nk) step_p(t + 2, std::integral_constant<int, (ST > 3 ? 2 : 0)>{}); }
-    } else {
-      for (; t + ST <= nk; t += ST) {
-        step(t, std::integral_constant<int, 0>{});
-        step(t + 1, std::integral_constant<int, 1>{});
-        if constexpr (ST > 2) step(t + 2, std::integral_constant<int, (ST > 2 ? 2 : 0)>{});
-        if constexpr (ST > 3) step(t + 3, std::integral_constant<int, (ST > 3 ? 3 : 0)>{});
-      }
-      if (t < nk) step(t, std::integral_constant<int, 0>{});
-      if (ST > 2 && t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
-      if constexpr (ST > 3) { if (t + 2 < nk) step(t + 2, std::integral_constant<int, (ST > 3 ? 2 : 0)>{}); }
+    for (; t + ST <= nk; t += ST) {
+      step(t, std::integral_constant<int, 0>{});
+      step(t + 1, std::integral_constant<int, 1>{});
+      if constexpr (ST > 2) step(t + 2, std::integral_constant<int, (ST > 2 ? 2 : 0)>{});
+      if constexpr (ST > 3) step(t + 3, std::integral_constant<int, (ST > 3 ? 3 : 0)>{});
     }
+    if (t < nk) step(t, std::integral_constant<int, 0>{});
+    if (ST > 2 && t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
+    if constexpr (ST > 3) { if (t + 2 < nk) step(t + 2, std::integral_constant<int, (ST > 3 ? 2 : 0)>{}); }
   }
 
   GEMM_STAMP(3);
@@ -1096,149 +991,14 @@ __global__ __launch_bounds__(TL::NT) void gemm_f8_kernel(GemmBatch batch) {
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Persistent 256 x 256 GEMM (big variant 5; forward / backward-data, one K pass): one block per CU
-// walks the tiles of every problem of the batch. The LAST K-step of a tile issues the NEXT tile's
-// first stage into the other LDS slot (interleaved with its MFMAs like every prefetch), so that
-// stage's latency hides behind the last MFMAs and the epilogue instead of stalling every tile's
-// start; the epilogue stages through the slot the last K-step read (slots padded to the 64-row fp32
-// staging tile: 2 x 66.5 KB). K-steps as the PIPE 1 kernel (fragments one sub-step ahead, pieces
-// spread over the first half of the step's MFMAs). Tiles are dealt XCD-major per round.
-// ---------------------------------------------------------------------------------------------
-template <class TL, bool A_KC, bool B_KC, int EPI>
-__global__ __launch_bounds__(TL::NT, 1) void gemm_persist_kernel(GemmBatch batch, int total_tiles) {
-  constexpr int BK = 64;
-  constexpr int GBM = TL::BM, GBN = TL::BN, NW = TL::NW, TM = TL::TM, TN = TL::TN;
-  constexpr int IMG_A = GBM * BK * 2, IMG_B = GBN * BK * 2, STAGE_BYTES = IMG_A + IMG_B;
-  constexpr int PIECES = (GBM + GBN) * BK / 512 / NW, PA = GBM * BK / 512 / NW;
-  constexpr int EPI_ROWS = 64, CTILE = EPI_ROWS * (GBN + 4) * 4;
-  constexpr int SLOT = STAGE_BYTES > CTILE ? STAGE_BYTES : CTILE;
-  constexpr int AI = TN, AJ = TM;  // SWAP layout
-  constexpr int NS = BK / 16, NMF = NS * AI * AJ;
-  __shared__ __attribute__((aligned(1024))) char lds[2 * SLOT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / TL::WN, wn = wave % TL::WN;
-  const int G = gridDim.x;
-  const int lin = (G % 8 == 0) ? (blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
-  // tile lt of the concatenated problems -> (problem, m0, n0); prob = -1 past the end
-  auto describe = [&](int lt, int& prob, int& m0, int& n0) {
-    prob = -1;
-    if (lt >= total_tiles) return;
-    int rem = lt;
-    for (int g = 0; g < batch.count; ++g) {
-      const int tn = (batch.p[g].N + GBN - 1) / GBN, nt = tn * ((batch.p[g].M + GBM - 1) / GBM);
-      if (rem < nt) { prob = g; m0 = (rem / tn) * GBM; n0 = (rem % tn) * GBN; return; }
-      rem -= nt;
-    }
-  };
-  int it = 0, prob, m0, n0;
-  describe(lin, prob, m0, n0);
-  if (prob < 0) return;
-  // the piece sources / buffer descriptors of the tile whose stages the next DMA pieces fetch
-  PieceSrc ps[PIECES];
-  i32x4 ra, rb;
-  auto setup = [&](int pr, int mm, int nn) {
-    const GemmProblem& Q = batch.p[pr];
-    ra = make_rsrc(Q.A, (int64_t)(A_KC ? Q.M : Q.K) * Q.lda * 2);
-    rb = make_rsrc(Q.B, (int64_t)(B_KC ? Q.N : Q.K) * Q.ldb * 2);
-#pragma unroll
-    for (int u = 0; u < PIECES; ++u)
-      ps[u] = u < PA ? piece_src<BK, A_KC, GBM, NW>(Q.lda, Q.M, mm, wave, lane, u)
-                     : piece_src<BK, B_KC, GBN, NW>(Q.ldb, Q.N, nn, wave, lane, u - PA);
-  };
-  setup(prob, m0, n0);
-  {
-    const GemmProblem& Q = batch.p[prob];
-#pragma unroll
-    for (int u = 0; u < PIECES; ++u) {
-      if (u < PA) issue_pre<BK, A_KC, GBM, NW>(ra, lds, ps[u], Q.lda, Q.K, 0, wave, u);
-      else issue_pre<BK, B_KC, GBN, NW>(rb, lds + IMG_A, ps[u], Q.ldb, Q.K, 0, wave, u - PA);
-    }
-  }
-  int slot = 0;  // LDS slot of the stage the next K-step reads
-  f32x16 acc[AI][AJ];
-  for (;;) {
-    const GemmProblem& P = batch.p[prob];
-    const int K = P.K, nk = (K + BK - 1) / BK;
-    int nprob, nm0, nn0;
-    describe((it + 1) * G + lin, nprob, nm0, nn0);
-#pragma unroll
-    for (int i = 0; i < AI; ++i)
-#pragma unroll
-      for (int j = 0; j < AJ; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-#pragma unroll 1
-    for (int tt = 0; tt < nk; ++tt) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this stage (and the last epilogue's stores)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's pieces landed; the other slot's reads are done
-      const bool last = tt + 1 == nk;
-      if (last && nprob >= 0) setup(nprob, nm0, nn0);  // the pieces below fetch the next tile's stage 0
-      const bool pre = !last || nprob >= 0;
-      const int k0n = last ? 0 : (tt + 1) * BK;
-      const int lda_n = last ? batch.p[nprob < 0 ? prob : nprob].lda : P.lda;
-      const int ldb_n = last ? batch.p[nprob < 0 ? prob : nprob].ldb : P.ldb;
-      const int K_n = last ? batch.p[nprob < 0 ? prob : nprob].K : K;
-      const char* imgA = lds + slot * SLOT;
-      const char* imgB = imgA + IMG_A;
-      char* stn = lds + (slot ^ 1) * SLOT;
-      bf16x8 fa[2][TM], fb[2][TN];
-#pragma unroll
-      for (int j = 0; j < TM; ++j) fa[0][j] = frag<BK, A_KC, GBM>(imgA, wm * TM * 32 + 32 * j, 0, lane);
-#pragma unroll
-      for (int i = 0; i < TN; ++i) fb[0][i] = frag<BK, B_KC, GBN>(imgB, wn * TN * 32 + 32 * i, 0, lane);
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const int c = s & 1;
-        if (s + 1 < NS) {
-#pragma unroll
-          for (int j = 0; j < TM; ++j) fa[c ^ 1][j] = frag<BK, A_KC, GBM>(imgA, wm * TM * 32 + 32 * j, s + 1, lane);
-#pragma unroll
-          for (int i = 0; i < TN; ++i) fb[c ^ 1][i] = frag<BK, B_KC, GBN>(imgB, wn * TN * 32 + 32 * i, s + 1, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < AI; ++i)
-#pragma unroll
-          for (int j = 0; j < AJ; ++j) {
-            acc[i][j] = mfma32(fb[c][i], fa[c][j], acc[i][j]);
-            const int q = (s * AI + i) * AJ + j;
-#pragma unroll
-            for (int u = 0; u < PIECES; ++u)
-              if (q == (u * NMF) / (2 * PIECES) && pre) {
-                if (u < PA) issue_pre<BK, A_KC, GBM, NW>(ra, stn, ps[u], lda_n, K_n, k0n, wave, u);
-                else issue_pre<BK, B_KC, GBN, NW>(rb, stn + IMG_A, ps[u], ldb_n, K_n, k0n, wave, u - PA);
-              }
-          }
-      }
-      slot ^= 1;
-    }
-    float alpha = P.alpha;
-    if (P.alpha_ptr) alpha *= *P.alpha_ptr;
-    // the last stage's slot (the other one holds the next tile's stage 0 in flight)
-    epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds + (slot ^ 1) * SLOT, P.o32, alpha, m0, n0, tid, lane, wave);
-    if (nprob < 0) break;
-    prob = nprob; m0 = nm0; n0 = nn0; ++it;
-  }
-}
-
-static int cu_count() {
-  static int n[16] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
-  if (!n[dev] && hipDeviceGetAttribute(&n[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n[dev] = 256;
-  return n[dev];
-}
-
-template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1, int PIPE = 0>
+template <class TL, int BK, int ST, bool A_KC, bool B_KC, bool SWAP, int EPI, int MINB = 1>
 static void launch_v(const GemmBatch& b, dim3 grid, hipStream_t s) {
 #ifdef MMT_GEMM_STAMPS
   GemmBatch bs = b;
   bs.stamps = g_stamps;
-  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI, MINB, PIPE>), grid, dim3(TL::NT), 0, s, bs);
+  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI, MINB>), grid, dim3(TL::NT), 0, s, bs);
 #else
-  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI, MINB, PIPE>), grid, dim3(TL::NT), 0, s, b);
+  hipLaunchKernelGGL((gemm_kernel<TL, BK, ST, A_KC, B_KC, SWAP, EPI, MINB>), grid, dim3(TL::NT), 0, s, b);
 #endif
 }
 
@@ -1280,20 +1040,20 @@ static int auto_splits(const GemmBatch& b, int splits) {
   return std::max(1, std::min(s, maxs));
 }
 
-// 256x256 pipeline: 0 = BK 64 x 2 stages, 1 = BK 32 x 4 (three K-steps in flight), 2 = BK 32 x 3
-// MMT_GEMM_PIPE (default 0): the software-pipelined K-step (PIPE = 1 kernels) in the default policy:
-// 256 x 256 variant 3, 128 x 128 variants 8 (3 blocks / CU epilogues) and 7 (the others). Standalone
-// (tools/gemm_bench.py, round 4) it is faster: one 256 x 256 block per CU over K = 16384 100 -> 116
-// TF/s, 4096^3 1136 -> 1180, C4 ffn0 889 -> 915 TF/s, C1 qkv1 39.2 -> 32.0 us, ffn2 dX 98.9 -> 93.3;
-// inside the training step it is slower (same box, two pairs: C1 8.78 -> 8.88 ms/step, target
-// 20.47 -> 20.98: the live weight-gradient and ffn2 dX launches 2-4 % longer), so off by default.
-static const int g_pipe = [] {
-  const char* e = getenv("MMT_GEMM_PIPE");
-  return e ? atoi(e) : 0;
-}();
+// 256x256 pipeline (MMT_GEMM_BIG_VARIANT): 0 = BK 64 x 2 stages, 1 = BK 32 x 4 (three K-steps in
+// flight), 2 = BK 32 x 3. Round 4 also built a software-pipelined K-step (the next sub-step's fragments
+// read while this one's MFMAs issue, the prefetch pieces spread between MFMAs) and a persistent
+// 256 x 256 kernel that prefetches the next tile's first stage under the last K-step and the epilogue.
+// Both won standalone (tools/gemm_bench.py: 4096^3 1136 -> 1180 TF/s, C4 ffn0 889 -> 915) and lost in
+// the training step beside the side stream (C1 8.78 -> 8.88 ms/step, target 20.47 -> 20.98), so they
+// were removed at the end of round 4.
+// Default: BK 32 x 4 for the weight gradients (both operands MN-contiguous, K = B*T: 128+ K-steps, the
+// deeper ring keeps three in flight; C1 *_dw family 3.44 -> 3.20 ms/step live, C3 73.8 -> 69.4),
+// BK 64 x 2 for the rest (the forward / data-gradient 256 x 256 launches measured 0.3-0.9 % slower
+// at BK 32 x 4 in C3 / C4: profiles/r4z_big_variant_ab.txt). MMT_GEMM_BIG_VARIANT sets all of them.
 static int g_big_variant = [] {
   const char* e = getenv("MMT_GEMM_BIG_VARIANT");
-  return e ? atoi(e) : (g_pipe ? 3 : 0);
+  return e ? atoi(e) : -1;
 }();
 
 // default 128 x 128 pipelines (build-time, tools/build_variant.py A/B): bf16-output epilogues at 3
@@ -1313,25 +1073,13 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
     dim3 grid(mt, EPI == EPI_ATOMIC_F32 ? auto_splits<TileL>(b, splits) : std::max(1, splits), b.count);
-    switch (g_gemm_big_variant_rt ? g_gemm_big_variant_rt : g_big_variant) {
+    const int bv = g_gemm_big_variant_rt ? g_gemm_big_variant_rt
+                   : g_big_variant >= 0  ? g_big_variant
+                   : (!A_KC && !B_KC)    ? 1
+                                         : 0;
+    switch (bv) {
       case 1: launch_v<TileL, 32, 4, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
       case 2: launch_v<TileL, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
-      case 3: launch_v<TileL, 64, 2, A_KC, B_KC, SWAP, EPI, 1, 1>(b, grid, s); break;
-      case 4: launch_v<TileL, 32, 4, A_KC, B_KC, SWAP, EPI, 1, 1>(b, grid, s); break;
-      case 5: {  // persistent (one K pass, K > 0); else the PIPE 1 kernel
-        int total = 0, kmin = 1 << 30;
-        max_tiles<TileL>(b, &total);
-        for (int g = 0; g < b.count; ++g) kmin = std::min(kmin, b.p[g].K);
-        if constexpr (SWAP && EPI != EPI_ATOMIC_F32 && EPI != EPI_BIAS_RESID_F32) {  // (resid: 25 spills)
-          if (grid.y == 1 && kmin > 0) {
-            hipLaunchKernelGGL((gemm_persist_kernel<TileL, A_KC, B_KC, EPI>), dim3(std::min(total, cu_count())),
-                               dim3(TileL::NT), 0, s, b, total);
-            break;
-          }
-        }
-        launch_v<TileL, 64, 2, A_KC, B_KC, SWAP, EPI, 1, 1>(b, grid, s);
-        break;
-      }
       default: launch_v<TileL, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     }
     return hipGetLastError();
@@ -1353,7 +1101,7 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
   // the step beside the side stream, 20.21 -> 20.37 ms: profiles/r3y_tilem_ab.txt; removed in round 4)
   const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw
                   : (!A_KC && !B_KC && env_dw >= 0) ? env_dw
-                  : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? (g_pipe ? 8 : MMT_OCC3_VARIANT) : (g_pipe ? 7 : MMT_DEF_VARIANT));
+                  : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? MMT_OCC3_VARIANT : MMT_DEF_VARIANT);
   switch (var) {
     case 1: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 2: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
@@ -1361,8 +1109,6 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     case 4: launch_v<TileS, 64, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     case 5: launch_v<TileS, 32, 3, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
     case 6: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI, 3>(b, grid, s); break;
-    case 7: launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI, 1, 1>(b, grid, s); break;
-    case 8: launch_v<TileS, 32, 2, A_KC, B_KC, SWAP, EPI, 3, 1>(b, grid, s); break;
     default: launch_v<TileS, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
   }
   return hipGetLastError();
@@ -1584,13 +1330,11 @@ hipError_t mmt_launch_gemm_resid_ln(const GemmBatch& b, hipStream_t s) {
   if (b.p[0].N == TileW::BN) {
     const int mt = max_tiles<TileW>(b, nullptr);
     if (mt == 0) return hipSuccess;
-    if (g_pipe) launch_v<TileW, 32, 2, true, true, true, EPI_BIAS_RESID_F32, 1, 1>(b, dim3(mt, 1, b.count), s);
-    else launch_v<TileW, 32, MMT_GEMM_W_ST, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
+    launch_v<TileW, 32, MMT_GEMM_W_ST, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
   } else {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
-    if (g_pipe) launch_v<TileL, 64, 2, true, true, true, EPI_BIAS_RESID_F32, 1, 1>(b, dim3(mt, 1, b.count), s);
-    else launch_v<TileL, 64, 2, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
+    launch_v<TileL, 64, 2, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
   }
   return hipGetLastError();
 }
@@ -1616,13 +1360,11 @@ hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
   if (b.p[0].N == TileW::BN) {
     const int mt = max_tiles<TileW>(b, nullptr);
     if (mt == 0) return hipSuccess;
-    if (g_pipe) launch_v<TileW, 32, 2, true, false, true, EPI_LN_BWD_F32, 1, 1>(b, dim3(mt, 1, b.count), s);
-    else launch_v<TileW, 32, MMT_GEMM_W_ST, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+    launch_v<TileW, 32, MMT_GEMM_W_ST, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
   } else {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
-    if (g_pipe) launch_v<TileL, 64, 2, true, false, true, EPI_LN_BWD_F32, 1, 1>(b, dim3(mt, 1, b.count), s);
-    else launch_v<TileL, 64, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
+    launch_v<TileL, 64, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
   }
   return hipGetLastError();
 }
