@@ -8,9 +8,9 @@ for c in c1 target c3 c4; do
   case $c in c1) t="";; target) t="_t";; *) t="_$c";; esac
   F=$(ls gpurun_out/${T}_pmc_fetch$t/*counter_collection.csv*) || exit 1
   W=$(ls gpurun_out/${T}_pmc_write$t/*counter_collection.csv*) || exit 1
-  if [ $c = c4 ]; then FF="ffn0=gemm_f8_kernel<TileCfg<2, 4, 4, 2>, 2>"; else FF="ffn0=true, true, true, 2, 3, 0>"; fi
+  if [ $c = c4 ]; then FF="ffn0=gemm_f8_kernel<TileCfg<2, 4, 4, 2>, 2>"; else FF="ffn0=true, true, true, 2, 3>"; fi
   args=("$FF" "*_dw=false, false, true,+slab_reduce" "attn_fwd=attn_fwd@0/2" "ca_attn_fwd=attn_fwd@1/2"
-        "attn_bwd=attn_bwd_dq+attn_bwd_dkdv@1/2" "ca_attn_bwd=attn_bwd_dq+attn_bwd_dkdv@0/2" "ffn2_dx=, 6, 1, 0>")
-  [ $c != c4 ] && args+=("ln_bwd_fused=, 9, 1, 0>")
+        "attn_bwd=attn_bwd_dq+attn_bwd_dkdv@1/2" "ca_attn_bwd=attn_bwd_dq+attn_bwd_dkdv@0/2" "ffn2_dx=, 6, 1>")
+  [ $c != c4 ] && args+=("ln_bwd_fused=, 9, 1>")
   python3 tools/pmc_traffic.py $c $F $W "${args[@]}" || exit 1
 done
