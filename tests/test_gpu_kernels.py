@@ -118,11 +118,13 @@ def test_gemm_backward_data(M, N, K, epi):
         assert rel(o32, base + ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [0x100 | 0x10000, 0x200 | 0x10000, 0x10000, 5, 2, 4])
-@pytest.mark.parametrize("M,N,K", [(512, 256, 512), (300, 264, 520), (768, 520, 136), (256, 1024, 64)])
+@pytest.mark.parametrize("variant", [0x100 | 0x10000, 0x200 | 0x10000, 0x10000, 5, 2, 4, 0x20000 | 0x10000])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 512), (300, 264, 520), (768, 520, 136), (256, 1024, 64),
+                                   (520, 776, 1000), (256, 256, 32)])
 def test_gemm_pipeline_variants(variant, M, N, K):
     """The 256 x 256 tile's rings (BK 32 x 4, BK 32 x 3, BK 64 x 2: bits 8-11, forced at every K by bit
-    16) and the deeper 128 x 128 rings (variants 5 / 2 / 4) on the forward and backward-data epilogues,
+    16), the ping-pong 256 x 256 kernel (gemm8_kernel, bit 17: K-tiles 1, 2, 3, 8, 9 and 16, ragged M / N / K)
+    and the deeper 128 x 128 rings (variants 5 / 2 / 4) on the forward and backward-data epilogues,
     ragged edges included (the rings' vmcnt counts depend on the stages left in flight)."""
     L = ML.lib()
     assert L.mmt_gemm_set_variant(variant) == 0
@@ -200,6 +202,77 @@ def test_gemm_identity_asymmetric_big_tile():
     assert rc == 0
     _sync()
     torch.testing.assert_close(o32, Bm[:, :n].t().contiguous())
+
+
+def test_gemm8_identity_asymmetric():
+    # transposition check through the ping-pong kernel (16x16x32 accumulator layout), both W layouts
+    n, k = 256, 512
+    L = ML.lib()
+    assert L.mmt_gemm_set_variant(0x20000 | 0x10000) == 0
+    try:
+        A = torch.zeros(n, k, device=DEV)
+        A[:, :n] = torch.eye(n, device=DEV)
+        Bm = torch.arange(n * k, device=DEV, dtype=torch.float32).view(n, k) % 17 - 8
+        o32 = torch.zeros(n, n, device=DEV)
+        Ab, Bb = bf(A), bf(Bm)
+        assert L.mmt_op_gemm(_s(), 1, 1, ML.EPI["store_f32"], 1, n, n, k, ML.ptr(Ab), k, ML.ptr(Bb), k, None,
+                             None, 0, None, 0, ML.ptr(o32), n, None, 0, 1.0) == 0
+        _sync()
+        torch.testing.assert_close(o32, Bm[:, :n].t().contiguous())
+        # backward-data form: W stored [K][N]; out = A @ W = W[:n, :]
+        Wk = bf(torch.arange(k * n, device=DEV, dtype=torch.float32).view(k, n) % 13 - 6)
+        o32.zero_()
+        assert L.mmt_op_gemm(_s(), 1, 0, ML.EPI["store_f32"], 1, n, n, k, ML.ptr(Ab), k, ML.ptr(Wk), n, None,
+                             None, 0, None, 0, ML.ptr(o32), n, None, 0, 1.0) == 0
+        _sync()
+        torch.testing.assert_close(o32, Wk.float()[:n, :])
+    finally:
+        L.mmt_gemm_set_variant(-1)
+
+
+@pytest.mark.parametrize("which", ["fwd", "dx", "dw"])
+def test_gemm_operand_beyond_2gib(which):
+    """buffer offsets are 32-bit, so a descriptor anchored at a whole operand read zeros past
+    2 GiB. The descriptors now start at the tile's first row (K-contiguous operands) or the K-step's first
+    row (MN-contiguous ones): an operand of 2.25 GiB gives the same products as torch on rows past the
+    boundary (forward, backward-data) and on the whole weight gradient."""
+    torch.manual_seed(11)
+    K = 1024
+    M = (1 << 20) + 65536  # M x K bf16 = 2.25 GiB
+    L = ML.lib()
+    if which in ("fwd", "dx"):
+        A = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+        A.uniform_(-1, 1)
+        N = 256
+        W = bf(torch.randn(N, K, device=DEV) * 0.05) if which == "fwd" else bf(torch.randn(K, N, device=DEV) * 0.05)
+        o16 = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        rc = L.mmt_op_gemm(_s(), 1, 1 if which == "fwd" else 0, ML.EPI["store_bf16"], 1, M, N, K, ML.ptr(A), K,
+                           ML.ptr(W), K if which == "fwd" else N, None, None, 0, None, 0, None, 0, ML.ptr(o16), N, 1.0)
+        assert rc == 0
+        _sync()
+        Wf = W.float().t() if which == "fwd" else W.float()
+        # rows either side of the 2 GiB byte offset of A, and the last rows
+        edge = (1 << 31) // (2 * K)
+        for r0 in (0, edge - 256, edge, M - 512):
+            ref = A[r0:r0 + 512].float() @ Wf
+            assert rel(o16[r0:r0 + 512], ref) < 1e-2, r0
+    else:
+        # dW[Mw, N] = dY[R, Mw]^T X[R, N] with dY of 2.25 GiB (K = R rows, MN-contiguous operands)
+        R, Mw, N = M, K, 64
+        dY = torch.empty(R, Mw, dtype=torch.bfloat16, device=DEV)
+        dY.uniform_(-1, 1)
+        X = torch.empty(R, N, dtype=torch.bfloat16, device=DEV)
+        X.uniform_(-1, 1)
+        out = torch.zeros(Mw, N, device=DEV)
+        slab = torch.empty(256 << 20, dtype=torch.uint8, device=DEV)
+        rc = L.mmt_op_gemm_wgrad(_s(), Mw, N, R, ML.ptr(dY), Mw, ML.ptr(X), N, ML.ptr(out), N, 1.0, ML.ptr(slab),
+                                 256 << 20)
+        assert rc == 0
+        _sync()
+        ref = torch.zeros(Mw, N, device=DEV)
+        for c in range(0, R, 65536):
+            ref += dY[c:c + 65536].float().t() @ X[c:c + 65536].float()
+        assert rel(out, ref) < 1e-4
 
 
 def test_gemm_backward_data_bias_grad_big_tile():

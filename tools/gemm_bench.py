@@ -126,7 +126,7 @@ def main():
     ap.add_argument("--variants", default="-1,0,6")
     ap.add_argument("--reps", type=int, default=20)
     args = ap.parse_args()
-    for v in [int(x) for x in args.variants.split(",")]:
+    for v in [int(x, 0) for x in args.variants.split(",")]:
         res = run(v, args.reps)
         for k, (us, tf) in res.items():
             print(f"variant {v}: {k:22s} {us:8.1f} us {tf:7.1f} TF/s", flush=True)
