@@ -151,8 +151,8 @@ int mmt_probe_read_at(mmt_ctx* ctx, int32_t pattern, double* total_ms, int64_t* 
  * one step in eight, so the probe's event records stay out of the other steps. */
 int mmt_probe_enable(mmt_ctx* ctx, int32_t on);
 /* Serial mode for measurement: on = 0 runs every launch of this context on the caller's stream (no
- * side stream for the weight gradients and keep bits), on != 0 restores the default. Switch between
- * training steps only. */
+ * side stream for the weight gradients and keep bits), on != 0 restores the default. Latched: the
+ * next mmt_forward applies it (a forward and its backward always run under one setting). */
 int mmt_set_side_stream(mmt_ctx* ctx, int32_t on);
 
 /* ---- device-resident batcher: get_batch (training_utils.py:333-384) on HBM token streams ---- */

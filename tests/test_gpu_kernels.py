@@ -158,8 +158,19 @@ def test_gemm_weight_grad(M, N, R, splits):
 @pytest.mark.parametrize("M,N,R", [(1024, 256, 16384), (384, 256, 4096), (900, 450, 1000), (6, 32, 300),
                                    (128, 256, 16384), (450, 256, 3000)])
 @pytest.mark.parametrize("slab_mb", [0, 64])
-def test_gemm_wgrad_slabs(M, N, R, slab_mb):
-    # the engine's weight-gradient path: split-K fp32 slabs + reduce (or one K pass without scratch)
+@pytest.mark.parametrize("variant", [-1, 0x30000])
+def test_gemm_wgrad_slabs(M, N, R, slab_mb, variant):
+    # the engine's weight-gradient path: split-K fp32 slabs + reduce (or one K pass without scratch);
+    # variant 0x30000: the ping-pong 256 x 256 kernel (MN-contiguous operands, K slices, XCD-major grid)
+    L = ML.lib()
+    assert L.mmt_gemm_set_variant(variant) == 0
+    try:
+        _wgrad_slabs(M, N, R, slab_mb)
+    finally:
+        L.mmt_gemm_set_variant(-1)
+
+
+def _wgrad_slabs(M, N, R, slab_mb):
     torch.manual_seed(M + 2 * N + R)
     lda, ldb = r8(M), r8(N)
     dY = torch.randn(R, M, device=DEV)
@@ -595,7 +606,7 @@ def test_cross_entropy(R, V):
     assert (dl[:, V:].float() == 0).all()
 
 
-@pytest.mark.parametrize("B,T,C,V", [(4, 32, 64, 57), (2, 256, 256, 900), (3, 4, 32, 3)])
+@pytest.mark.parametrize("B,T,C,V", [(4, 32, 64, 57), (2, 256, 256, 900), (3, 4, 32, 3), (4, 256, 256, 3000), (2, 64, 64, 5000)])
 def test_embedding(B, T, C, V):
     torch.manual_seed(B + T + C + V)
     idx = torch.randint(0, V, (B, T), device=DEV)

@@ -200,11 +200,10 @@ FULL = {
 }
 
 
-@pytest.mark.parametrize("name", ["c3", "c4"])
-def test_full_size_training_property(name):
+def _train_full(name, prec, steps=20):
     import mmt_optim
     from model import MultimodalTransformer
-    M, C, H, L, T, B, cross, prec = FULL[name]
+    M, C, H, L, T, B, cross, _ = FULL[name]
     V = [900, 13, 144, 5] * (M // 4)
     config_utils._config_cache = {"n_embd": C, "n_head": H, "n_layer": L, "block_size": T, "dropout": 0.1,
                                   "device": "cuda", "batch_size": B, "eval_iters": 1, "precision": prec}
@@ -219,7 +218,7 @@ def test_full_size_training_property(name):
     tgt = [s[:, 1:].contiguous() for s in seq]
     hist = []
     m.nonfinite_loss_mask(sticky=True, clear=True)
-    for step in range(20):
+    for step in range(steps):
         _, losses = m(idx, tgt)
         opt.zero_grad(set_to_none=True)
         sum(losses).backward()
@@ -227,15 +226,43 @@ def test_full_size_training_property(name):
         hist.append(torch.stack([l.detach() for l in losses]))
     torch.cuda.synchronize()
     h = torch.stack(hist).cpu()
-    print(name, "loss first", h[0].tolist(), "last", h[-1].tolist())
-    assert torch.isfinite(h).all()
-    assert int(m.nonfinite_loss_mask(sticky=True).item()) == 0
-    assert torch.isfinite(m.flat_params).all()
-    # the total falls by > 10 % and no modality's loss rises by more than 0.5 %: the narrow output
-    # heads of the small vocabularies (Linear(C, V//2) -> tanh) move slowly at lr 3e-4, and in 20
-    # steps of the 24-layer fp8 C4 model the V = 5 stream ends anywhere between -1 % and +0.2 % of
-    # its start depending on the accumulation order of the backward kernels (round 4: 1.6068 ->
-    # 1.5940 / 1.5966 / 1.6096 with three numerically equivalent attention / Q/K/V backward
-    # variants), so "strictly below" would test rounding, not learning
+    flag = int(m.nonfinite_loss_mask(sticky=True).item())
+    finite = bool(torch.isfinite(m.flat_params).all().item())
+    del m, opt
+    torch.cuda.empty_cache()
+    return h, flag, finite
+
+
+def test_full_size_training_property_c3():
+    """C3 (bf16): finite, flag 0, and EVERY modality's loss falls (mean of the last 3 steps below the first)."""
+    h, flag, finite = _train_full("c3", "bf16")
+    print("c3 loss first", h[0].tolist(), "last", h[-1].tolist())
+    assert torch.isfinite(h).all() and flag == 0 and finite
     last = h[-3:].mean(0)
-    assert last.sum() < 0.9 * h[0].sum() and (last < 1.005 * h[0]).all(), (h[0], h[-1])
+    assert last.sum() < 0.9 * h[0].sum() and (last < h[0]).all(), (h[0], h[-1])
+
+
+def test_full_size_training_property_c4_fp8_vs_bf16():
+    """C4 with the MX-fp8 forward GEMMs against the SAME 20 steps in bf16 (same seed, init, batch and dropout
+    masks): the fp8 run must learn what the bf16 run learns, per modality.
+    Band (stated here): where the bf16 loss falls clearly (by > 2 % of its start over the 20 steps), the fp8
+    loss must fall by at least half as much; where it does not (the small-vocabulary heads whose Linear(C,
+    V//2) -> tanh bottleneck moves slowly at lr 3e-4), the two runs' changes must agree within 1 % of the
+    start -- rounding, not a failure to learn, moves them there. The totals both fall by > 10 %."""
+    h8, flag8, fin8 = _train_full("c4", "fp8")
+    h16, flag16, fin16 = _train_full("c4", "bf16")
+    d8 = h8[-3:].mean(0) - h8[0]
+    d16 = h16[-3:].mean(0) - h16[0]
+    print("c4 fp8  first", h8[0].tolist(), "last", h8[-1].tolist(), "change", d8.tolist())
+    print("c4 bf16 first", h16[0].tolist(), "last", h16[-1].tolist(), "change", d16.tolist())
+    for h, flag, fin in ((h8, flag8, fin8), (h16, flag16, fin16)):
+        assert torch.isfinite(h).all() and flag == 0 and fin
+        assert h[-3:].mean(0).sum() < 0.9 * h[0].sum(), (h[0], h[-1])
+    # both runs start from the same parameters: the first losses differ by the fp8 forward's rounding only
+    assert ((h8[0] - h16[0]).abs() / h16[0]).max() < 2e-2, (h8[0], h16[0])
+    for i in range(h8.shape[1]):
+        start = h16[0, i].item()
+        if d16[i] < -0.02 * start:
+            assert d8[i] < 0.5 * d16[i], (i, d8[i].item(), d16[i].item())
+        else:
+            assert abs(d8[i] - d16[i]) < 0.01 * start, (i, d8[i].item(), d16[i].item())

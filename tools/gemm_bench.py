@@ -59,6 +59,9 @@ SHAPES = [
     ("tgt_qkv1_fwd", 1, 1, "bias_tanh_bf16", R, 768, 512, 1),
     ("tgt_proj_dx", 1, 0, "dtanh_bf16", R, 512, 512, 1),
     ("tgt_qkv1_dx", 1, 0, "store_f32", R, 512, 768, 1),
+    ("tgt_ffn0_epi_only", 1, 1, "bias_relu_bf16", R, 2048, 0, 1),
+    ("tgt_ffn2dx_epi_only", 1, 0, "drelu_bf16", R, 2048, 0, 1),
+    ("tgt_ffn2_fwd", 1, 1, "bias_resid_f32", R, 512, 2048, 1),
     ("c4_ffn0_fwd", 1, 1, "bias_relu_bf16", R, 4096, 1024, 1),
     ("c4_ffn0_store", 1, 1, "store_bf16", R, 4096, 1024, 1),
     ("c4_ffn2_dx", 1, 0, "drelu_bf16", R, 4096, 1024, 1),

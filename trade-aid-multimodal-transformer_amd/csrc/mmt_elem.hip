@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbBatch batch, int R, i
 }
 
 // token-table gradient, privatised in LDS: a block owns one column slab (SLAB floats, the widest
-// power of two with V * SLAB floats <= EMB_LDS_FLOATS) of one modality's table and a chunk of rows;
+// power of two with V * SLAB floats <= the launch's LDS limit) of one modality's table and a chunk of rows;
 // it scatter-adds its rows into the LDS slab (ds_add_f32) and flushes the slab. Two flush forms:
 //  * with a scratch buffer (EmbProblem::part, the engine's path): plain stores of the whole slab into
 //    the chunk's partial table [chunk][V][C], then embed_tok_reduce_kernel adds the partial tables
@@ -249,11 +249,15 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbBatch batch, int R, i
 //    drained (round 4: 174 us live at C1 with 64 blocks per modality of 16 dependent load rounds);
 //  * without one: one global atomic per touched entry, rows per block >= 4 V so the atomics stay few.
 // A vocabulary too large for a 4-float slab takes direct atomics.
-#define EMB_LDS_FLOATS 8192
-__host__ __device__ __forceinline__ int emb_slab(int V, int C) {
-  if ((int64_t)V * C <= EMB_LDS_FLOATS) return C;
+// LDS per block: 32 KiB when every problem of the launch has partial-table scratch (short chunks, many
+// blocks per CU), 64 KiB for the atomic-flush form (mmt_op_embedding_bwd without scratch), so
+// vocabularies up to 4096 keep the LDS-privatised slab there
+#define EMB_LDS_PART 8192
+#define EMB_LDS_ATOMIC 16384
+__host__ __device__ __forceinline__ int emb_slab(int V, int C, int lf) {
+  if ((int64_t)V * C <= lf) return C;
   int p = 256;  // largest power-of-two slab dividing C that fits (4 always divides C)
-  while (p > 4 && (C % p != 0 || (int64_t)V * p > EMB_LDS_FLOATS)) p >>= 1;
+  while (p > 4 && (C % p != 0 || (int64_t)V * p > lf)) p >>= 1;
   return p;
 }
 #ifndef EMB_U
@@ -261,9 +265,9 @@ __host__ __device__ __forceinline__ int emb_slab(int V, int C) {
 #endif
 // rows per chunk: with partial tables two load rounds per thread (as long as the [chunk][V][C]
 // tables fit the B*T*C-float scratch), else >= 4 V rows (atomic flush)
-__host__ __device__ __forceinline__ int emb_chunk(const EmbProblem& P, int R, int C) {
-  const int rpp = 256 / (emb_slab(P.V, C) >> 2);
-  if (P.part && (int64_t)P.V * emb_slab(P.V, C) <= EMB_LDS_FLOATS) {
+__host__ __device__ __forceinline__ int emb_chunk(const EmbProblem& P, int R, int C, int lf) {
+  const int rpp = 256 / (emb_slab(P.V, C, lf) >> 2);
+  if (P.part && (int64_t)P.V * emb_slab(P.V, C, lf) <= lf) {
     int ch = rpp * EMB_U * 2;
     while ((int64_t)((R + ch - 1) / ch) * P.V > R && ch < R) ch <<= 1;
     if ((int64_t)((R + ch - 1) / ch) * P.V <= R) return ch;
@@ -272,24 +276,25 @@ __host__ __device__ __forceinline__ int emb_chunk(const EmbProblem& P, int R, in
   while (ch < 4 * P.V && ch < R) ch <<= 1;
   return ch;
 }
-__host__ __device__ __forceinline__ bool emb_use_part(const EmbProblem& P, int R, int C) {
-  if (!P.part || (int64_t)P.V * emb_slab(P.V, C) > EMB_LDS_FLOATS) return false;
-  const int ch = emb_chunk(P, R, C);
+__host__ __device__ __forceinline__ bool emb_use_part(const EmbProblem& P, int R, int C, int lf) {
+  if (!P.part || (int64_t)P.V * emb_slab(P.V, C, lf) > lf) return false;
+  const int ch = emb_chunk(P, R, C, lf);
   return (int64_t)((R + ch - 1) / ch) * P.V <= R;
 }
+template <int LF>
 __global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int R, int C) {
   const EmbProblem& P = batch.p[blockIdx.z];
   const int V = P.V;
-  const int slab = emb_slab(V, C);
+  const int slab = emb_slab(V, C, LF);
   const int nslab = C / slab;
-  const int chunk = emb_chunk(P, R, C);
+  const int chunk = emb_chunk(P, R, C, LF);
   const int nchunk = (R + chunk - 1) / chunk;
   if ((int)blockIdx.x >= nslab * nchunk) return;
   const int sl = blockIdx.x % nslab, ck = blockIdx.x / nslab;
   const int c0 = sl * slab;
   const int r0 = ck * chunk, r1 = min(R, r0 + chunk);
-  __shared__ float acc[EMB_LDS_FLOATS];
-  const bool priv = (int64_t)V * slab <= EMB_LDS_FLOATS;
+  __shared__ float acc[LF];
+  const bool priv = (int64_t)V * slab <= LF;
   if (priv) {
     for (int q = threadIdx.x; q < V * slab; q += 256) acc[q] = 0.f;
     __syncthreads();
@@ -327,7 +332,7 @@ __global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int 
   }
   if (priv) {
     __syncthreads();
-    if (emb_use_part(P, R, C)) {  // the whole slab into this chunk's partial table
+    if (emb_use_part(P, R, C, LF)) {  // the whole slab into this chunk's partial table
       float* pt = P.part + (int64_t)ck * V * C + c0;
       for (int q = threadIdx.x; q < V * slab; q += 256) pt[(int64_t)(q / slab) * C + (q % slab)] = acc[q];
     } else {
@@ -342,11 +347,12 @@ __global__ __launch_bounds__(256) void embed_tok_bwd_kernel(EmbBatch batch, int 
 // and adds it with four atomics (a thread looping over every chunk ran 256 dependent loads deep for
 // the small vocabularies: 68 us at C1)
 #define EMB_RED 16
+template <int LF>
 __global__ __launch_bounds__(256) void embed_tok_reduce_kernel(EmbBatch batch, int R, int C) {
   const EmbProblem& P = batch.p[blockIdx.z];
-  if (!emb_use_part(P, R, C)) return;
+  if (!emb_use_part(P, R, C, LF)) return;
   const int V = P.V, C4 = C >> 2;
-  const int ch = emb_chunk(P, R, C);
+  const int ch = emb_chunk(P, R, C, LF);
   const int nchunk = (R + ch - 1) / ch;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int k0 = blockIdx.y * EMB_RED;
@@ -407,27 +413,32 @@ hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStrea
   const int R = B * T;
   if (C % 4 || C > 1024) return hipErrorInvalidValue;
   // grid: the largest (slabs x row chunks) over the problems
+  bool all_part = true;
+  for (int g = 0; g < b.count; ++g) all_part = all_part && b.p[g].part != nullptr;
+  const int lf = all_part ? EMB_LDS_PART : EMB_LDS_ATOMIC;
   int maxblocks = 1, maxv = 1;
   bool any_part = false;
   for (int g = 0; g < b.count; ++g) {
-    const int ch = emb_chunk(b.p[g], R, C);
-    const int nb = (C / emb_slab(b.p[g].V, C)) * ((R + ch - 1) / ch);
+    const int ch = emb_chunk(b.p[g], R, C, lf);
+    const int nb = (C / emb_slab(b.p[g].V, C, lf)) * ((R + ch - 1) / ch);
     maxblocks = nb > maxblocks ? nb : maxblocks;
     maxv = b.p[g].V > maxv ? b.p[g].V : maxv;
-    any_part = any_part || emb_use_part(b.p[g], R, C);
+    any_part = any_part || emb_use_part(b.p[g], R, C, lf);
   }
-  hipLaunchKernelGGL(embed_tok_bwd_kernel, dim3(maxblocks, 1, b.count), dim3(256), 0, s, b, R, C);
+  if (all_part) hipLaunchKernelGGL(embed_tok_bwd_kernel<EMB_LDS_PART>, dim3(maxblocks, 1, b.count), dim3(256), 0, s, b, R, C);
+  else hipLaunchKernelGGL(embed_tok_bwd_kernel<EMB_LDS_ATOMIC>, dim3(maxblocks, 1, b.count), dim3(256), 0, s, b, R, C);
   if (any_part) {
     int maxg = 1;
     for (int g = 0; g < b.count; ++g) {
-      if (!emb_use_part(b.p[g], R, C)) continue;
-      const int ch = emb_chunk(b.p[g], R, C);
+      if (!emb_use_part(b.p[g], R, C, lf)) continue;
+      const int ch = emb_chunk(b.p[g], R, C, lf);
       const int ng = ((R + ch - 1) / ch + EMB_RED - 1) / EMB_RED;
       maxg = ng > maxg ? ng : maxg;
     }
     const int64_t n4 = (int64_t)maxv * (C / 4);
-    hipLaunchKernelGGL(embed_tok_reduce_kernel, dim3((unsigned)((n4 + 255) / 256), maxg, b.count), dim3(256), 0, s, b, R,
-                       C);
+    const dim3 grid((unsigned)((n4 + 255) / 256), maxg, b.count);
+    if (all_part) hipLaunchKernelGGL(embed_tok_reduce_kernel<EMB_LDS_PART>, grid, dim3(256), 0, s, b, R, C);
+    else hipLaunchKernelGGL(embed_tok_reduce_kernel<EMB_LDS_ATOMIC>, grid, dim3(256), 0, s, b, R, C);
   }
   // all problems of one batch must share the positional table (one model): dpos of p[0]
   for (int g = 1; g < b.count; ++g)

@@ -160,6 +160,9 @@ struct mmt_ctx {
   hipStream_t side = nullptr;
   int side_device = -1;
   bool side_off = false;  // mmt_set_side_stream(ctx, 0): this context runs everything on the caller's stream
+  bool side_off_req = false;  // the requested setting, latched into side_off by the next mmt_forward (a
+                              // forward and its backward always see one setting: work forked to the side
+                              // stream is always joined)
   // mmt_backward (all stages in one call): no join per stage; the side stream's work of stage t is
   // recorded in stage_ev[t & 1] and the main stream waits for it only at the start of stage t + 2,
   // the first stage that rewrites that parity's scratch (Plan). mmt_backward_stage called alone (the
@@ -1726,6 +1729,7 @@ int mmt_forward(mmt_ctx* c, void* stream, int32_t batch, const int64_t* const* i
   if (c->plan.B != batch) make_plan(c, batch);
   int rc = ensure_device_tables(c);
   if (rc) return rc;
+  c->side_off = c->side_off_req;
   Runner r{c, (hipStream_t)stream, workspace, params, nullptr, batch, batch * c->T};
   // dropout (training mode only, as nn.Dropout): one seed per training forward, reused by its backward
   r.drop = training && c->cfg.dropout > 0.f;
@@ -1823,10 +1827,11 @@ int mmt_backward(mmt_ctx* c, void* stream, const float* loss_grads, const float*
   int rc = MMT_OK;
   for (int s = 0; s < c->L + 2 && rc == MMT_OK; ++s) rc = mmt_backward_stage(c, stream, s, loss_grads, params, grads, workspace);
   c->defer_join = false;
-  if (rc) return rc;
+  // the join also on the error path: no weight-gradient GEMM (or its split-K slab) of this backward is
+  // left running on the side stream once control is back with the caller
   Runner r{c, (hipStream_t)stream, workspace, params, nullptr, c->plan.B, c->plan.B * c->T};
   r.join();
-  return r.rc;
+  return rc ? rc : r.rc;
 }
 
 int mmt_adamw_step(mmt_ctx* c, void* stream, float* params, const float* grads, float* m, float* v, int64_t n,
@@ -1865,11 +1870,11 @@ extern "C" int mmt_set_dropout_seed(mmt_ctx* c, uint64_t seed) {
 // comma-separated patterns of `label` (e.g. "*_dw,attn_fwd,attn_bwd,ffn0"), recorded on the stream
 // the launch runs on, so bench.py can price kernels inside the timed region.
 // serial mode for measurement (bench.py's serial roofline leg): 0 = everything of this context on the
-// caller's stream, 1 = the side stream again; switch between steps only (a backward joins the side
-// stream its forward forked)
+// caller's stream, 1 = the side stream again. Latched: the next mmt_forward applies it, so a call between
+// a forward and its backward (or between backward stages) never strands forked side-stream work
 extern "C" int mmt_set_side_stream(mmt_ctx* c, int32_t on) {
   if (!c) return MMT_ERR_INVALID;
-  c->side_off = on == 0;
+  c->side_off_req = on == 0;
   return MMT_OK;
 }
 

@@ -593,7 +593,7 @@ static int g_big_variant = [] {
 #ifndef MMT_DEF_VARIANT
 #define MMT_DEF_VARIANT 0
 #endif
-hipError_t mmt_launch_gemm8(const GemmBatch& b, int epi, bool b_kc, int mt, hipStream_t s);  // mmt_gemm8.hip
+hipError_t mmt_launch_gemm8(const GemmBatch& b, int epi, bool a_kc, bool b_kc, dim3 grid, hipStream_t s);  // mmt_gemm8.hip
 
 static bool gemm8_on() {
   static const int env = [] {
@@ -609,13 +609,11 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
   if (big) {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
-    // forward / backward-data products (K-contiguous X) on the ping-pong kernel
-    if constexpr (A_KC && SWAP && EPI != EPI_ATOMIC_F32) {
-      if (gemm8_on()) {
-        return mmt_launch_gemm8(b, EPI, B_KC, mt, s);
-      }
-    }
     dim3 grid(mt, EPI == EPI_ATOMIC_F32 ? auto_splits<TileL>(b, splits) : std::max(1, splits), b.count);
+    // forward / backward-data / weight-gradient (slab, accumulate) products on the ping-pong kernel
+    if constexpr (SWAP && (EPI != EPI_ATOMIC_F32) && (A_KC || !B_KC)) {
+      if (gemm8_on()) return mmt_launch_gemm8(b, EPI, A_KC, B_KC, grid, s);
+    }
     const int bv = g_gemm_big_variant_rt ? g_gemm_big_variant_rt
                    : g_big_variant >= 0  ? g_big_variant
                    : (!A_KC && !B_KC)    ? 1

@@ -24,9 +24,11 @@
 // read. A wave's wait + the barrier that closes its load segment publish its pieces; with the one-barrier
 // group stagger every read still follows both groups' waits (the reader's load segment starts after the
 // other group's next barrier). Refills reuse a half-tile >= 2 phases after its last read.
-// K-contiguous images [128 rows][64 k] (128-B rows, kc_swz<64>); an MN-contiguous W (B_KC = false: the
-// backward-data product, W stored [K][N]) as [64 k][128 n] (256-B rows, chunk ^ ((k & 3) << 2 | (k >> 3 & 1) << 1),
-// conflict-free ds_read_b64_tr_b16 reads).
+// K-contiguous images [128 rows][64 k] (128-B rows, kc_swz<64>); an MN-contiguous operand (B_KC = false: the
+// backward-data product, W stored [K][N]; A_KC = B_KC = false: the weight gradient dW = dY^T X, both stored
+// [K][rows]) as [64 k][128 cols] (256-B rows, chunk ^ ((k & 3) << 2 | (k >> 3 & 1) << 1), conflict-free
+// ds_read_b64_tr_b16 reads). Split-K (weight gradients): blockIdx.y = K slice, each writing its own fp32 slab
+// (o32 + slice * split_stride), with the XCD-major (tile, slice, problem) order of gemm_kernel.
 // ---------------------------------------------------------------------------------------------
 template <int SUB, bool IS_W, bool KC>
 __device__ __forceinline__ void issue_half(const i32x4& rsrc, uint32_t img, int ld, int rows_total, int K, int r0, int k0,
@@ -43,10 +45,10 @@ __device__ __forceinline__ void issue_half(const i32x4& rsrc, uint32_t img, int 
       const int trow = IS_W ? ((irow >> 5) * 64 + (irow & 31) + SUB * 32) : ((irow >> 6) * 128 + (irow & 63) + SUB * 64);
       const int gk = k0 + chunk * 8;
       voff = (r0 + trow < rows_total && gk < K) ? (trow * ld + gk) * 2 : 0x7fffffff;
-    } else {  // W [K][N] (rsrc based at row k0): image [64 k][128 n]
+    } else {  // operand stored [K][rows] (rsrc based at row k0): image [64 k][128 cols]
       const int kr = 4 * i + (lane >> 4);
       const int c = (lane & 15) ^ (((kr & 3) << 2) | (((kr >> 3) & 1) << 1));  // image chunk stored at slot lane & 15
-      const int tcol = (c >> 2) * 64 + (c & 3) * 8 + SUB * 32;
+      const int tcol = IS_W ? (c >> 2) * 64 + (c & 3) * 8 + SUB * 32 : (c >> 3) * 128 + (c & 7) * 8 + SUB * 64;
       voff = (k0 + kr < K && r0 + tcol < rows_total) ? (kr * ld + r0 + tcol) * 2 : 0x7fffffff;
     }
     dma16(rsrc, img + i * 1024, voff);
@@ -72,14 +74,22 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int EPI, bool B_KC>
+template <int EPI, bool A_KC, bool B_KC>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmBatch batch) {
   using TL = TileL;  // 256 x 256, 8 waves 2 (m) x 4 (n): epilogue geometry
   constexpr int HT = 16384;          // half-tile bytes
   constexpr int EPI_ROWS = 64;
-  int tile = blockIdx.x;
-  const int prob = blockIdx.z;
-  {
+  int tile = blockIdx.x, split = blockIdx.y, prob = blockIdx.z;
+  const int nsplit = gridDim.y;
+  if (batch.xcd_plane) {  // XCD-major order of the whole (tile, split, problem) grid (as gemm_kernel)
+    const int nwg = gridDim.x * nsplit * gridDim.z;
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + nsplit * blockIdx.z);
+    const int x = lin % 8, q = nwg / 8, rr = nwg % 8;
+    const int l2 = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + lin / 8;
+    tile = l2 % gridDim.x;
+    split = (l2 / gridDim.x) % nsplit;
+    prob = l2 / (gridDim.x * nsplit);
+  } else {
     const int nwg = gridDim.x;
     const int x = tile % 8, q = nwg / 8, rr = nwg % 8;
     tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + tile / 8;
@@ -93,7 +103,11 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmBatch batch) {
   if (tile >= tiles_m * tiles_n) return;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * 256, n0 = tn * 256;
-  const int nk = (K + 63) / 64;
+  const int ktiles = (K + 63) / 64;
+  const int kper = (ktiles + nsplit - 1) / nsplit;
+  const int kt0 = split * kper;
+  const int nk = max(0, min(ktiles, kt0 + kper) - kt0);
+  if (EPI == EPI_ATOMIC_F32 && nk == 0) return;
   __shared__ __attribute__((aligned(1024))) char lds[8 * HT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -107,17 +121,19 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmBatch batch) {
 
   if (nk > 0) {
     const int lda = __builtin_amdgcn_readfirstlane(P.lda), ldb = __builtin_amdgcn_readfirstlane(P.ldb);
+    const bf16_t* const Ap = P.A;
     const bf16_t* const Bp = P.B;
-    const i32x4 rx = op_rsrc<true>(P.A, lda, M, K, m0, 0);
+    const i32x4 rx_kc = A_KC ? op_rsrc<true>(Ap, lda, M, K, m0, 0) : i32x4{0, 0, 0, 0};
     const i32x4 rw_kc = B_KC ? op_rsrc<true>(Bp, ldb, N, K, n0, 0) : i32x4{0, 0, 0, 0};
-    // rsrc of an MN-contiguous W from row k0 (32-bit offsets: op_rsrc); N offsets stay absolute there
+    // rsrc of an MN-contiguous operand from row k0 (32-bit offsets: op_rsrc); column offsets stay absolute there
+    auto rx = [&](int k0) { return A_KC ? rx_kc : op_rsrc<false>(Ap, lda, M, K, 0, k0); };
     auto rw = [&](int k0) { return B_KC ? rw_kc : op_rsrc<false>(Bp, ldb, N, K, 0, k0); };
     const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_u32(lds));
-    auto issue = [&](int which, int buf, int t) {  // which: 0 XA, 1 WA, 2 WB, 3 XB
+    auto issue = [&](int which, int buf, int t) {  // which: 0 XA, 1 WA, 2 WB, 3 XB; t: K-tile of this slice
       const uint32_t base = lbase + buf * 4 * HT;
-      const int k0 = t * 64;
-      if (which == 0) issue_half<0, false, true>(rx, base + 0 * HT, lda, M, K, m0, k0, wave, lane);
-      else if (which == 3) issue_half<1, false, true>(rx, base + 1 * HT, lda, M, K, m0, k0, wave, lane);
+      const int k0 = (kt0 + t) * 64;
+      if (which == 0) issue_half<0, false, A_KC>(rx(k0), base + 0 * HT, lda, M, K, m0, k0, wave, lane);
+      else if (which == 3) issue_half<1, false, A_KC>(rx(k0), base + 1 * HT, lda, M, K, m0, k0, wave, lane);
       else if (which == 1) issue_half<0, true, B_KC>(rw(k0), base + 2 * HT, ldb, N, K, n0, k0, wave, lane);
       else issue_half<1, true, B_KC>(rw(k0), base + 3 * HT, ldb, N, K, n0, k0, wave, lane);
     };
@@ -126,7 +142,8 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmBatch batch) {
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) xf[mb][s] = frag16_kc(img, wr * 64 + 16 * mb, s, lane);
+        for (int s = 0; s < 2; ++s)
+          xf[mb][s] = A_KC ? frag16_kc(img, wr * 64 + 16 * mb, s, lane) : frag16_mn(img, wr * 64 + 16 * mb, s, lane);
     };
     auto read_w = [&](const char* img) {
 #pragma unroll
@@ -201,37 +218,47 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmBatch batch) {
   }
   float alpha = P.alpha;
   if (P.alpha_ptr) alpha *= *P.alpha_ptr;
-  float* o32 = P.o32;
+  float* o32 = P.o32 + (P.split_stride ? (int64_t)split * P.split_stride : (int64_t)0);
   epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
 }
 
-template <int EPI>
-static hipError_t launch8(const GemmBatch& b, bool b_kc, int mt, hipStream_t s) {
-  if (b_kc) hipLaunchKernelGGL((gemm8_kernel<EPI, true>), dim3(mt, 1, b.count), dim3(512), 0, s, b);
-  else hipLaunchKernelGGL((gemm8_kernel<EPI, false>), dim3(mt, 1, b.count), dim3(512), 0, s, b);
+template <int EPI, bool A_KC, bool B_KC>
+static hipError_t launch8(const GemmBatch& b, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemm8_kernel<EPI, A_KC, B_KC>), grid, dim3(512), 0, s, b);
   return hipGetLastError();
 }
 
-// the forward (b_kc) and backward-data (!b_kc: W stored [K][N]) products; mt = 256 x 256 tiles of the
-// largest problem. hipErrorInvalidValue for an epilogue the kernel does not instantiate.
-hipError_t mmt_launch_gemm8(const GemmBatch& b, int epi, bool b_kc, int mt, hipStream_t s) {
-  if (b_kc) {
+// grid = (256 x 256 tiles of the largest problem, K slices, problems). The forward (a_kc, b_kc), backward-data
+// (a_kc, !b_kc: W stored [K][N]) and weight-gradient (!a_kc, !b_kc: slab or accumulate) products;
+// hipErrorInvalidValue for an epilogue the kernel does not instantiate.
+hipError_t mmt_launch_gemm8(const GemmBatch& b, int epi, bool a_kc, bool b_kc, dim3 grid, hipStream_t s) {
+  if (a_kc && b_kc) {
     switch (epi) {
-      case EPI_STORE_BF16: return launch8<EPI_STORE_BF16>(b, true, mt, s);
-      case EPI_BIAS_TANH_BF16: return launch8<EPI_BIAS_TANH_BF16>(b, true, mt, s);
-      case EPI_BIAS_RELU_BF16: return launch8<EPI_BIAS_RELU_BF16>(b, true, mt, s);
-      case EPI_BIAS_RESID_F32: return launch8<EPI_BIAS_RESID_F32>(b, true, mt, s);
-      case EPI_STORE_F32: return launch8<EPI_STORE_F32>(b, true, mt, s);
-      case EPI_ACC_F32: return launch8<EPI_ACC_F32>(b, true, mt, s);
+      case EPI_STORE_BF16: return launch8<EPI_STORE_BF16, true, true>(b, grid, s);
+      case EPI_BIAS_TANH_BF16: return launch8<EPI_BIAS_TANH_BF16, true, true>(b, grid, s);
+      case EPI_BIAS_RELU_BF16: return launch8<EPI_BIAS_RELU_BF16, true, true>(b, grid, s);
+      case EPI_BIAS_RESID_F32: return launch8<EPI_BIAS_RESID_F32, true, true>(b, grid, s);
+      case EPI_STORE_F32: return launch8<EPI_STORE_F32, true, true>(b, grid, s);
+      case EPI_ACC_F32: return launch8<EPI_ACC_F32, true, true>(b, grid, s);
       default: return hipErrorInvalidValue;
     }
   }
-  switch (epi) {
-    case EPI_STORE_BF16: return launch8<EPI_STORE_BF16>(b, false, mt, s);
-    case EPI_DTANH_BF16: return launch8<EPI_DTANH_BF16>(b, false, mt, s);
-    case EPI_DRELU_BF16: return launch8<EPI_DRELU_BF16>(b, false, mt, s);
-    case EPI_STORE_F32: return launch8<EPI_STORE_F32>(b, false, mt, s);
-    case EPI_ACC_F32: return launch8<EPI_ACC_F32>(b, false, mt, s);
-    default: return hipErrorInvalidValue;
+  if (a_kc) {
+    switch (epi) {
+      case EPI_STORE_BF16: return launch8<EPI_STORE_BF16, true, false>(b, grid, s);
+      case EPI_DTANH_BF16: return launch8<EPI_DTANH_BF16, true, false>(b, grid, s);
+      case EPI_DRELU_BF16: return launch8<EPI_DRELU_BF16, true, false>(b, grid, s);
+      case EPI_STORE_F32: return launch8<EPI_STORE_F32, true, false>(b, grid, s);
+      case EPI_ACC_F32: return launch8<EPI_ACC_F32, true, false>(b, grid, s);
+      default: return hipErrorInvalidValue;
+    }
   }
+  if (!b_kc) {
+    switch (epi) {
+      case EPI_STORE_F32: return launch8<EPI_STORE_F32, false, false>(b, grid, s);
+      case EPI_ACC_F32: return launch8<EPI_ACC_F32, false, false>(b, grid, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  return hipErrorInvalidValue;
 }
