@@ -217,6 +217,18 @@ int mmt_op_gemm_qkv(void* stream, int32_t M, int32_t N, int32_t K, const void* A
  * pass, the engine's path for every dW of the backward */
 int mmt_op_gemm_wgrad(void* stream, int32_t M, int32_t N, int32_t K, const void* A, int32_t lda, const void* B,
                       int32_t ldb, float* out, int32_t ldc, float alpha, void* slab, int64_t slab_bytes);
+/* attention out-projection as ONE fused launch (the engine's forward path at C = 256 / 512; replaces the
+ * pair mmt_op_gemm(bias_tanh_bf16) + mmt_op_gemm(bias_resid_f32), reference model.py:82-92 / 102-117):
+ *   h[M, C/2]  = bf16(tanh(x[M, C] W0[C/2, C]^T + b0))      (stored: the backward reads it)
+ *   out[M, C]  = resid + keep(m, n) * (h W2[C, C/2]^T + b2)  (fp32; hash dropout of drop_key / drop_thr,
+ *                kept values times drop_scale, 0: off), out16 (nullable) its bf16 copy;
+ *   lnf_y (nullable) = bf16(LayerNorm(out) * lnf_gamma + lnf_beta), lnf_mean / lnf_rstd its row statistics
+ * with h kept in LDS between the products. C must be 256 or 512 (else MMT_ERR_UNSUPPORTED); row strides
+ * ldx, ldw0 (W0), ldw2 (W2), ldh (h); out / resid / out16 / lnf_y have stride C. */
+int mmt_op_mlp2(void* stream, int32_t M, int32_t C, const void* x, int32_t ldx, const void* w0, int32_t ldw0,
+                const float* b0, const void* w2, int32_t ldw2, const float* b2, void* h, int32_t ldh, const float* resid,
+                float* out, void* out16, uint32_t drop_key, uint32_t drop_thr, float drop_scale, const float* lnf_gamma,
+                const float* lnf_beta, void* lnf_y, float* lnf_mean, float* lnf_rstd);
 int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
                          void* y16, float* mean, float* rstd);
 int mmt_op_layernorm_bwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* mean,

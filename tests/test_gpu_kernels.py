@@ -397,6 +397,59 @@ def test_gemm_ln_bwd_fused(M, N, K, drop):
                                 1.0) == -2  # MMT_ERR_UNSUPPORTED
 
 
+@pytest.mark.parametrize("M,C,drop,lnf", [(1000, 256, 0.0, False), (300, 256, 0.1, True), (4096, 512, 0.1, False),
+                                          (130, 512, 0.0, True), (65536, 512, 0.1, False), (65536, 256, 0.0, True)])
+def test_mlp2_fused(M, C, drop, lnf):
+    """The attention out-projection as one launch (mmt_op_mlp2: Linear(C, C/2) -> tanh -> Linear(C/2, C) ->
+    hash dropout -> + residual, h kept in LDS; reference model.py:82-92) against torch on the same bf16
+    operands: h (stored for the backward) within one bf16 rounding of the torch tanh, the fp32 output
+    rel 1e-3 (h enters the second product as bf16 in both), the optional next LayerNorm on the owned
+    rows; the full-chip cases keep every CU busy with both ring protocols."""
+    import mmt_oracle as O
+    torch.manual_seed(M + C)
+    N1 = C // 2
+    ldx = C
+    x = bf(torch.randn(M, C, device=DEV))
+    w0 = bf(torch.randn(N1, C, device=DEV) * 0.05)
+    b0 = torch.randn(N1, device=DEV) * 0.1
+    w2 = bf(torch.randn(C, N1, device=DEV) * 0.05)
+    b2 = torch.randn(C, device=DEV) * 0.1
+    resid = torch.randn(M, C, device=DEV)
+    h = torch.zeros(M, N1, dtype=torch.bfloat16, device=DEV)
+    out = torch.zeros(M, C, device=DEV)
+    out16 = torch.zeros(M, C, dtype=torch.bfloat16, device=DEV)
+    hd = O.HashDropout(11, drop) if drop else None
+    key = 0x2468ACE
+    g = torch.randn(C, device=DEV)
+    be = torch.randn(C, device=DEV)
+    ly = torch.zeros(M, C, dtype=torch.bfloat16, device=DEV) if lnf else None
+    lm = torch.zeros(M, device=DEV) if lnf else None
+    lr = torch.zeros(M, device=DEV) if lnf else None
+    L = ML.lib()
+    rc = L.mmt_op_mlp2(_s(), M, C, ML.ptr(x), ldx, ML.ptr(w0), C, ML.ptr(b0), ML.ptr(w2), N1, ML.ptr(b2), ML.ptr(h), N1,
+                       ML.ptr(resid), ML.ptr(out), ML.ptr(out16), key, hd.thr if hd else 0, hd.scale if hd else 1.0,
+                       ML.ptr(g) if lnf else None, ML.ptr(be) if lnf else None, ML.ptr(ly), ML.ptr(lm), ML.ptr(lr))
+    assert rc == 0
+    _sync()
+    href = torch.tanh(x.float() @ w0.float().t() + b0)
+    assert rel(h, href) < 8e-3
+    y = h.float() @ w2.float().t() + b2  # the kernel's own bf16 h as the second operand
+    if hd:
+        rows = torch.arange(M).numpy()[:, None]
+        cols = torch.arange(C).numpy()[None, :]
+        y = y * hd._mask(key, rows, cols).to(DEV)
+    ref = resid + y
+    assert rel(out, ref) < 1e-4
+    assert rel(out16, ref) < 1e-2
+    if lnf:
+        lref = torch.nn.functional.layer_norm(out, (C,), g, be, 1e-5)
+        assert rel(ly, lref) < 1e-2
+        assert rel(lm, out.mean(1)) < 1e-5
+    # other widths are refused (the engine then runs the two GEMMs)
+    assert L.mmt_op_mlp2(_s(), M, 128, ML.ptr(x), ldx, ML.ptr(w0), C, ML.ptr(b0), ML.ptr(w2), N1, ML.ptr(b2), ML.ptr(h),
+                         N1, ML.ptr(resid), ML.ptr(out), None, 0, 0, 1.0, None, None, None, None, None) == -2
+
+
 # --------------------------------------------------------------------------------- attention
 def _attn_ref(q, ks, vs, scale):
     # q [B,H,T,hs], ks/vs list of [B,H,T,hs]; sum over streams of causal softmax attention

@@ -693,6 +693,39 @@ struct Runner {
     gemm(dx, true, false, EPI_STORE_F32, 1, gname);
     ok(mmt_launch_ln_bwd(lb, R, C, s), lname);
   }
+  // the attention out-projection Linear(C, C/2) -> tanh -> Linear(C/2, C) + dropout + residual as one fused
+  // launch (mmt_launch_mlp2: h stays in LDS between the products); false (nothing launched) when the
+  // shape is outside the fused kernel or MMT_MLP2=0, and the caller runs the two GEMMs
+  bool mlp2(const GemmProblem* g1s, const GemmProblem* g2s, int n, const char* what) {
+    static const bool on = [] {
+      const char* e = getenv("MMT_MLP2");
+      return e ? atoi(e) != 0 : true;
+    }();
+    if (rc != MMT_OK || !on || n < 1) return false;
+    Mlp2Batch chunk[(MMT_MAX_GROUP + MMT_MLP2_GROUP - 1) / MMT_MLP2_GROUP] = {};
+    const int nch = (n + MMT_MLP2_GROUP - 1) / MMT_MLP2_GROUP;
+    for (int i = 0; i < n; ++i) {
+      Mlp2Batch& b = chunk[i / MMT_MLP2_GROUP];
+      b.g1[b.count] = g1s[i];
+      b.g2[b.count] = g2s[i];
+      ++b.count;
+    }
+    for (int k = 0; k < nch; ++k)
+      if (!mmt_mlp2_ok(chunk[k])) return false;
+    const int id = probe_begin(what, s);
+    for (int k = 0; k < nch; ++k) ok(mmt_launch_mlp2(chunk[k], s), what);
+    if (id >= 0) {
+      double fl = 0, by = 0;
+      GemmBatch g1{}, g2{};
+      g1.count = g2.count = n;
+      for (int g = 0; g < n; ++g) { g1.p[g] = g1s[g]; g2.p[g] = g2s[g]; }
+      gemm_cost(g1, EPI_BIAS_TANH_BF16, &fl, &by);
+      gemm_cost(g2, EPI_BIAS_RESID_F32, &fl, &by);
+      for (int g = 0; g < n; ++g) by -= (double)g2s[g].M * g2s[g].K * 2.0;  // h is not read back
+      probe_end(id, s, fl, by);
+    }
+    return true;
+  }
   // forward residual GEMM with the next LayerNorm's forward fused (mmt_launch_gemm_resid_ln)
   bool gemm_resid_ln(const GemmBatch& b, const char* what) {
     if (rc != MMT_OK || !mmt_gemm_resid_ln_ok(b)) return false;
@@ -932,18 +965,27 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         for (int ll = 1; ll < c->L; ++ll) gen_masks(ll);
     }
     r.attn(ab, false, scale, "attn_fwd");
-    for (int i = 0; i < M; ++i) {
-      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].o), C, wpk, x[i].P0, R);
-      g.p[i].bias = r.P(x[i].bp0); g.p[i].o16 = r.W<bf16_t>(a[i].p1); g.p[i].ldo16 = ldp;
+    {
+      // out-projection: Linear(C, C/2) -> tanh -> Linear(C/2, C) -> dropout -> + residual (model.py:82-92,
+      // 224), fused into one launch where the shape allows (C = 256 / 512), else two GEMMs
+      GemmProblem pg1[MAXM], pg2[MAXM];
+      for (int i = 0; i < M; ++i) {
+        GemmProblem& g1 = pg1[i];
+        g1 = gp_fwd(r.W<bf16_t>(a[i].o), C, wpk, x[i].P0, R);
+        g1.bias = r.P(x[i].bp0); g1.o16 = r.W<bf16_t>(a[i].p1); g1.ldo16 = ldp;
+        GemmProblem& g2 = pg2[i];
+        g2 = gp_fwd(r.W<bf16_t>(a[i].p1), ldp, wpk, x[i].P2, R);
+        g2.bias = r.P(x[i].bp2); g2.resid = xin[i]; g2.ldres = C;
+        g2.o32 = r.W<float>(a[i].x1); g2.ldc = C;
+        r.set_drop(g2, l, i, DS_SA_PROJ);
+      }
+      if (!r.mlp2(pg1, pg2, M, "proj")) {
+        for (int i = 0; i < M; ++i) g.p[i] = pg1[i];
+        r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "proj0");
+        for (int i = 0; i < M; ++i) g.p[i] = pg2[i];
+        r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "proj2");
+      }
     }
-    r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "proj0");
-    for (int i = 0; i < M; ++i) {
-      g.p[i] = gp_fwd(r.W<bf16_t>(a[i].p1), ldp, wpk, x[i].P2, R);
-      g.p[i].bias = r.P(x[i].bp2); g.p[i].resid = xin[i]; g.p[i].ldres = C;
-      g.p[i].o32 = r.W<float>(a[i].x1); g.p[i].ldc = C;
-      r.set_drop(g.p[i], l, i, DS_SA_PROJ);
-    }
-    r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "proj2");
     for (int i = 0; i < M; ++i) {
       lb.p[i].x = r.W<float>(a[i].x1); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].beta = r.P(x[i].ln2b);
       lb.p[i].y = r.W<bf16_t>(a[i].c); lb.p[i].mean = r.W<float>(a[i].mean2); lb.p[i].rstd = r.W<float>(a[i].rstd2);
@@ -1060,8 +1102,10 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         r.set_drop(g2.p[u], l, i, DS_CA_PROJ);
         xout[i] = r.W<float>(a[i].x3);
       }
-      r.gemm(g0, true, true, EPI_BIAS_TANH_BF16, 1, "ca_proj0");
-      r.gemm(g2, true, true, EPI_BIAS_RESID_F32, 1, "ca_proj2");
+      if (!r.mlp2(g0.p, g2.p, g0.count, "ca_proj")) {
+        r.gemm(g0, true, true, EPI_BIAS_TANH_BF16, 1, "ca_proj0");
+        r.gemm(g2, true, true, EPI_BIAS_RESID_F32, 1, "ca_proj2");
+      }
     }
     xin = xout;
   }

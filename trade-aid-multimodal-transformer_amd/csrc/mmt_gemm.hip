@@ -594,11 +594,21 @@ static int g_big_variant = [] {
 #define MMT_DEF_VARIANT 0
 #endif
 hipError_t mmt_launch_gemm8(const GemmBatch& b, int epi, bool a_kc, bool b_kc, dim3 grid, hipStream_t s);  // mmt_gemm8.hip
+// the (operand layouts, epilogue) pairs mmt_gemm8.hip instantiates
+constexpr bool gemm8_supports(bool akc, bool bkc, int epi) {
+  return (akc && bkc && (epi == EPI_STORE_BF16 || epi == EPI_BIAS_TANH_BF16 || epi == EPI_BIAS_RELU_BF16 ||
+                         epi == EPI_BIAS_RESID_F32 || epi == EPI_STORE_F32 || epi == EPI_ACC_F32)) ||
+         (akc && !bkc && (epi == EPI_STORE_BF16 || epi == EPI_DTANH_BF16 || epi == EPI_DRELU_BF16 ||
+                          epi == EPI_STORE_F32 || epi == EPI_ACC_F32)) ||
+         (!akc && !bkc && (epi == EPI_STORE_F32 || epi == EPI_ACC_F32));
+}
 
 static bool gemm8_on() {
+  // default on (round 5): C4 355 -> 350 ms/step, C3 153.3 -> 152.4, target / C1 neutral (same-box A/B,
+  // profiles/r5e_ab.txt); MMT_GEMM8=0 restores the 2-stage 256 x 256 ring everywhere
   static const int env = [] {
     const char* e = getenv("MMT_GEMM8");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 1;
   }();
   return g_gemm8_rt >= 0 ? g_gemm8_rt != 0 : env != 0;
 }
@@ -611,7 +621,7 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     if (mt == 0) return hipSuccess;
     dim3 grid(mt, EPI == EPI_ATOMIC_F32 ? auto_splits<TileL>(b, splits) : std::max(1, splits), b.count);
     // forward / backward-data / weight-gradient (slab, accumulate) products on the ping-pong kernel
-    if constexpr (SWAP && (EPI != EPI_ATOMIC_F32) && (A_KC || !B_KC)) {
+    if constexpr (SWAP && gemm8_supports(A_KC, B_KC, EPI)) {
       if (gemm8_on()) return mmt_launch_gemm8(b, EPI, A_KC, B_KC, grid, s);
     }
     const int bv = g_gemm_big_variant_rt ? g_gemm_big_variant_rt
@@ -669,12 +679,34 @@ static int g_big_kmin = [] {
   const char* e = getenv("MMT_GEMM_BIG_KMIN");
   return e ? atoi(e) : 1024;
 }();
+// K threshold of the ping-pong 256 x 256 kernel for launches with many tiles: at K = 512 it wins where
+// the launch has >= 4 tiles per CU (the target's ffn0 and ffn2 dX: 221 -> 177 and 252 -> 230 us
+// standalone; smaller launches leave CUs idle or lose the 128 x 128 tile's 2-3 blocks per CU beside the
+// side stream: every K = 512 launch on it measured +1 % on the target step)
+static int g_gemm8_kmin = [] {
+  const char* e = getenv("MMT_GEMM8_KMIN");
+  return e ? atoi(e) : 512;
+}();
+static int g_gemm8_min_tiles = [] {
+  const char* e = getenv("MMT_GEMM8_MIN_TILES");
+  return e ? atoi(e) : 1024;
+}();
 static bool use_big(const GemmBatch& b) {
   if (!g_big_mode || b.count == 0) return false;
+  bool big = true, qkv2 = false;
+  int tiles = 0;
   for (int g = 0; g < b.count; ++g) {
     const GemmProblem& P = b.p[g];
-    if (P.M < TileL::BM || P.N < TileL::BN || (P.K < g_big_kmin && !g_force_big_rt)) return false;
+    if (P.M < TileL::BM || P.N < TileL::BN) return false;
+    if (P.K < g_big_kmin && !g_force_big_rt) big = false;
+    qkv2 = qkv2 || P.qkv2_out != nullptr;
+    tiles += ((P.M + 255) / 256) * ((P.N + 255) / 256);
   }
+  if (big) return true;
+  // shorter K on the ping-pong kernel: only big launches, and never the fused Q/K/V stage 2 (128 x 128 only)
+  if (!gemm8_on() || qkv2 || tiles < g_gemm8_min_tiles) return false;
+  for (int g = 0; g < b.count; ++g)
+    if (b.p[g].K < g_gemm8_kmin) return false;
   return true;
 }
 

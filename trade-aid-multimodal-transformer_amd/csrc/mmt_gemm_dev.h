@@ -279,12 +279,31 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
     bias0 = *reinterpret_cast<const f32x4*>(P.bias + n);
     bias1 = *reinterpret_cast<const f32x4*>(P.bias + n + 4);
   }
+  // the aux operand (tanh' / ReLU' input) of pass p + 1 is loaded while pass p runs, the first pass's
+  // before the first staging: its HBM latency was exposed once per pass (ffn2 dX at the target: the
+  // epilogue alone 110-150 us of a 260 us launch). The pass barriers are raw s_barriers behind an LDS
+  // wait: __syncthreads() would also drain those loads (and the previous pass's stores) at every pass.
+  u32x4 auxn[IT];
+  auto load_aux = [&](int pass_) {
+    if (!(n + 8 <= N && vec_ok)) return;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int m = m0 + pass_ * EPI_ROWS + it * RPI + rsub;
+      if (m < M) auxn[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
+    }
+  };
+  if constexpr (HAS_AUX) load_aux(0);
+  auto lds_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll 1
   for (int pass = 0; pass < GBM / EPI_ROWS; ++pass) {
-    __syncthreads();  // stage-ring / previous pass reads done
+    lds_barrier();  // stage-ring / previous pass reads done
     stage_acc<TL, EPI_ROWS>(acc, ct, pass, lane, wave);
-    __syncthreads();
+    lds_barrier();
     const int mb = m0 + pass * EPI_ROWS;
     if constexpr (LNB) {
       // a row's GBN columns are TPR = 32 consecutive threads (one half wave): row sums by 5 xor
@@ -363,11 +382,15 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
       // issue every operand load of this thread's rows first (memory-level parallelism)
       u32x4 auxv[IT];
       f32x4 resv[IT][2];
+      if constexpr (HAS_AUX) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) auxv[it] = auxn[it];
+        if (pass + 1 < GBM / EPI_ROWS) load_aux(pass + 1);
+      }
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int m = mb + it * RPI + rsub;
         if (m < M) {
-          if (HAS_AUX) auxv[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
           const float* rp = EPI == EPI_BIAS_RESID_F32 ? P.resid + (int64_t)m * P.ldres + n
                                                       : o32 + (int64_t)m * P.ldc + n;
           if (HAS_RES) {

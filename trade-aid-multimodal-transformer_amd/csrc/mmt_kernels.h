@@ -114,6 +114,25 @@ hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s);
 // weight gradients o32 += alpha * A^T B over K rows (both operands MN-contiguous): split-K into fp32
 // slabs in `slab` (capacity slab_bytes) + one reduce pass; without room, one K pass accumulating
 hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_bytes, hipStream_t s);
+
+// Fused two-GEMM MLP (round 5; SURVEY K6 / K11: the attention out-projection Linear(C, C/2) -> tanh ->
+// Linear(C/2, C) of model.py:82-92, 102-117): per problem
+//   h   = tanh(A W0^T + b0)            (g1: A [M][K1] bf16, B = W0 [N1][K1] packed, bias b0, o16 = h out)
+//   out = epilogue(h W2^T + b2)        (g2: B = W2 [N2][N1] packed, bias b2, EPI_BIAS_RESID_F32 fields:
+//                                        resid, o32, optional o16 / dropout / next-LayerNorm lnf_*)
+// with h resident in LDS between the two products (it is still stored to g1.o16 for the backward).
+// N1 = 128 or 256, N2 = 2 N1, K1 = N2 (C = 256 or 512); hipErrorInvalidValue otherwise (the caller
+// runs the two GEMMs).
+// (at most MMT_MLP2_GROUP problems per launch: two GemmProblem arrays of 8 would pass the 4 KiB
+// kernel-argument limit; the engine launches groups of up to 8 modalities in chunks)
+#define MMT_MLP2_GROUP 4
+struct Mlp2Batch {
+  GemmProblem g1[MMT_MLP2_GROUP];
+  GemmProblem g2[MMT_MLP2_GROUP];
+  int count;
+};
+bool mmt_mlp2_ok(const Mlp2Batch& b);
+hipError_t mmt_launch_mlp2(const Mlp2Batch& b, hipStream_t s);
 // forward linear Y = X W^T on MX-fp8 operands (A = X [M][K], B = W [N][K], both K-contiguous e4m3fn
 // with E8M0 exponents per 32 K elements; K % 32 == 0) via v_mfma_scale_f32_32x32x64_f8f6f4, any
 // of the bf16 GEMM's forward epilogues; fp32 accumulation

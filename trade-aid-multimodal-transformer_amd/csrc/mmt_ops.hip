@@ -54,6 +54,27 @@ int mmt_op_gemm_wgrad(void* stream, int32_t M, int32_t N, int32_t K, const void*
   return st(e);
 }
 
+int mmt_op_mlp2(void* stream, int32_t M, int32_t C, const void* x, int32_t ldx, const void* w0, int32_t ldw0,
+                const float* b0, const void* w2, int32_t ldw2, const float* b2, void* h, int32_t ldh, const float* resid,
+                float* out, void* out16, uint32_t drop_key, uint32_t drop_thr, float drop_scale, const float* lnf_gamma,
+                const float* lnf_beta, void* lnf_y, float* lnf_mean, float* lnf_rstd) {
+  if (M < 1 || C < 2) return MMT_ERR_INVALID;
+  Mlp2Batch b{};
+  b.count = 1;
+  GemmProblem& p1 = b.g1[0];
+  p1.A = (const bf16_t*)x; p1.lda = ldx; p1.B = (const bf16_t*)w0; p1.ldb = ldw0; p1.bias = b0;
+  p1.o16 = (bf16_t*)h; p1.ldo16 = ldh; p1.alpha = 1.f; p1.M = M; p1.N = C / 2; p1.K = C;
+  GemmProblem& p2 = b.g2[0];
+  p2.A = (const bf16_t*)h; p2.lda = ldh; p2.B = (const bf16_t*)w2; p2.ldb = ldw2; p2.bias = b2;
+  p2.resid = resid; p2.ldres = C; p2.o32 = out; p2.ldc = C; p2.o16 = (bf16_t*)out16; p2.ldo16 = C;
+  p2.alpha = 1.f; p2.M = M; p2.N = C; p2.K = C / 2;
+  p2.drop_key = drop_key; p2.drop_thr = drop_thr; p2.drop_scale = drop_scale;
+  p2.lnf_gamma = lnf_gamma; p2.lnf_beta = lnf_beta; p2.lnf_y = (bf16_t*)lnf_y; p2.lnf_mean = lnf_mean;
+  p2.lnf_rstd = lnf_rstd;
+  if (!mmt_mlp2_ok(b)) return MMT_ERR_UNSUPPORTED;
+  return st(mmt_launch_mlp2(b, (hipStream_t)stream));
+}
+
 int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
                          void* y16, float* mean, float* rstd) {
   LnBatch b{};

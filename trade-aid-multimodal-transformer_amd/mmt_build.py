@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(CSRC, "build")
 LIB = os.path.join(HERE, "libmmt_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["mmt_gemm.hip", "mmt_gemm8.hip", "mmt_attn.hip", "mmt_attn2.hip", "mmt_elem.hip", "mmt_qkv2.hip", "mmt_engine.hip", "mmt_ops.hip", "mmt_batch.hip", "mmt_decode.hip"]
+SOURCES = ["mmt_gemm.hip", "mmt_gemm8.hip", "mmt_mlp2.hip", "mmt_attn.hip", "mmt_attn2.hip", "mmt_elem.hip", "mmt_qkv2.hip", "mmt_engine.hip", "mmt_ops.hip", "mmt_batch.hip", "mmt_decode.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(REPO, "include"), "-I" + CSRC,
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
 
