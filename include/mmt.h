@@ -229,6 +229,13 @@ int mmt_op_mlp2(void* stream, int32_t M, int32_t C, const void* x, int32_t ldx, 
                 const float* b0, const void* w2, int32_t ldw2, const float* b2, void* h, int32_t ldh, const float* resid,
                 float* out, void* out16, uint32_t drop_key, uint32_t drop_thr, float drop_scale, const float* lnf_gamma,
                 const float* lnf_beta, void* lnf_y, float* lnf_mean, float* lnf_rstd);
+/* its backward-data pair as ONE launch (the engine's backward path at C = 256 / 512; replaces
+ * mmt_op_gemm(dtanh_bf16) + mmt_op_gemm(store_bf16)): dh[M, C/2] = bf16(alpha (dy[M, C] W2[C, C/2]) (1 - h^2))
+ * with db0 (nullable) += its fp32 column sums, dx[M, C] = bf16(dh W0[C/2, C]); W2 / W0 are the forward
+ * weights as stored ([C][C/2] / [C/2][C], row strides ldw2 / ldw0), h the forward's saved tanh output */
+int mmt_op_mlp2_bwd(void* stream, int32_t M, int32_t C, const void* dy, int32_t lddy, const void* w2, int32_t ldw2,
+                    const void* h, int32_t ldh, float alpha, const void* w0, int32_t ldw0, void* dh, int32_t lddh,
+                    float* db0, void* dx);
 int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
                          void* y16, float* mean, float* rstd);
 int mmt_op_layernorm_bwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* mean,

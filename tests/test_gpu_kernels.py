@@ -450,6 +450,32 @@ def test_mlp2_fused(M, C, drop, lnf):
                          N1, ML.ptr(resid), ML.ptr(out), None, 0, 0, 1.0, None, None, None, None, None) == -2
 
 
+@pytest.mark.parametrize("M,C", [(1000, 256), (130, 512), (4096, 512), (65536, 512), (65536, 256)])
+def test_mlp2_bwd_fused(M, C):
+    """The out-projection's backward-data pair as one launch (mmt_op_mlp2_bwd) against torch on the same bf16
+    operands: dh = (dy W2) * (1 - h^2) within one bf16 rounding, db0 its fp32 column sums, dx = dh W0 from the
+    kernel's own bf16 dh (rel 1e-2: one more rounding)."""
+    torch.manual_seed(M + C + 1)
+    N1 = C // 2
+    dy = bf(torch.randn(M, C, device=DEV))
+    w2 = bf(torch.randn(C, N1, device=DEV) * 0.05)   # the forward's W2 [C][C/2]
+    w0 = bf(torch.randn(N1, C, device=DEV) * 0.05)   # the forward's W0 [C/2][C]
+    h = bf(torch.tanh(torch.randn(M, N1, device=DEV)))
+    dh = torch.zeros(M, N1, dtype=torch.bfloat16, device=DEV)
+    dx = torch.zeros(M, C, dtype=torch.bfloat16, device=DEV)
+    db0 = torch.full((N1,), 0.5, device=DEV)
+    alpha = 0.75
+    L = ML.lib()
+    rc = L.mmt_op_mlp2_bwd(_s(), M, C, ML.ptr(dy), C, ML.ptr(w2), N1, ML.ptr(h), N1, alpha, ML.ptr(w0), C, ML.ptr(dh),
+                           N1, ML.ptr(db0), ML.ptr(dx))
+    assert rc == 0
+    _sync()
+    dref = alpha * (dy.float() @ w2.float()) * (1 - h.float() ** 2)
+    assert rel(dh, dref) < 1e-2
+    assert rel(db0 - 0.5, dref.sum(0)) < 1e-4
+    assert rel(dx, dh.float() @ w0.float()) < 1e-2
+
+
 # --------------------------------------------------------------------------------- attention
 def _attn_ref(q, ks, vs, scale):
     # q [B,H,T,hs], ks/vs list of [B,H,T,hs]; sum over streams of causal softmax attention

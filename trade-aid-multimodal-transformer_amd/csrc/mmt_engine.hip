@@ -696,7 +696,8 @@ struct Runner {
   // the attention out-projection Linear(C, C/2) -> tanh -> Linear(C/2, C) + dropout + residual as one fused
   // launch (mmt_launch_mlp2: h stays in LDS between the products); false (nothing launched) when the
   // shape is outside the fused kernel or MMT_MLP2=0, and the caller runs the two GEMMs
-  bool mlp2(const GemmProblem* g1s, const GemmProblem* g2s, int n, const char* what) {
+  // bwd: the backward-data pair (mmt_launch_mlp2_bwd: dh = (dY W2) tanh', dx = dh W0)
+  bool mlp2(const GemmProblem* g1s, const GemmProblem* g2s, int n, const char* what, bool bwd = false) {
     static const bool on = [] {
       const char* e = getenv("MMT_MLP2");
       return e ? atoi(e) != 0 : true;
@@ -711,17 +712,17 @@ struct Runner {
       ++b.count;
     }
     for (int k = 0; k < nch; ++k)
-      if (!mmt_mlp2_ok(chunk[k])) return false;
+      if (!(bwd ? mmt_mlp2_bwd_ok(chunk[k]) : mmt_mlp2_ok(chunk[k]))) return false;
     const int id = probe_begin(what, s);
-    for (int k = 0; k < nch; ++k) ok(mmt_launch_mlp2(chunk[k], s), what);
+    for (int k = 0; k < nch; ++k) ok(bwd ? mmt_launch_mlp2_bwd(chunk[k], s) : mmt_launch_mlp2(chunk[k], s), what);
     if (id >= 0) {
       double fl = 0, by = 0;
       GemmBatch g1{}, g2{};
       g1.count = g2.count = n;
       for (int g = 0; g < n; ++g) { g1.p[g] = g1s[g]; g2.p[g] = g2s[g]; }
-      gemm_cost(g1, EPI_BIAS_TANH_BF16, &fl, &by);
-      gemm_cost(g2, EPI_BIAS_RESID_F32, &fl, &by);
-      for (int g = 0; g < n; ++g) by -= (double)g2s[g].M * g2s[g].K * 2.0;  // h is not read back
+      gemm_cost(g1, bwd ? EPI_DTANH_BF16 : EPI_BIAS_TANH_BF16, &fl, &by);
+      gemm_cost(g2, bwd ? EPI_STORE_BF16 : EPI_BIAS_RESID_F32, &fl, &by);
+      for (int g = 0; g < n; ++g) by -= (double)g2s[g].M * g2s[g].K * 2.0;  // h / dh is not read back
       probe_end(id, s, fl, by);
     }
     return true;
@@ -1433,16 +1434,22 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       dx.p[u].dbias = grads + x[i].bc0;
     }
     r.dwgemm(dw, "ca_proj2_dw");
-    r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "ca_proj2_dx");
+    GemmProblem pdx0[MAXM];
+    for (int u = 0; u < nc; ++u) {
+      const int i = cx[u];
+      pdx0[u] = gp_dx(r.W<bf16_t>(p.gpc[par][i]), ldp, wpk, x[i].C0, R);
+      pdx0[u].o16 = r.W<bf16_t>(p.gdo[i]); pdx0[u].ldo16 = C;
+    }
+    const bool fused = r.mlp2(dx.p, pdx0, nc, "ca_proj_dx", true);
+    if (!fused) r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "ca_proj2_dx");
     for (int u = 0; u < nc; ++u) {
       const int i = cx[u];
       const bf16_t* g = r.W<bf16_t>(p.gpc[par][i]);
       dw.p[u] = gp_dw(g, ldp, r.W<bf16_t>(a[i].oc), C, grads, x[i].C0, R);
-      dx.p[u] = gp_dx(g, ldp, wpk, x[i].C0, R);
-      dx.p[u].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[u].ldo16 = C;
+      dx.p[u] = pdx0[u];
     }
     r.dwgemm(dw, "ca_proj0_dw");
-    r.gemm(dx, true, false, EPI_STORE_BF16, 1, "ca_proj0_dx");
+    if (!fused) r.gemm(dx, true, false, EPI_STORE_BF16, 1, "ca_proj0_dx");
     r.flush();
     AttnBatch ab{}; ab.count = nc;
     for (int u = 0; u < nc; ++u) {
@@ -1552,15 +1559,24 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     dx.p[i].dbias = grads + x[i].bp0;
   }
   r.dwgemm(dw, "proj2_dw");
-  r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "proj2_dx");
-  for (int i = 0; i < M; ++i) {
-    const bf16_t* g = r.W<bf16_t>(p.gp[par][i]);
-    dw.p[i] = gp_dw(g, ldp, r.W<bf16_t>(a[i].o), C, grads, x[i].P0, R);
-    dx.p[i] = gp_dx(g, ldp, wpk, x[i].P0, R);
-    dx.p[i].o16 = r.W<bf16_t>(p.gdo[i]); dx.p[i].ldo16 = C;
+  {
+    // both data-gradient products in one launch where the fused kernel takes the shape (C = 256 / 512)
+    GemmProblem pdx0[MAXM];
+    for (int i = 0; i < M; ++i) {
+      const bf16_t* g = r.W<bf16_t>(p.gp[par][i]);
+      pdx0[i] = gp_dx(g, ldp, wpk, x[i].P0, R);
+      pdx0[i].o16 = r.W<bf16_t>(p.gdo[i]); pdx0[i].ldo16 = C;
+    }
+    const bool fused = r.mlp2(dx.p, pdx0, M, "proj_dx", true);
+    if (!fused) r.gemm(dx, true, false, EPI_DTANH_BF16, 1, "proj2_dx");
+    for (int i = 0; i < M; ++i) {
+      const bf16_t* g = r.W<bf16_t>(p.gp[par][i]);
+      dw.p[i] = gp_dw(g, ldp, r.W<bf16_t>(a[i].o), C, grads, x[i].P0, R);
+      dx.p[i] = pdx0[i];
+    }
+    r.dwgemm(dw, "proj0_dw");
+    if (!fused) r.gemm(dx, true, false, EPI_STORE_BF16, 1, "proj0_dx");
   }
-  r.dwgemm(dw, "proj0_dw");
-  r.gemm(dx, true, false, EPI_STORE_BF16, 1, "proj0_dx");
   r.flush();
   AttnBatch ab{}; ab.count = M;
   for (int i = 0; i < M; ++i) {

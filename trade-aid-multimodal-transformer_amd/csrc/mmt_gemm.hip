@@ -620,9 +620,17 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
     dim3 grid(mt, EPI == EPI_ATOMIC_F32 ? auto_splits<TileL>(b, splits) : std::max(1, splits), b.count);
-    // forward / backward-data / weight-gradient (slab, accumulate) products on the ping-pong kernel
+    // forward / backward-data products on the ping-pong kernel; the weight gradients (both operands
+    // MN-contiguous) only with MMT_GEMM8_DW=1: standalone 2-4 % faster, but on the side stream beside the
+    // main stream's attention backward the step measured slower (C1 attention backward 198 -> 207 us live,
+    // the *_dw family 107 -> 113 us; profiles/r5f_ab.txt)
     if constexpr (SWAP && gemm8_supports(A_KC, B_KC, EPI)) {
-      if (gemm8_on()) return mmt_launch_gemm8(b, EPI, A_KC, B_KC, grid, s);
+      static const bool dw8 = [] {
+        const char* e = getenv("MMT_GEMM8_DW");
+        return e ? atoi(e) != 0 : false;
+      }();
+      // (mmt_gemm_set_variant bit 17 forces it everywhere: the kernel tests)
+      if (gemm8_on() && (A_KC || dw8 || g_gemm8_rt == 1)) return mmt_launch_gemm8(b, EPI, A_KC, B_KC, grid, s);
     }
     const int bv = g_gemm_big_variant_rt ? g_gemm_big_variant_rt
                    : g_big_variant >= 0  ? g_big_variant

@@ -133,6 +133,12 @@ struct Mlp2Batch {
 };
 bool mmt_mlp2_ok(const Mlp2Batch& b);
 hipError_t mmt_launch_mlp2(const Mlp2Batch& b, hipStream_t s);
+// its backward-data pair in one launch: dh = alpha (dY W2) * (1 - h^2) (g1: A = dY [M][C], B = W2 [C][C/2]
+// MN-contiguous, aux = h, o16 = dh, dbias += column sums of dh (nullable)), dx = dh W0 (g2: B = W0
+// [C/2][C] MN-contiguous, o16 = dx); dh stays in LDS between the products and is stored for the W0
+// weight gradient
+bool mmt_mlp2_bwd_ok(const Mlp2Batch& b);
+hipError_t mmt_launch_mlp2_bwd(const Mlp2Batch& b, hipStream_t s);
 // forward linear Y = X W^T on MX-fp8 operands (A = X [M][K], B = W [N][K], both K-contiguous e4m3fn
 // with E8M0 exponents per 32 K elements; K % 32 == 0) via v_mfma_scale_f32_32x32x64_f8f6f4, any
 // of the bf16 GEMM's forward epilogues; fp32 accumulation

@@ -222,6 +222,249 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Backward of the same MLP (reference model.py:82-92 under autograd), the two data-gradient products in
+// one launch:
+//   dh = (dY W2) * (1 - h^2)    stage 1: dY [M][C] (the branch gradient, dropout mask applied) K-contiguous,
+//                               W2 [C][C/2] MN-contiguous (transposed LDS reads), h the forward's saved
+//                               tanh output (prefetched at kernel start), db0 += column sums of dh
+//   dx = dh W0                  stage 2: dh from the LDS image, W0 [C/2][C] MN-contiguous
+// dh also leaves for the W0 weight gradient (side stream). g1: A = dY, B = W2, aux = h, o16 = dh, dbias =
+// db0 (nullable); g2: B = W0, o16 = dx.
+// ---------------------------------------------------------------------------------------------
+template <int N1>
+__global__ __launch_bounds__(512, 1) void mlp2_bwd_kernel(Mlp2Batch batch) {
+  using CF = MlpCfg<N1>;
+  using T2 = typename CF::T2;
+  constexpr int N2 = CF::N2, BK = MLP_BK;
+  constexpr int TN1 = CF::T1::TN, TN2 = T2::TN, TM = 2;
+  constexpr int IMG_X = MLP_BM * BK * 2;
+  constexpr int PIECES1 = (MLP_BM + N1) * BK / 512 / 8;
+  __shared__ __attribute__((aligned(1024))) char lds[CF::LDS];
+  char* himg = lds + CF::RING;
+
+  const int prob = blockIdx.z;
+  const GemmProblem& P1 = batch.g1[prob];
+  const GemmProblem& P2 = batch.g2[prob];
+  const int M = __builtin_amdgcn_readfirstlane(P1.M);
+  const int ntiles = (M + MLP_BM - 1) / MLP_BM;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  if (tile >= ntiles) return;
+  const int m0 = tile * MLP_BM;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / 4, wn = wave % 4;
+  const int h = lane >> 5, r = lane & 31;
+
+  // tanh' input: h[m][n] for this lane's accumulator elements (4 consecutive columns per (i, j, g)),
+  // issued before the ring so its latency hides under stage 1
+  u32x2 hv[TN1][TM][4];
+  {
+    const bf16_t* hp = P1.aux;
+    const int ldh = P1.ldaux;
+#pragma unroll
+    for (int i = 0; i < TN1; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wm * 64 + 32 * j + r;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = wn * TN1 * 32 + 32 * i + 8 * g + 4 * h;
+          hv[i][j][g] = m < M ? *reinterpret_cast<const u32x2*>(hp + (int64_t)m * ldh + n) : u32x2{0u, 0u};
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < TN1; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) asm volatile("" : "+v"(hv[i][j][g]));  // consumed: its wait sits here
+  }
+
+  f32x16 acc1[TN1][TM];
+#pragma unroll
+  for (int i = 0; i < TN1; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc1[i][j][e] = 0.f;
+  {
+    const int K = CF::K1;
+    const int lda = __builtin_amdgcn_readfirstlane(P1.lda), ldb = __builtin_amdgcn_readfirstlane(P1.ldb);
+    const i32x4 ra = op_rsrc<true>(P1.A, lda, M, K, m0, 0);
+    const bf16_t* const Bp = P1.B;
+    constexpr int nk = CF::K1 / BK;
+    constexpr int ST = CF::S1_ST;
+    auto issue = [&](int slot, int t) {
+      char* st = lds + slot * CF::S1_STAGE;
+      issue_tile<BK, true, MLP_BM, 8>(ra, st, lda, M, K, m0, t * BK, wave, lane);
+      issue_tile<BK, false, N1, 8>(op_rsrc<false>(Bp, ldb, N1, K, 0, t * BK), st + IMG_X, ldb, N1, K, 0, t * BK, wave, lane);
+    };
+#pragma unroll
+    for (int t = 0; t < ST - 1; ++t) issue(t, t);
+    auto step = [&](int t, auto UC) {
+      constexpr int U = decltype(UC)::value;
+      wait_vm(PIECES1 * min(ST - 2, nk - 1 - t));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + ST - 1 < nk) issue((U + ST - 1) % ST, t + ST - 1);
+      const char* imgA = lds + U * CF::S1_STAGE;
+      const char* imgB = imgA + IMG_X;
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8 fa[TM], fb[TN1];
+#pragma unroll
+        for (int j = 0; j < TM; ++j) fa[j] = frag<BK, true, MLP_BM>(imgA, wm * 64 + 32 * j, s, lane);
+#pragma unroll
+        for (int i = 0; i < TN1; ++i) fb[i] = frag<BK, false, N1>(imgB, wn * TN1 * 32 + 32 * i, s, lane);
+#pragma unroll
+        for (int i = 0; i < TN1; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) acc1[i][j] = mfma32(fb[i], fa[j], acc1[i][j]);
+      }
+    };
+    int t = 0;
+    for (; t + ST <= nk; t += ST) {
+      step(t, std::integral_constant<int, 0>{});
+      step(t + 1, std::integral_constant<int, 1>{});
+      step(t + 2, std::integral_constant<int, 2>{});
+    }
+    if (t < nk) step(t, std::integral_constant<int, 0>{});
+    if (t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
+  }
+
+  constexpr int K2 = N1;
+  constexpr int nk2 = K2 / BK;
+  const int ldw0 = __builtin_amdgcn_readfirstlane(P2.ldb);
+  const bf16_t* const W0p = P2.B;
+  auto issue2 = [&](int slot, int t) {
+    issue_tile<BK, false, N2, 8>(op_rsrc<false>(W0p, ldw0, N2, K2, 0, t * BK), lds + slot * CF::S2_STAGE, ldw0, N2, K2,
+                                 0, t * BK, wave, lane);
+  };
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // the stage-1 ring is free
+  issue2(0, 0);
+
+  // stage-1 epilogue: dh = acc1 (1 - h^2) -> bf16 -> the LDS image; db0 column sums in fp32 (the two m
+  // sub-tiles, then the 32 lanes of the half: xor shuffles), one atomic per column per wave
+  {
+    float* db = P1.dbias;
+    const float alpha = P1.alpha;
+#pragma unroll
+    for (int i = 0; i < TN1; ++i) {
+      const int nb = wn * TN1 * 32 + 32 * i;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float cs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const int ml = wm * 64 + 32 * j + r;
+          float d[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t w = hv[i][j][g][e >> 1];
+            const float t = bf2f((e & 1) ? (w >> 16) : (w & 0xffff));
+            d[e] = m0 + ml < M ? alpha * acc1[i][j][4 * g + e] * (1.0f - t * t) : 0.f;
+            cs[e] += d[e];
+          }
+          *reinterpret_cast<u32x2*>(himg + h_off<CF::HPITCH>(ml, (nb >> 3) + g) + 8 * h) =
+              u32x2{pack2bf(d[0], d[1]), pack2bf(d[2], d[3])};
+        }
+        if (db) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
+            if (r == 0) atomicAdd(db + nb + 8 * g + 4 * h + e, cs[e]);
+          }
+        }
+      }
+    }
+  }
+
+  f32x16 acc2[TN2][TM];
+#pragma unroll
+  for (int i = 0; i < TN2; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc2[i][j][e] = 0.f;
+  {
+    auto step2 = [&](int t, auto UC) {
+      constexpr int U = decltype(UC)::value;
+      wait_vm(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + 1 < nk2) issue2(U ^ 1, t + 1);
+      const char* imgW = lds + U * CF::S2_STAGE;
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8 fa[TM], fb[TN2];
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const int m = wm * 64 + 32 * j + r;
+          fa[j] = *reinterpret_cast<const bf16x8*>(himg + h_off<CF::HPITCH>(m, (t * BK + 16 * s) / 8 + h));
+        }
+#pragma unroll
+        for (int i = 0; i < TN2; ++i) fb[i] = frag<BK, false, N2>(imgW, wn * TN2 * 32 + 32 * i, s, lane);
+#pragma unroll
+        for (int i = 0; i < TN2; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) acc2[i][j] = mfma32(fb[i], fa[j], acc2[i][j]);
+      }
+    };
+#pragma unroll
+    for (int t = 0; t < nk2; t += 2) {
+      step2(t, std::integral_constant<int, 0>{});
+      if (t + 1 < nk2) step2(t + 1, std::integral_constant<int, 1>{});
+    }
+  }
+
+  epilogue_swap<T2, EPI_STORE_BF16, CF::EPI_ROWS>(P2, acc2, lds, P2.o32, P2.alpha, m0, 0, tid, lane, wave);
+
+  {
+    constexpr int CPR = N1 / 8;
+    bf16_t* ho = P1.o16;
+    const int ldo = P1.ldo16;
+#pragma unroll
+    for (int q = tid; q < MLP_BM * CPR; q += 512) {
+      const int m = q / CPR, c = q % CPR;
+      if (m0 + m < M)
+        *reinterpret_cast<u32x4*>(ho + (int64_t)(m0 + m) * ldo + 8 * c) =
+            *reinterpret_cast<const u32x4*>(himg + h_off<CF::HPITCH>(m, c));
+    }
+  }
+}
+
+bool mmt_mlp2_bwd_ok(const Mlp2Batch& b) {
+  if (b.count <= 0 || b.count > MMT_MLP2_GROUP) return false;
+  const int n1 = b.g1[0].N;
+  if (n1 != 128 && n1 != 256) return false;
+  for (int g = 0; g < b.count; ++g) {
+    const GemmProblem& p1 = b.g1[g];
+    const GemmProblem& p2 = b.g2[g];
+    if (p1.N != n1 || p1.K != 2 * n1 || p2.N != 2 * n1 || p2.K != n1 || p2.M != p1.M || p1.M < 1) return false;
+    if (!p1.A || !p1.B || !p1.aux || !p1.o16 || !p2.B || !p2.o16) return false;
+    if ((p1.lda & 7) || (p1.ldb & 7) || (p2.ldb & 7) || (p1.ldo16 & 7) || (p1.ldaux & 3) || (p2.ldo16 & 7) ||
+        p1.lda < p1.K || p1.ldb < p1.N || p2.ldb < p2.N || p1.ldo16 < n1 || p1.ldaux < n1)
+      return false;
+    if (((uintptr_t)p1.A | (uintptr_t)p1.B | (uintptr_t)p2.B | (uintptr_t)p1.o16 | (uintptr_t)p2.o16) & 15) return false;
+    if (((uintptr_t)p1.aux) & 7) return false;
+    if (p2.alpha_ptr || p1.alpha_ptr || p2.alpha != 1.0f || p2.bias) return false;
+    if ((int64_t)513 * std::max(p1.lda, std::max(p1.ldb, p2.ldb)) * 2 >= ((int64_t)1 << 31)) return false;
+  }
+  return true;
+}
+
+hipError_t mmt_launch_mlp2_bwd(const Mlp2Batch& b, hipStream_t s) {
+  if (!mmt_mlp2_bwd_ok(b)) return hipErrorInvalidValue;
+  int mt = 0;
+  for (int g = 0; g < b.count; ++g) mt = std::max(mt, (b.g1[g].M + MLP_BM - 1) / MLP_BM);
+  if (b.g1[0].N == 128) hipLaunchKernelGGL(mlp2_bwd_kernel<128>, dim3(mt, 1, b.count), dim3(512), 0, s, b);
+  else hipLaunchKernelGGL(mlp2_bwd_kernel<256>, dim3(mt, 1, b.count), dim3(512), 0, s, b);
+  return hipGetLastError();
+}
+
 bool mmt_mlp2_ok(const Mlp2Batch& b) {
   if (b.count <= 0 || b.count > MMT_MLP2_GROUP) return false;
   const int n1 = b.g1[0].N;

@@ -75,6 +75,23 @@ int mmt_op_mlp2(void* stream, int32_t M, int32_t C, const void* x, int32_t ldx, 
   return st(mmt_launch_mlp2(b, (hipStream_t)stream));
 }
 
+int mmt_op_mlp2_bwd(void* stream, int32_t M, int32_t C, const void* dy, int32_t lddy, const void* w2, int32_t ldw2,
+                    const void* h, int32_t ldh, float alpha, const void* w0, int32_t ldw0, void* dh, int32_t lddh,
+                    float* db0, void* dx) {
+  if (M < 1 || C < 2) return MMT_ERR_INVALID;
+  Mlp2Batch b{};
+  b.count = 1;
+  GemmProblem& p1 = b.g1[0];
+  p1.A = (const bf16_t*)dy; p1.lda = lddy; p1.B = (const bf16_t*)w2; p1.ldb = ldw2; p1.aux = (const bf16_t*)h;
+  p1.ldaux = ldh; p1.o16 = (bf16_t*)dh; p1.ldo16 = lddh; p1.dbias = db0; p1.alpha = alpha; p1.M = M; p1.N = C / 2;
+  p1.K = C;
+  GemmProblem& p2 = b.g2[0];
+  p2.A = (const bf16_t*)dh; p2.lda = lddh; p2.B = (const bf16_t*)w0; p2.ldb = ldw0; p2.o16 = (bf16_t*)dx; p2.ldo16 = C;
+  p2.alpha = 1.f; p2.M = M; p2.N = C; p2.K = C / 2;
+  if (!mmt_mlp2_bwd_ok(b)) return MMT_ERR_UNSUPPORTED;
+  return st(mmt_launch_mlp2_bwd(b, (hipStream_t)stream));
+}
+
 int mmt_op_layernorm_fwd(void* stream, int32_t R, int32_t C, const float* x, const float* gamma, const float* beta,
                          void* y16, float* mean, float* rstd) {
   LnBatch b{};

@@ -95,6 +95,8 @@ _SIGS = {
                                    c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint32, ctypes.c_uint32, c_f32]),
     "mmt_op_mlp2": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp,
                             c_vp, c_vp, ctypes.c_uint32, ctypes.c_uint32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mmt_op_mlp2_bwd": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32, c_vp, c_i32, c_vp,
+                                c_i32, c_vp, c_vp]),
     "mmt_op_layernorm_fwd": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mmt_op_layernorm_bwd": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mmt_op_attention_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(c_vp),
