@@ -71,6 +71,37 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* lds, int stride, int dt,
   return join4(lds_tr16(lds + kb * stride + col), lds_tr16(lds + (kb + 8) * stride + col));
 }
 
+// hs-32 slice image of the backward's shared operands (round 5, as the hs-64 rings' images of
+// mmt_attn2.hip): 32-row slices of two 16-column sub-images 1152 B apart (1 KiB + 128 B pad), the two
+// 16-B halves of a row swapped when bit 3 of the row is set. Row reads (ds_read_b128, a row per lane)
+// and transposed reads (ds_read_b64_tr_b16, 4 rows x 16 columns per 16-lane group) are both
+// conflict-free; the [row][40] image of Geo<32>::RW took 2-way conflicts on every transposed read
+// (SQ_LDS_BANK_CONFLICT 0.31 / 0.25 of the dQ / dK-dV passes' LDS cycles at C1, round 4)
+constexpr int SL_SUB = 1152, SL_SLICE = 2 * SL_SUB;
+template <int HS>
+struct SliceImg {
+  static constexpr bool on = HS == 32;
+};
+// byte offset of 16-B chunk `chunk` (8 columns, 0..3) of row `row`
+__device__ __forceinline__ int sl_off(int row, int chunk) {
+  return (row >> 5) * SL_SLICE + (chunk >> 1) * SL_SUB + (row & 31) * 32 + (((chunk & 1) ^ ((row >> 3) & 1)) << 4);
+}
+// row fragment: row row0 + r of the slice at row0 (a multiple of 32), columns 16 s + 8 h .. + 7
+// (per-lane part r 32 + swapped half: one register; the slice and s are immediates / scalars)
+__device__ __forceinline__ bf16x8 sl_row(const bf16_t* img, int row0, int r, int s, int h) {
+  const int o = (row0 >> 5) * SL_SLICE + s * SL_SUB + r * 32 + ((h ^ ((r >> 3) & 1)) << 4);
+  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(img) + o);
+}
+// transposed fragment of the slice at row0 (as tr_frag: column 16 (g & 1) + 4 p of rows
+// 16 s + 4 (g >> 1) + q and + 8): the first row set has bit 3 clear, the second set, so the swap is
+// fixed per set and the per-lane parts are two registers
+__device__ __forceinline__ bf16x8 sl_tr(const bf16_t* img, int row0, int s, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int L = (g & 1) * SL_SUB + (p & 1) * 8 + (4 * (g >> 1) + q) * 32;
+  const char* b = reinterpret_cast<const char*>(img) + (row0 >> 5) * SL_SLICE + 512 * s;
+  return join4(lds_tr16(b + L + ((p >> 1) << 4)), lds_tr16(b + L + 256 + (((p >> 1) ^ 1) << 4)));
+}
+
 // accumulator registers 8s..8s+7 -> bf16 operand fragment
 __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
   const u32x4 v = {pack2bf(a[8 * s], a[8 * s + 1]), pack2bf(a[8 * s + 2], a[8 * s + 3]),
@@ -141,6 +172,18 @@ struct Stager {
       const int cc = isb ? c - HALF : c;
       const int row = cc / CH, col = (cc % CH) * 8;
       *reinterpret_cast<u32x4*>(isb ? lb + row * sb + col : la + row * sa + col) = v[u];
+    }
+  }
+  // both operands as slice images (SliceImg; HS == 32: 4 chunks per row)
+  __device__ __forceinline__ void store_slices(bf16_t* la, bf16_t* lb, int tid) const {
+    constexpr int CH = Geo<HS>::CH, HALF = Chunk<HS>::HALF;
+    static_assert(CH == 4, "slice images hold 32 columns");
+#pragma unroll
+    for (int u = 0; u < Chunk<HS>::NSTG; ++u) {
+      const int c = tid + 256 * u;
+      const bool isb = c >= HALF;
+      const int cc = isb ? c - HALF : c;
+      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(isb ? lb : la) + sl_off(cc / CH, cc % CH)) = v[u];
     }
   }
 };
@@ -542,12 +585,13 @@ __device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, cons
   zero16(sa);
   zero16(pa);
   if (NQ == 2) { zero16(sb); zero16(pb); }
+  constexpr bool SL = SliceImg<HS>::on;
   if (NQ == 2) {
     bf16x8 kf[G::NKS], vf[G::NKS];
 #pragma unroll
     for (int s = 0; s < G::NKS; ++s) {
-      kf[s] = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
-      vf[s] = *reinterpret_cast<const bf16x8*>(vs + (kl + r) * G::RW + 16 * s + 8 * h);
+      kf[s] = SL ? sl_row(ks, kl, r, s, h) : *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
+      vf[s] = SL ? sl_row(vs, kl, r, s, h) : *reinterpret_cast<const bf16x8*>(vs + (kl + r) * G::RW + 16 * s + 8 * h);
     }
 #pragma unroll
     for (int s = 0; s < G::NKS; ++s) {
@@ -559,8 +603,8 @@ __device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, cons
   } else {  // register-lean order (hs >= 48)
 #pragma unroll
     for (int s = 0; s < G::NKS; ++s) {
-      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
-      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vs + (kl + r) * G::RW + 16 * s + 8 * h);
+      const bf16x8 kf = SL ? sl_row(ks, kl, r, s, h) : *reinterpret_cast<const bf16x8*>(ks + (kl + r) * G::RW + 16 * s + 8 * h);
+      const bf16x8 vf = SL ? sl_row(vs, kl, r, s, h) : *reinterpret_cast<const bf16x8*>(vs + (kl + r) * G::RW + 16 * s + 8 * h);
       sa = mfma32(kf, a.qf[s], sa);
       pa = mfma32(vf, a.dof[s], pa);
     }
@@ -572,7 +616,7 @@ __device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, cons
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int dt = 0; dt < G::ND; ++dt) kt[s][dt] = tr_frag(kts + kl * kts_ld, kts_ld, dt, s, lane);
+      for (int dt = 0; dt < G::ND; ++dt) kt[s][dt] = SL ? sl_tr(kts, kl, s, lane) : tr_frag(kts + kl * kts_ld, kts_ld, dt, s, lane);
     dq_ds<HS, DA, DROP>(sa, pa, a, k0, c2, dsc, wa, h, dfa);
     dq_ds<HS, DB, DROP>(sb, pb, b, k0, c2, dsc, wb, h, dfb);
 #pragma unroll
@@ -587,7 +631,8 @@ __device__ __forceinline__ void dq_step(const bf16_t* ks, const bf16_t* vs, cons
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int dt = 0; dt < G::ND; ++dt) a.dq[dt] = mfma32(tr_frag(kts + kl * kts_ld, kts_ld, dt, s, lane), dfa[s], a.dq[dt]);
+      for (int dt = 0; dt < G::ND; ++dt)
+        a.dq[dt] = mfma32(SL ? sl_tr(kts, kl, s, lane) : tr_frag(kts + kl * kts_ld, kts_ld, dt, s, lane), dfa[s], a.dq[dt]);
   }
 }
 
@@ -639,7 +684,8 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
     for (int rr = 0; rr < NR; ++rr) {
       st.load(P.k[jj] + head * P.kv_hstride, P.kv_ld, P.v[jj] + head * P.kv_hstride, P.kv_ld, rowbase,
               cc * ROWS + rr * SR, T, tid);
-      st.store(ks + rr * SR * G::RW, G::RW, vs + rr * SR * G::RW, G::RW, tid);
+      if constexpr (SliceImg<HS>::on) st.store_slices(ks + rr * SR * G::RW, vs + rr * SR * G::RW, tid);
+      else st.store(ks + rr * SR * G::RW, G::RW, vs + rr * SR * G::RW, G::RW, tid);
     }
     if (DROP) mst.store(msk, tid);
   };
@@ -780,10 +826,11 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
   // S and dP, then the transposed Q / dO fragments for dK / dV behind the softmax VALU): the
   // compiler then waits on counted lgkmcnt instead of a read -> wait -> MFMA chain per fragment
   bf16x8 qr[G::NKS], dr[G::NKS];
+  constexpr bool SL = SliceImg<HS>::on;
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
-    qr[s] = *reinterpret_cast<const bf16x8*>(qs + (ql + r) * G::RW + 16 * s + 8 * h);
-    dr[s] = *reinterpret_cast<const bf16x8*>(dos + (ql + r) * G::RW + 16 * s + 8 * h);
+    qr[s] = SL ? sl_row(qs, ql, r, s, h) : *reinterpret_cast<const bf16x8*>(qs + (ql + r) * G::RW + 16 * s + 8 * h);
+    dr[s] = SL ? sl_row(dos, ql, r, s, h) : *reinterpret_cast<const bf16x8*>(dos + (ql + r) * G::RW + 16 * s + 8 * h);
   }
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s) {
@@ -795,8 +842,8 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
   for (int s = 0; s < 2; ++s)
 #pragma unroll
     for (int dt = 0; dt < G::ND; ++dt) {
-      dot[s][dt] = tr_frag(dos + ql * G::RW, G::RW, dt, s, lane);
-      qtr[s][dt] = tr_frag(qs + ql * G::RW, G::RW, dt, s, lane);
+      dot[s][dt] = SL ? sl_tr(dos, ql, s, lane) : tr_frag(dos + ql * G::RW, G::RW, dt, s, lane);
+      qtr[s][dt] = SL ? sl_tr(qs, ql, s, lane) : tr_frag(qs + ql * G::RW, G::RW, dt, s, lane);
     }
   f32x4 l4[4], d4[4];
 #pragma unroll
@@ -916,7 +963,8 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
     }
   };
   auto store = [&]() {
-    st.store(qs, G::RW, dos, G::RW, tid);
+    if constexpr (SliceImg<HS>::on) st.store_slices(qs, dos, tid);
+    else st.store(qs, G::RW, dos, G::RW, tid);
     if (DROP) mst.store(msk, tid);
 #pragma unroll
     for (int u = 0; u < NSL; ++u) {

@@ -346,7 +346,11 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_kernel(Mlp2Batch batch) {
   issue2(0, 0);
 
   // stage-1 epilogue: dh = acc1 (1 - h^2) -> bf16 -> the LDS image; db0 column sums in fp32 (the two m
-  // sub-tiles, then the 32 lanes of the half: xor shuffles), one atomic per column per wave
+  // sub-tiles, then the 32 lanes of the half: xor shuffles; the two m-halves of the block through LDS
+  // beyond the stage-2 ring, then one coalesced atomic per column per block: per-wave atomics onto the
+  // same N1 addresses from every block serialised at the memory side)
+  float* red = reinterpret_cast<float*>(lds + CF::S2_ST * CF::S2_STAGE);
+  static_assert(CF::S2_ST * CF::S2_STAGE + 2 * N1 * 4 <= CF::RING, "column-sum area inside the ring");
   {
     float* db = P1.dbias;
     const float alpha = P1.alpha;
@@ -375,8 +379,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_kernel(Mlp2Batch batch) {
           for (int e = 0; e < 4; ++e) {
 #pragma unroll
             for (int o = 1; o < 32; o <<= 1) cs[e] += __shfl_xor(cs[e], o, 64);
-            if (r == 0) atomicAdd(db + nb + 8 * g + 4 * h + e, cs[e]);
           }
+          if (r == 0) *reinterpret_cast<f32x4*>(red + wm * N1 + nb + 8 * g + 4 * h) = f32x4{cs[0], cs[1], cs[2], cs[3]};
         }
       }
     }
@@ -420,6 +424,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_kernel(Mlp2Batch batch) {
     }
   }
 
+  if (P1.dbias && tid < N1) atomicAdd(P1.dbias + tid, red[tid] + red[N1 + tid]);  // (published by the stage-2 barriers)
   epilogue_swap<T2, EPI_STORE_BF16, CF::EPI_ROWS>(P2, acc2, lds, P2.o32, P2.alpha, m0, 0, tid, lane, wave);
 
   {
