@@ -698,11 +698,20 @@ struct Runner {
   // shape is outside the fused kernel or MMT_MLP2=0, and the caller runs the two GEMMs
   // bwd: the backward-data pair (mmt_launch_mlp2_bwd: dh = (dY W2) tanh', dx = dh W0)
   bool mlp2(const GemmProblem* g1s, const GemmProblem* g2s, int n, const char* what, bool bwd = false) {
+    // forward fused by default: C1 8.80 -> 8.70 ms/step (standalone 45.9 -> 43.0 us at C1, 119.6 -> 112.8 us
+    // at the target); the backward pair stays two GEMMs by default (MMT_MLP2_BWD=1 fuses it): fused it
+    // measured 33.5 / 80.6 us against 29.3 / 61.6 us for the pair (C1 / target, tools/mlp2_bench.py) -- one
+    // block per CU at 136 KiB of LDS with both B operands read transposed cannot hide what the two 2-3
+    // blocks-per-CU GEMMs overlap (profiles/r5h_*.txt)
     static const bool on = [] {
       const char* e = getenv("MMT_MLP2");
       return e ? atoi(e) != 0 : true;
     }();
-    if (rc != MMT_OK || !on || n < 1) return false;
+    static const bool on_bwd = [] {
+      const char* e = getenv("MMT_MLP2_BWD");
+      return e ? atoi(e) != 0 : false;
+    }();
+    if (rc != MMT_OK || !on || (bwd && !on_bwd) || n < 1) return false;
     Mlp2Batch chunk[(MMT_MAX_GROUP + MMT_MLP2_GROUP - 1) / MMT_MLP2_GROUP] = {};
     const int nch = (n + MMT_MLP2_GROUP - 1) / MMT_MLP2_GROUP;
     for (int i = 0; i < n; ++i) {

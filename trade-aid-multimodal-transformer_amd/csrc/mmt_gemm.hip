@@ -599,18 +599,31 @@ constexpr bool gemm8_supports(bool akc, bool bkc, int epi) {
   return (akc && bkc && (epi == EPI_STORE_BF16 || epi == EPI_BIAS_TANH_BF16 || epi == EPI_BIAS_RELU_BF16 ||
                          epi == EPI_BIAS_RESID_F32 || epi == EPI_STORE_F32 || epi == EPI_ACC_F32)) ||
          (akc && !bkc && (epi == EPI_STORE_BF16 || epi == EPI_DTANH_BF16 || epi == EPI_DRELU_BF16 ||
-                          epi == EPI_STORE_F32 || epi == EPI_ACC_F32)) ||
+                          epi == EPI_STORE_F32 || epi == EPI_ACC_F32 || epi == EPI_LN_BWD_F32)) ||
          (!akc && !bkc && (epi == EPI_STORE_F32 || epi == EPI_ACC_F32));
 }
 
+static bool gemm8_ln_on();
+
 static bool gemm8_on() {
   // default on (round 5): C4 355 -> 350 ms/step, C3 153.3 -> 152.4, target / C1 neutral (same-box A/B,
-  // profiles/r5e_ab.txt); MMT_GEMM8=0 restores the 2-stage 256 x 256 ring everywhere
+  // profiles/r5_gemm8_mlp2_ab.txt); MMT_GEMM8=0 restores the 2-stage 256 x 256 ring everywhere
   static const int env = [] {
     const char* e = getenv("MMT_GEMM8");
     return e ? atoi(e) : 1;
   }();
   return g_gemm8_rt >= 0 ? g_gemm8_rt != 0 : env != 0;
+}
+
+// the row-wide (N = 256) LayerNorm-fused launches on the ping-pong kernel: MMT_GEMM8_LN=0 keeps them on the
+// 2-stage ring (variant bit 17 / 18 still force the ping-pong kernel on / off for the tests)
+static bool gemm8_ln_on() {
+  static const bool env = [] {
+    const char* e = getenv("MMT_GEMM8_LN");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (g_gemm8_rt >= 0) return g_gemm8_rt == 1;
+  return gemm8_on() && env;
 }
 
 template <bool A_KC, bool B_KC, bool SWAP, int EPI>
@@ -623,7 +636,7 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     // forward / backward-data products on the ping-pong kernel; the weight gradients (both operands
     // MN-contiguous) only with MMT_GEMM8_DW=1: standalone 2-4 % faster, but on the side stream beside the
     // main stream's attention backward the step measured slower (C1 attention backward 198 -> 207 us live,
-    // the *_dw family 107 -> 113 us; profiles/r5f_ab.txt)
+    // the *_dw family 107 -> 113 us; profiles/r5_gemm8_mlp2_ab.txt)
     if constexpr (SWAP && gemm8_supports(A_KC, B_KC, EPI)) {
       static const bool dw8 = [] {
         const char* e = getenv("MMT_GEMM8_DW");
@@ -928,6 +941,8 @@ hipError_t mmt_launch_gemm_resid_ln(const GemmBatch& b, hipStream_t s) {
   } else {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
+    // the ping-pong kernel takes the 256 x 256 row-wide tile too (same epilogue, LayerNorm included)
+    if (gemm8_ln_on()) return mmt_launch_gemm8(b, EPI_BIAS_RESID_F32, true, true, dim3(mt, 1, b.count), s);
     launch_v<TileL, 64, 2, true, true, true, EPI_BIAS_RESID_F32>(b, dim3(mt, 1, b.count), s);
   }
   return hipGetLastError();
@@ -958,6 +973,7 @@ hipError_t mmt_launch_gemm_ln_bwd(const GemmBatch& b, hipStream_t s) {
   } else {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
+    if (gemm8_ln_on()) return mmt_launch_gemm8(b, EPI_LN_BWD_F32, true, false, dim3(mt, 1, b.count), s);
     launch_v<TileL, 64, 2, true, false, true, EPI_LN_BWD_F32>(b, dim3(mt, 1, b.count), s);
   }
   return hipGetLastError();

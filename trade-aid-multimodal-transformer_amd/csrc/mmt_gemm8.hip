@@ -245,6 +245,7 @@ hipError_t mmt_launch_gemm8(const GemmBatch& b, int epi, bool a_kc, bool b_kc, d
   }
   if (a_kc) {
     switch (epi) {
+      case EPI_LN_BWD_F32: return launch8<EPI_LN_BWD_F32, true, false>(b, grid, s);
       case EPI_STORE_BF16: return launch8<EPI_STORE_BF16, true, false>(b, grid, s);
       case EPI_DTANH_BF16: return launch8<EPI_DTANH_BF16, true, false>(b, grid, s);
       case EPI_DRELU_BF16: return launch8<EPI_DRELU_BF16, true, false>(b, grid, s);
