@@ -570,15 +570,16 @@ def test_attention_fwd_bwd(B, T, H, hs, ns):
         assert rel(heads(got_v[j]), vf[j].grad) < 2e-2, (j, rel(heads(got_v[j]), vf[j].grad))
 
 
-@pytest.mark.parametrize("ring", [0, 1, 3, 7, 8, 15])
+@pytest.mark.parametrize("ring", [0, 1, 3, 7, 8, 15, 47])
 @pytest.mark.parametrize("B,T,H,ns", [(2, 100, 2, 1), (1, 520, 2, 2), (1, 1024, 1, 1), (2, 300, 2, 3), (1, 33, 2, 1),
-                                      (3, 64, 2, 7)])
+                                      (3, 64, 2, 7), (2, 512, 2, 1), (1, 500, 3, 1), (3, 7, 2, 1), (1, 96, 1, 1)])
 def test_attention_hs64_backward_variants(B, T, H, ns, ring):
     """Every hs-64 attention variant (mmt_attn_set_ring: 0 the chunked dQ and dK/dV passes, 1 the
     slice-streamed dK/dV ring, 3 both rings with two query tiles per wave in the dQ ring, 7 that with
     the dK/dV ring at 3 waves per SIMD; bit 3 the slice-streamed forward: 8 with the chunked
-    backward, 15 everything on the rings) against the same torch reference, ragged T and
-    multi-stream (up to 7 KV streams) included."""
+    backward, 15 everything on the rings; bit 5 the one-pass backward where T <= 512 and one KV
+    stream: 47) against the same torch reference, ragged T and multi-stream (up to 7 KV streams)
+    included."""
     L = ML.lib()
     old = L.mmt_attn_set_ring(ring)
     try:

@@ -8,10 +8,13 @@ cancellation-heavy value-path / tiny-head grads carry ~5-15 % bf16 noise),
 params after AdamW steps close to the reference's (the update of a step is ~lr, compared with
 an absolute bound of 0.1*lr + bf16 slack).
 """
+import ctypes
+
 import pytest
 import torch
 
 import config_utils
+import mmt_lib as ML
 from golden_io import MODEL_FIXTURES, model_fixture
 
 pytestmark = pytest.mark.gpu
@@ -123,6 +126,21 @@ def test_dropout_step_matches_oracle_masks(name, p):
         lg, _ = m([t.cuda() for t in idx], [t.cuda() for t in tgt])
     for i in range(cfg.M):
         assert rel(lg[i], torch.from_numpy(z[f"logits.{i}"])) < 2e-2, i
+
+
+@pytest.mark.parametrize("C,H,T,cross,p", [(128, 2, 160, [False, True], 0.1), (128, 2, 300, [True, False], 0.2),
+                                             (128, 2, 512, [False, False], 0.1)])
+def test_dropout_fused_hs64_backward_matches_oracle(C, H, T, cross, p):
+    """The one-pass hs-64 attention backward (mmt_attn_set_ring bit 5; self-attention at T <= 512)
+    under dropout: the keep-bit records it reads per (query tile, key tiles 0..qt) against the
+    oracle's hash masks, as the multichunk test below does for the two-pass kernels."""
+    L = ML.lib()
+    L.mmt_attn_set_ring.restype = ctypes.c_int
+    old = L.mmt_attn_set_ring(47)
+    try:
+        test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p)
+    finally:
+        L.mmt_attn_set_ring(old)
 
 
 @pytest.mark.parametrize("C,H,T,cross,p", [(64, 2, 288, [True, False], 0.2), (128, 2, 160, [False, True], 0.1),

@@ -22,6 +22,16 @@ SHAPES = [
     ("c4_ffn0", 65536, 4096, 1024, "nt"),
     ("sq4k", 4096, 4096, 4096, "nt"),
     ("sq8k", 8192, 8192, 8192, "nt"),
+    # weight gradients dW[M,N] = dY[K,M]^T X[K,N] (K = B*T = 16,384 rows per modality), 4 modalities
+    # batched as the grouped launches are ("tn", bmm over 4)
+    ("tgt_ffn0_dw", 2048, 512, 16384, "tn4"),
+    ("tgt_ffn2_dw", 512, 2048, 16384, "tn4"),
+    ("tgt_qkv1_dw", 768, 512, 16384, "tn4"),
+    ("tgt_proj0_dw", 256, 512, 16384, "tn4"),
+    ("tgt_proj2_dw", 512, 256, 16384, "tn4"),
+    ("c1_ffn0_dw", 1024, 256, 16384, "tn4"),
+    ("c1_ffn2_dw", 256, 1024, 16384, "tn4"),
+    ("c4_ffn0_dw", 4096, 1024, 16384, "tn1"),
 ]
 
 
@@ -31,10 +41,18 @@ def main():
     args = ap.parse_args()
     dev = "cuda"
     for name, M, N, K, tr in SHAPES:
-        a = torch.randn(M, K, device=dev).to(torch.bfloat16)
-        w = torch.randn(N, K, device=dev).to(torch.bfloat16) if tr == "nt" else torch.randn(K, N, device=dev).to(torch.bfloat16)
+        nb = 1
+        if tr.startswith("tn"):
+            nb = int(tr[2:])
+            a = torch.randn(nb, K, M, device=dev).to(torch.bfloat16)
+            w = torch.randn(nb, K, N, device=dev).to(torch.bfloat16)
+        else:
+            a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            w = torch.randn(N, K, device=dev).to(torch.bfloat16) if tr == "nt" else torch.randn(K, N, device=dev).to(torch.bfloat16)
 
         def call():
+            if tr.startswith("tn"):
+                return torch.bmm(a.transpose(1, 2), w)
             return a @ w.t() if tr == "nt" else a @ w
 
         for _ in range(3):
@@ -47,7 +65,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / args.reps * 1e3
-        tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+        tf = 2.0 * nb * M * N * K / (us * 1e-6) / 1e12
         print(f"hipblaslt {name:14s} {M}x{N}x{K} {tr}: {us:8.1f} us {tf:7.1f} TF/s ({tf / 2500 * 100:5.1f} % of 2.5 PF)",
               flush=True)
 

@@ -1049,7 +1049,8 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
 }
 
 // attention variant knob (bit 0: the slice-streamed hs-64 dK/dV pass, bit 1: its dQ pass, bit 2: the
-// dK/dV pass at 3 waves per SIMD, bit 3: the slice-streamed hs-64 forward): MMT_ATTN_RING, or
+// dK/dV pass at 3 waves per SIMD, bit 3: the slice-streamed hs-64 forward, bit 5: the one-pass hs-64
+// backward at T <= 512 with one KV stream): MMT_ATTN_RING, or
 // mmt_attn_set_ring() for in-process A/B
 static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
@@ -1098,6 +1099,8 @@ static hipError_t attn_launch(const AttnBatch& bt, int B, int T, int H, float sc
     // hs 64: the slice-streamed kernels (mmt_attn2.hip): bit 1 of the knob the dQ pass, bit 0 the
     // dK/dV pass; MMT_ATTN_RING=0 (or mmt_attn_set_ring(0)) keeps the chunked ones
     const bool ring = HS == 64 && ring64_fits(bt, T);
+    // knob bit 5: dQ, dK, dV in one pass (mmt_attn2.hip) for T <= 512 and one KV stream
+    if (ring && (g_attn_ring & 32) && T <= 512 && ns == 1) return mmt_attn_bwd_fused64(bt, B, T, H, scale, drop, s);
     if (ring && (g_attn_ring & 2)) {
       const hipError_t e = mmt_attn_bwd_dq_ring64(bt, B, T, H, scale, drop, s);
       if (e != hipSuccess) return e;  // (hipGetLastError cleared it: report it here)

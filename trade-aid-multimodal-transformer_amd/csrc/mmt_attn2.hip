@@ -786,6 +786,353 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ring64x2(AttnBatch batch, int
   }
 }
 
+// =============================================================================================
+// One-pass backward at hs 64 for T <= 512 and one KV stream (the target shape's self-attention):
+// grid (B*H, 1, problems), one workgroup per (batch, head) owns ALL nt <= 16 key tiles, so dQ needs
+// no sum across workgroups and S / dP are computed once (the two-pass form recomputes both in its
+// dQ pass: 7 products per tile pair instead of 5). Wave w owns key tiles w, 7-w, 8+w, 15-w (every
+// causal walk 17 tile pairs long at nt = 16), their V rows and dK / dV accumulators in registers
+// (256 accumulator registers at one wave per SIMD), and walks the query slices 0 .. nt-1:
+//   * K of the whole sequence sits in LDS as slice images (read by rows for S, transposed for dQ);
+//   * each query slice (Q, dO, O images, the LSE row, the keep-bit records of key tiles 0..qt)
+//     streams through an LDS-DMA ring S - 1 slices ahead, one barrier per slice;
+//   * per tile: S = Q K^T, dP = dO V^T (keys on lanes), P, dS; dV += (Z P)^T dO, dK += dS^T Q;
+//     dS crosses a wave-private LDS transpose image once and dQ_w += dS K runs on MFMA;
+//   * each wave's dQ partial (its tiles of the slice, summed on MFMA) goes to its fp32 LDS tile; after
+//     a second barrier each wave sums 8 rows over the four tiles, scales, converts and stores them
+//     (LDS float atomics instead measured 5.8x slower for the whole kernel: ds_add_f32 serialises);
+//   * D = rowsum(dO * O) comes from the slice's O image (every wave computes the slice's 32 rows).
+// Registers: dK / dV 256 (accumulator registers), V 64, the slice's Q / dO row fragments 32, dQ partial 32.
+// =============================================================================================
+template <bool DROP, int S>
+__global__ __launch_bounds__(256, 1) void attn_bwd_fused64(AttnBatch batch, int T, int H, float scale) {
+  constexpr int NKS = 4, ND = 2, NT = 16;
+  static_assert(S >= 2 && 4 * (S - 2) <= 16, "ring slots: S - 1 slices in flight");
+  constexpr int KIMG = NT * IMG64;  // K of the sequence, 16 slice images
+  constexpr int OFF_DO = IMG64, OFF_O = 2 * IMG64, OFF_L = 3 * IMG64, OFF_M = OFF_L + 256;
+  constexpr int SLOT = OFF_M + (DROP ? NT * 128 : 0);
+  // per-wave fp32 dQ partials of the slice [32 q][64 d]; the first 2 KiB of a wave's partial hold its
+  // dS transpose image ([32 keys][32 q] bf16) while its tiles run
+  constexpr int OFF_DQ = KIMG + S * SLOT;
+  constexpr int OFF_DT = OFF_DQ + 4 * 8192;  // per-wave D of the slice's rows
+  constexpr int EPW = 40;                    // epilogue transpose row stride (bf16)
+  static_assert(4 * 2 * 32 * EPW * 2 <= S * SLOT, "epilogue transposes alias the ring");
+  __shared__ __attribute__((aligned(1024))) char lds[OFF_DT + 4 * 128];
+  const AttnProblem& P = batch.p[blockIdx.z];
+  const int nt = (T + 31) / 32;
+  const int bh = blockIdx.x;
+  const int b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t rowbase = (int64_t)b * T;
+  const float c2 = scale * kLog2e2;
+  const bool ragged = (T & 31) != 0;
+  const int kts[4] = {w, 7 - w, 8 + w, 15 - w};
+
+  // V rows of the wave's key tiles (keys on lanes: the B operands of dP)
+  bf16x8 vf[4][NKS];
+  {
+    u32x4 vr[4][NKS];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int tk = kts[t] * 32 + r;
+      const bool ok = kts[t] < nt && tk < T;
+      const bf16_t* vp = P.v[0] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        vr[t][s] = ok ? *reinterpret_cast<const u32x4*>(vp + 16 * s + 8 * h) : z;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        asm volatile("" : "+v"(vr[t][s]));  // waited for here, ahead of the DMA prologue
+        vf[t][s] = __builtin_bit_cast(bf16x8, vr[t][s]);
+      }
+  }
+  f32x16 dk[4][ND], dv[4][ND];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      zero16(dk[t][dt]);
+      zero16(dv[t][dt]);
+      asm volatile("" : "+a"(dk[t][dt]));
+      asm volatile("" : "+a"(dv[t][dt]));
+    }
+
+  const i32x4 rk = make_rsrc(P.k[0] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+  const i32x4 rl = make_rsrc(P.lse[0] + (int64_t)bh * T, (int64_t)T * 4);
+  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+  const i32x4 rm = make_rsrc(DROP ? P.dmask[0] + (int64_t)bh * ntri * 32 : P.dmask[0], ntri * 128);
+  const int prow = lane >> 1;
+  const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
+  // K of the sequence (wave w: key tiles w, w+4, w+8, w+12), the oldest pieces of every wave
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int kt = (u >> 2) * 4 + w, cb = u & 3;
+    if (kt < nt) {
+      const int grow = kt * 32 + prow;
+      const int voff = grow < T ? (grow * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
+      dma16(rk, __builtin_amdgcn_readfirstlane(lds_u32(lds + kt * IMG64 + cb * SUB)), voff);
+    }
+  }
+  // slice pieces per wave: 3 of the 12 Q / dO / O sub-images, the LSE row (wave 0), the keep-bit
+  // records of key tiles 8m .. 8m+7 (wave 1 + m)
+  const int per = 3 + (w == 0 ? 1 : 0) + (DROP && (w == 1 || w == 2) ? 1 : 0);
+  auto issue = [&](int slot, int qt) {
+    char* sb = lds + KIMG + slot * SLOT;
+    const int grow = qt * 32 + prow;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int piece = 3 * w + u;
+      const int op = piece >> 2, cb = piece & 3;
+      // (the operand is wave-uniform: its descriptor is built here, a select of three descriptors
+      // went through a scratch array)
+      const int ld = op == 0 ? P.q_ld : op == 1 ? P.dout_ld : P.o_ld;
+      const bf16_t* base = op == 0 ? P.q : op == 1 ? P.dout : P.o;
+      const i32x4 rs = make_rsrc(base + rowbase * ld + head * 64, (int64_t)T * ld * 2);
+      const int voff = grow < T ? (grow * ld + cb * 16 + pcol) * 2 : OOB;
+      dma16(rs, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * IMG64 + cb * SUB)), voff);
+    }
+    if (w == 0) {
+      const int voff = (lane < 32 && qt * 32 + lane < T) ? (qt * 32 + lane) * 4 : OOB;
+      dma4(rl, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_L)), voff);
+    }
+    if (DROP && (w == 1 || w == 2)) {
+      const int rec = 8 * (w - 1) + (lane >> 3);
+      const int voff = rec <= qt ? (qt * (qt + 1) / 2 + rec) * 128 + (lane & 7) * 16 : OOB;
+      dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M + (w - 1) * 1024)), voff);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nt) issue(i, i);
+
+  const int o_row = img_off(r, 0, h);
+  const int g = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+  const int o_tr0 = img_off(4 * (g >> 1) + qq, g & 1, p >> 1) + 8 * (p & 1);
+  const int o_tr1 = img_off(8 + 4 * (g >> 1) + qq, g & 1, p >> 1) + 8 * (p & 1);
+  const int o_mk = key_dword(r) * 4;
+  // dS transpose image ([key][q], 64-B rows, 8-B chunk c of row k stored at chunk c ^ ((k >> 1) & 7)):
+  // lane (r, h) writes chunk 2 gg + h of row r (its dS of queries 8 gg + 4 h .. + 3); the A operand
+  // of dQ (queries on lanes) comes back with the k order of the K^T fragments below (rows
+  // 16 s + 4 h + qq and + 8, chunks 4 (g & 1) + p): both read kinds conflict-free
+  char* dsi = lds + OFF_DQ + w * 8192;
+  auto dsw = [&](int gg) { return r * 64 + (((2 * gg + h) ^ ((r >> 1) & 7)) << 3); };
+  const int ra0 = 4 * (g >> 1) + qq, ra1 = ra0 + 8;
+  const int o_da0 = ra0 * 64 + (((4 * (g & 1) + p) ^ ((ra0 >> 1) & 7)) << 3);
+  const int o_da1 = ra1 * 64 + (((4 * (g & 1) + p) ^ ((ra1 >> 1) & 7)) << 3);
+  float* dtab = reinterpret_cast<float*>(lds + OFF_DT) + w * 32;
+  const float dsc = DROP ? P.drop_scale : 1.f;
+  // element e of a tile accumulator is query row (e & 3) + 8 (e >> 2) + 4 h of the tile, key r:
+  // bit e of m_diag keeps the diagonal tile's causal half (key <= query), bit e of m_rows the rows
+  // of a ragged last query tile that lie before T (its keys past T then lie above the diagonal)
+  uint32_t m_diag = 0, m_rows = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+    m_diag |= (uint32_t)(r <= row) << e;
+    m_rows |= (uint32_t)((nt - 1) * 32 + row < T) << e;
+  }
+
+  // one key tile of this wave against the slice's query tile (mk: the elements kept by the mask)
+  // (the transposed Q / dO fragments and the LSE / D rows are read per tile: held across the slice
+  // they pushed the wave past 512 registers)
+  auto tile = [&](const char* sb, int qt, int kt, f32x16 (&dkt)[ND], f32x16 (&dvt)[ND], const bf16x8 (&vft)[NKS],
+                  const bf16x8 (&qr)[NKS], const bf16x8 (&dr)[NKS], f32x16 (&dqp)[ND], uint32_t mk) {
+    const char* ki = lds + kt * IMG64;
+    const uint32_t mw = DROP ? *reinterpret_cast<const uint32_t*>(sb + OFF_M + kt * 128 + o_mk) >> (4 * h) : 0u;
+    bf16x8 kf[NKS];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(ki + o_row + s * SUB);
+    f32x16 sacc, dpacc;
+    zero16(sacc);
+    zero16(dpacc);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      sacc = mfma32(qr[s], kf[s], sacc);     // S[q][key]
+      dpacc = mfma32(dr[s], vft[s], dpacc);  // dP[q][key]
+    }
+    uint32_t pp[8], dd[8];
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(sb + OFF_L + (8 * gg + 4 * h) * 4);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(dtab + 8 * gg + 4 * h);
+#pragma unroll
+      for (int e4 = 0; e4 < 4; e4 += 2) {
+        float pm[2], ds[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int e = 4 * gg + e4 + u;
+          float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[e], c2, -l4[e4 + u]));
+          pv = keep_f(pv, __builtin_amdgcn_sbfe((int)mk, e, 1));
+          float dp = dpacc[e];
+          if (DROP) {
+            const int kbit = __builtin_amdgcn_sbfe((int)mw, 8 * gg + e4 + u, 1);
+            pm[u] = keep_f(pv, kbit);
+            dp = keep_f(dp, kbit);
+          } else {
+            pm[u] = pv;
+          }
+          ds[u] = pv * __builtin_fmaf(dp, dsc, -d4[e4 + u]);
+        }
+        pp[2 * gg + e4 / 2] = pack2bf(pm[0], pm[1]);
+        dd[2 * gg + e4 / 2] = pack2bf(ds[0], ds[1]);
+      }
+    }
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) *reinterpret_cast<u32x2*>(dsi + dsw(gg)) = u32x2{dd[2 * gg], dd[2 * gg + 1]};
+    bf16x8 qtr[2][ND], dot[2][ND];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        dot[s][dt] = join4(lds_tr16(sb + OFF_DO + o_tr0 + 512 * s + 2 * SUB * dt),
+                           lds_tr16(sb + OFF_DO + o_tr1 + 512 * s + 2 * SUB * dt));
+        qtr[s][dt] = join4(lds_tr16(sb + o_tr0 + 512 * s + 2 * SUB * dt), lds_tr16(sb + o_tr1 + 512 * s + 2 * SUB * dt));
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, u32x4{pp[4 * s], pp[4 * s + 1], pp[4 * s + 2], pp[4 * s + 3]});
+      const bf16x8 df = __builtin_bit_cast(bf16x8, u32x4{dd[4 * s], dd[4 * s + 1], dd[4 * s + 2], dd[4 * s + 3]});
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        dvt[dt] = mfma32(pf, dot[s][dt], dvt[dt]);
+        dkt[dt] = mfma32(df, qtr[s][dt], dkt[dt]);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {  // dK / dV live in the accumulator registers between tiles
+      asm volatile("" : "+a"(dvt[dt]));
+      asm volatile("" : "+a"(dkt[dt]));
+    }
+    // dQ_w[q][d] += dS[q][key] K[key][d]: dS (queries on lanes) from the transpose image, K^T
+    // fragments (d on lanes) from the K image, both in the permuted k order of tr16 reads
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 da = join4(lds_tr16(dsi + o_da0 + 1024 * s), lds_tr16(dsi + o_da1 + 1024 * s));
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        const bf16x8 kt_ = join4(lds_tr16(ki + o_tr0 + 512 * s + 2 * SUB * dt), lds_tr16(ki + o_tr1 + 512 * s + 2 * SUB * dt));
+        dqp[dt] = mfma32(da, kt_, dqp[dt]);
+      }
+    }
+  };
+
+  // dQ rows of slice qt: wave w sums rows 8w .. 8w+7 over the partials of the nw waves that had
+  // tiles in the slice, scales, converts and stores them
+  auto finish_dq = [&](int qt, int nw) {
+    const int row = 8 * w + (lane >> 3), c0 = (lane & 7) * 8;
+    f32x4 a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < nw; ++u) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(lds + OFF_DQ + u * 8192 + (row * 64 + c0) * 4);
+      a += src[0];
+      c += src[1];
+    }
+    const int t = qt * 32 + row;
+    if (t < T)
+      *reinterpret_cast<u32x4*>(P.dq + (rowbase + t) * P.dq_ld + head * 64 + c0) =
+          u32x4{pack2bf(a[0] * scale, a[1] * scale), pack2bf(a[2] * scale, a[3] * scale),
+                pack2bf(c[0] * scale, c[1] * scale), pack2bf(c[2] * scale, c[3] * scale)};
+  };
+
+  // the slice's tiles of this wave: D of the slice's rows, then each key tile at or below the query
+  // tile; the wave's dQ partial leaves into its fp32 partial tile
+  auto slice = [&](int i) {
+    const char* sb = lds + KIMG + (i % S) * SLOT;
+    bf16x8 qr[NKS], dr[NKS];
+    float dsum = 0.f;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      qr[s] = *reinterpret_cast<const bf16x8*>(sb + o_row + s * SUB);
+      dr[s] = *reinterpret_cast<const bf16x8*>(sb + OFF_DO + o_row + s * SUB);
+      const u32x4 ov = *reinterpret_cast<const u32x4*>(sb + OFF_O + o_row + s * SUB);
+      const u32x4 dv4 = __builtin_bit_cast(u32x4, dr[s]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dsum = __builtin_fmaf(bf2f(ov[e] & 0xffff), bf2f(dv4[e] & 0xffff), dsum);
+        dsum = __builtin_fmaf(bf2f(ov[e] >> 16), bf2f(dv4[e] >> 16), dsum);
+      }
+    }
+    dsum = xh_sum(dsum);  // D of query row r (both halves)
+    if (h == 0) dtab[r] = dsum;
+    f32x16 dqp[ND];
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) zero16(dqp[dt]);
+    const bool mask_all = ragged && i == nt - 1;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kt = kts[t];
+      if (kt < nt && kt <= i) {
+        // causal / ragged mask as a bit per accumulator element (one variant of the tile: two
+        // made the register allocator shuffle the dK / dV accumulators between them)
+        const uint32_t mk = (kt == i ? m_diag : 0xffffu) & (mask_all ? m_rows : 0xffffu);
+        tile(sb, i, kt, dk[t], dv[t], vf[t], qr, dr, dqp, mk);
+      }
+    }
+    float* part = reinterpret_cast<float*>(lds + OFF_DQ + w * 8192);
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) part[((e & 3) + 8 * (e >> 2) + 4 * h) * 64 + 32 * dt + r] = dqp[dt][e];
+  };
+
+#pragma unroll 1
+  for (int i = 0; i < nt; ++i) {
+    wait_vm(per * min(S - 2, nt - 1 - i));  // this wave's pieces of slice i landed (and K before them)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's pieces landed; slice i - 1's reads are done
+    if (i + S - 1 < nt) issue((i + S - 1) % S, i + S - 1);
+    const int nw = min(i + 1, 4);  // waves with a key tile at or below this query tile (w <= i)
+    if (w < nw) slice(i);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every partial of slice i is written
+    finish_dq(i, nw);
+  }
+
+
+  // dK / dV of the wave's key tiles, transposed through its LDS slot (aliasing the ring) into
+  // row-major 16-B pieces, as the dK/dV pass
+  bf16_t* et = reinterpret_cast<bf16_t*>(lds + KIMG) + w * (2 * 32 * EPW);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int kt = kts[t];
+    if (kt >= nt) continue;
+    const int k0 = kt * 32;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        et[kr * EPW + r] = f2bf(dk[t][dt][e] * scale);
+        et[32 * EPW + kr * EPW + r] = f2bf(DROP ? dv[t][dt][e] * P.drop_scale : dv[t][dt][e]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = i * 16 + (lane >> 2), d0 = dt * 32 + (lane & 3) * 8;
+        const u32x4 vk = *reinterpret_cast<const u32x4*>(et + row * EPW + (lane & 3) * 8);
+        const u32x4 vv = *reinterpret_cast<const u32x4*>(et + 32 * EPW + row * EPW + (lane & 3) * 8);
+        if (k0 + row < T) {
+          const int64_t off = (rowbase + k0 + row) * P.dkv_ld + d0;
+          *reinterpret_cast<u32x4*>(P.dk[0] + head * P.dkv_hstride + off) = vk;
+          *reinterpret_cast<u32x4*>(P.dv[0] + head * P.dkv_hstride + off) = vv;
+        }
+      }
+    }
+  }
+}
+
+hipError_t mmt_attn_bwd_fused64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, hipStream_t s) {
+  if (T > 512 || bt.p[0].nstreams != 1) return hipErrorInvalidValue;
+  const dim3 grid(B * H, 1, bt.count);
+  if (drop) hipLaunchKernelGGL((attn_bwd_fused64<true, 3>), grid, dim3(256), 0, s, bt, T, H, scale);
+  else hipLaunchKernelGGL((attn_bwd_fused64<false, 3>), grid, dim3(256), 0, s, bt, T, H, scale);
+  return hipGetLastError();
+}
+
 hipError_t mmt_attn_fwd_ring64(const AttnBatch& bt, int B, int T, int H, float scale, bool drop, hipStream_t s) {
   const int nt = (T + 31) / 32;
   const dim3 g2(((nt + 7) / 8) * B * H, 1, bt.count);

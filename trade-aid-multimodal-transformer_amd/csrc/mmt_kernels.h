@@ -230,13 +230,14 @@ struct AttnBatch { AttnProblem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
 hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
 // hs 64 dK/dV pass streaming the query slices through an LDS-DMA ring (mmt_attn2.hip)
-// variant (the mmt_attn_set_ring bits): 4 = 3 waves per SIMD, 8 / 16 = 8 / 4 key tiles per workgroup at
-// every T (default 4)
+// variant (the mmt_attn_set_ring bits): 4 = 3 waves per SIMD (default), else 2
 hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, int variant,
                                     hipStream_t s);
 // hs 64 dQ pass (and D_j) streaming the key slices through an LDS-DMA ring (mmt_attn2.hip)
 hipError_t mmt_attn_bwd_dq_ring64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, hipStream_t s);
 hipError_t mmt_attn_fwd_ring64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, hipStream_t s);
+// hs 64, T <= 512, one KV stream: dQ, dK, dV in one pass, one workgroup per (batch, head) (mmt_attn2.hip)
+hipError_t mmt_attn_bwd_fused64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, hipStream_t s);
 // fill dmask[j] (j < nstreams) of every problem with drop_thr != 0 from its counter hash
 hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStream_t s);
 
