@@ -8,9 +8,15 @@ for c in c1 target c3 c4; do
   case $c in c1) t="";; target) t="_t";; *) t="_$c";; esac
   F=$(ls gpurun_out/${T}_pmc_fetch$t/*counter_collection.csv*) || exit 1
   W=$(ls gpurun_out/${T}_pmc_write$t/*counter_collection.csv*) || exit 1
-  if [ $c = c4 ]; then FF="ffn0=gemm_f8_kernel<TileCfg<2, 4, 4, 2>, 2>"; else FF="ffn0=true, true, true, 2, 3>"; fi
+  # round 5: K >= 512 forward / data-gradient launches of >= 1024 tiles run the ping-pong kernel
+  # (gemm8_kernel<EPI, A_KC, B_KC>), the LayerNorm-fused N = 256 launches too (C1)
+  case $c in
+    c1) FF="ffn0=true, true, true, 2, 3>"; DX="ffn2_dx=, 6, 1>"; LN="ln_bwd_fused=gemm8_kernel<9, true, false>";;
+    c4) FF="ffn0=gemm_f8_kernel<TileCfg<2, 4, 4, 2>, 2>"; DX="ffn2_dx=gemm8_kernel<6, true, false>"; LN="";;
+    *) FF="ffn0=gemm8_kernel<2, true, true>"; DX="ffn2_dx=gemm8_kernel<6, true, false>"; LN="ln_bwd_fused=, 9, 1>";;
+  esac
   args=("$FF" "*_dw=false, false, true,+slab_reduce" "attn_fwd=attn_fwd@0/2" "ca_attn_fwd=attn_fwd@1/2"
-        "attn_bwd=attn_bwd_dq+attn_bwd_dkdv@1/2" "ca_attn_bwd=attn_bwd_dq+attn_bwd_dkdv@0/2" "ffn2_dx=, 6, 1>")
-  [ $c != c4 ] && args+=("ln_bwd_fused=, 9, 1>")
+        "attn_bwd=attn_bwd_dq+attn_bwd_dkdv@1/2" "ca_attn_bwd=attn_bwd_dq+attn_bwd_dkdv@0/2" "$DX")
+  [ -n "$LN" ] && args+=("$LN")
   python3 tools/pmc_traffic.py $c $F $W "${args[@]}" || exit 1
 done
