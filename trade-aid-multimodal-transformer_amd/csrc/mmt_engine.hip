@@ -975,6 +975,14 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         for (int ll = 1; ll < c->L; ++ll) gen_masks(ll);
     }
     r.attn(ab, false, scale, "attn_fwd");
+    // ln2 in the fused out-projection's epilogue (MMT_LN2_FUSE=0: the separate ln_fwd pass; fp8 keeps
+    // it, the pass also writes the MX-fp8 copy)
+    static const bool ln2_env = [] {
+      const char* e = getenv("MMT_LN2_FUSE");
+      return e ? atoi(e) != 0 : true;
+    }();
+    const bool ln2_fuse = ln2_env && !f8;
+    bool ln2_done = false;
     {
       // out-projection: Linear(C, C/2) -> tanh -> Linear(C/2, C) -> dropout -> + residual (model.py:82-92,
       // 224), fused into one launch where the shape allows (C = 256 / 512), else two GEMMs
@@ -988,20 +996,28 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
         g2.bias = r.P(x[i].bp2); g2.resid = xin[i]; g2.ldres = C;
         g2.o32 = r.W<float>(a[i].x1); g2.ldc = C;
         r.set_drop(g2, l, i, DS_SA_PROJ);
+        if (ln2_fuse) {  // the fused launch owns whole rows: ln2 runs in its epilogue (no MX-fp8 copy)
+          g2.lnf_gamma = r.P(x[i].ln2w); g2.lnf_beta = r.P(x[i].ln2b); g2.lnf_y = r.W<bf16_t>(a[i].c);
+          g2.lnf_mean = r.W<float>(a[i].mean2); g2.lnf_rstd = r.W<float>(a[i].rstd2);
+        }
       }
-      if (!r.mlp2(pg1, pg2, M, "proj")) {
+      const bool fused = r.mlp2(pg1, pg2, M, "proj");  // (nothing launched when it returns false)
+      ln2_done = fused && ln2_fuse;
+      if (!fused) {
         for (int i = 0; i < M; ++i) g.p[i] = pg1[i];
         r.gemm(g, true, true, EPI_BIAS_TANH_BF16, 1, "proj0");
-        for (int i = 0; i < M; ++i) g.p[i] = pg2[i];
+        for (int i = 0; i < M; ++i) { g.p[i] = pg2[i]; g.p[i].lnf_y = nullptr; }
         r.gemm(g, true, true, EPI_BIAS_RESID_F32, 1, "proj2");
       }
     }
-    for (int i = 0; i < M; ++i) {
-      lb.p[i].x = r.W<float>(a[i].x1); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].beta = r.P(x[i].ln2b);
-      lb.p[i].y = r.W<bf16_t>(a[i].c); lb.p[i].mean = r.W<float>(a[i].mean2); lb.p[i].rstd = r.W<float>(a[i].rstd2);
-      ln8(lb.p[i], a[i].c8, a[i].cs8);
+    if (!ln2_done) {
+      for (int i = 0; i < M; ++i) {
+        lb.p[i].x = r.W<float>(a[i].x1); lb.p[i].gamma = r.P(x[i].ln2w); lb.p[i].beta = r.P(x[i].ln2b);
+        lb.p[i].y = r.W<bf16_t>(a[i].c); lb.p[i].mean = r.W<float>(a[i].mean2); lb.p[i].rstd = r.W<float>(a[i].rstd2);
+        ln8(lb.p[i], a[i].c8, a[i].cs8);
+      }
+      r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "ln2_fwd");
     }
-    r.ok(mmt_launch_ln_fwd(lb, R, C, r.s), "ln2_fwd");
     for (int i = 0; i < M; ++i) {
       g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].c8), C, r.W<uint8_t>(a[i].cs8), ldsC, w8, x[i].F0, R)
                   : gp_fwd(r.W<bf16_t>(a[i].c), C, wpk, x[i].F0, R);
@@ -1428,6 +1444,11 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     }
   }
   if (c->any_cross) {
+    // MMT_DROP_COPY_FUSE=0: the separate drop_copy pass for every modality (A/B)
+    static const bool fuse_copy = [] {
+      const char* e = getenv("MMT_DROP_COPY_FUSE");
+      return e ? atoi(e) != 0 : true;
+    }();
     std::vector<int> cx;
     for (int i = 0; i < M; ++i) if (x[i].cross) cx.push_back(i);
     const int nc = (int)cx.size();
@@ -1497,7 +1518,16 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     }
     r.gemm_ln_bwd(dx, lc, R, C, "ca_q_dx", "lnc_bwd");
     // KV projections: dWkv += dkv^T x2_j ; dres[j] += dkv Wkv (one launch per query modality:
-    // different query modalities accumulate into the same dres[j])
+    // different query modalities accumulate into the same dres[j]). The LAST query modality that
+    // accumulates into dres[j] also writes its bf16 copy for the FFN backward in that epilogue (FFN
+    // dropout mask, FFN output-bias gradient as column sums): a separate drop_copy pass re-read the
+    // fp32 rows (6 x 38 us per step at the target). Only a modality no launch accumulates into (one
+    // cross modality: its own dres) keeps the copy pass.
+    d16_advance(c);
+    std::vector<int> last_writer(M, -1);
+    for (int i : cx)
+      for (int j = 0; j < M; ++j)
+        if (j != i) last_writer[j] = i;
     for (int i : cx) {
       GemmBatch kw{}; kw.count = 0;
       GemmBatch kx{}; kx.count = 0;
@@ -1508,6 +1538,10 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
         kw.p[kw.count++] = gp_dw(g, 2 * C, r.W<bf16_t>(a[j].x2h), C, grads, x[i].Wkv[jj], R);
         GemmProblem d = gp_dx(g, 2 * C, wpk, x[i].Wkv[jj], R);
         d.o32 = r.W<float>(p.dres[j]); d.ldc = C;
+        if (last_writer[j] == i && fuse_copy) {
+          d.o16 = d16_cur(c, r, j); d.ldo16 = C; d.dbias = grads + x[j].bf2;
+          r.set_drop(d, l, j, DS_FFN);
+        }
         kx.p[kx.count++] = d;
         ++jj;
         if (kw.count == MMT_MAX_GROUP) {
@@ -1518,14 +1552,15 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       if (kw.count) { r.dwgemm(kw, "ca_kv_dw"); r.gemm(kx, true, false, EPI_ACC_F32, 1, "ca_kv_dx"); }
     }
     r.flush();
-    // bf16 copy for the FFN backward: FFN dropout mask + FFN output-bias gradient
-    DropCopyBatch db{}; db.count = M;
-    d16_advance(c);
+    // bf16 copy for the FFN backward of the modalities no fused epilogue covered
+    DropCopyBatch db{}; db.count = 0;
     for (int i = 0; i < M; ++i) {
-      db.p[i].src = r.W<float>(p.dres[i]); db.p[i].dst = d16_cur(c, r, i); db.p[i].dsum = grads + x[i].bf2;
-      r.set_drop(db.p[i], l, i, DS_FFN);
+      if (fuse_copy && last_writer[i] >= 0) continue;
+      DropCopyProblem& q = db.p[db.count++];
+      q.src = r.W<float>(p.dres[i]); q.dst = d16_cur(c, r, i); q.dsum = grads + x[i].bf2;
+      r.set_drop(q, l, i, DS_FFN);
     }
-    r.ok(mmt_launch_drop_copy(db, R, C, r.s), "dres16");
+    if (db.count) r.ok(mmt_launch_drop_copy(db, R, C, r.s), "dres16");
   }
   if (r.rc != MMT_OK) return r.rc;
   // FFN

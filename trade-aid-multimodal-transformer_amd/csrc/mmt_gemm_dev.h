@@ -142,7 +142,18 @@ __device__ __forceinline__ float epi_scalar(const GemmProblem& P, float* o32, fl
     r += P.resid[(int64_t)m * P.ldres + n];
   }
   const int64_t o = (int64_t)m * P.ldc + n;
-  if (EPI == EPI_ACC_F32) { o32[o] += r; return r; }
+  if (EPI == EPI_ACC_F32) {
+    // + optional dropout-masked bf16 copy of the accumulated value (o16: the engine's last writer of a
+    // residual-gradient row block), whose column sums the caller adds to dbias
+    const float acc = o32[o] + r;
+    o32[o] = acc;
+    if (!P.o16) return r;
+    float c = acc;
+    if (P.drop_thr)
+      c = mmt_keep(mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)n >> 1), (uint32_t)n, P.drop_thr) ? c * P.drop_scale : 0.0f;
+    P.o16[(int64_t)m * P.ldo16 + n] = f2bf(c);
+    return c;
+  }
   if (EPI == EPI_ATOMIC_F32) { atomicAdd(o32 + o, r); return r; }
   if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32) {
     o32[o] = r;
@@ -159,7 +170,7 @@ template <int EPI>
 __device__ __forceinline__ void epi_pad(const GemmProblem& P, int m, int n) {
   constexpr bool bf16_out = EPI == EPI_STORE_BF16 || EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_BIAS_RELU_BF16 ||
                             EPI == EPI_DTANH_BF16 || EPI == EPI_DRELU_BF16;
-  if (bf16_out || (EPI == EPI_BIAS_RESID_F32 && P.o16)) {
+  if (bf16_out || ((EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32) && P.o16)) {
     if (n < P.ldo16) P.o16[(int64_t)m * P.ldo16 + n] = 0;
   }
 }
@@ -263,7 +274,8 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
   constexpr bool MX_OUT = EPI == EPI_BIAS_RELU_BF16 || EPI == EPI_BIAS_TANH_BF16 || EPI == EPI_STORE_BF16;
   // fused LayerNorm backward (whole rows per block: N == GBN, checked by the launcher)
   constexpr bool LNB = EPI == EPI_LN_BWD_F32;
-  const bool want_db = (CAN_DB || LNB) && P.dbias != nullptr;
+  // (EPI_ACC_F32 with a bf16 copy: the copy's column sums)
+  const bool want_db = (CAN_DB || LNB || (EPI == EPI_ACC_F32 && P.o16 != nullptr)) && P.dbias != nullptr;
   float cg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, cb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x4 gam0 = {0.f, 0.f, 0.f, 0.f}, gam1 = {0.f, 0.f, 0.f, 0.f};
   if (LNB && n + 8 <= N) {
@@ -456,6 +468,22 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
           if (EPI == EPI_BIAS_RESID_F32 && P.o16)
             *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
                 u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+          if (EPI == EPI_ACC_F32 && P.o16) {
+            // the dropout-masked bf16 copy of the accumulated rows (the consuming branch's dY) and
+            // its column sums (that branch's output-bias gradient), as drop_copy_kernel
+            if (P.drop_thr) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {  // n is even: one hash per column pair
+                const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n >> 1) + q);
+                r[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? r[2 * q] * P.drop_scale : 0.0f;
+                r[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? r[2 * q + 1] * P.drop_scale : 0.0f;
+              }
+            }
+            *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+                u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[e] += r[e];
+          }
           if (EPI == EPI_BIAS_RESID_F32 && (GBN == 256 || GBN == 512) && P.lnf_y) {
             // the next LayerNorm on this row (whole rows per block: N == GBN, mmt_launch_gemm_resid_ln;
             // lnf_y is uniform per problem and m < M per half wave, so every lane of the row's half
