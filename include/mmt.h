@@ -280,6 +280,10 @@ int mmt_op_embedding_bwd(void* stream, int32_t B, int32_t T, int32_t C, int32_t 
  * dtok, so the rows split into short chunks without global atomics; dtok is accumulated (+=) */
 int mmt_op_embedding_bwd_ws(void* stream, int32_t B, int32_t T, int32_t C, int32_t V, const int64_t* idx,
                             const float* dx, float* dtok, float* dpos, float* scratch);
+// token-table gradient variant of the scratch path (mmt_op_embedding_bwd_ws, the engine's): 1 (default,
+// env MMT_EMB_SORT) = counting sort of the rows by token + run sums (no LDS float atomics), 0 = the
+// LDS-privatised slabs with per-chunk partial tables; returns the previous value (tests, A/B)
+int mmt_emb_set_sort(int on);
 
 /* ---- MX-fp8 primitives (C4's fp8 path; BASELINE configs[4]) --------------------------------
  * MX-fp8 = OCP e4m3fn bytes + one E8M0 exponent byte (bias 127) per 32 consecutive K elements of a

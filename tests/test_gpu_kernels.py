@@ -707,14 +707,26 @@ def test_embedding(B, T, C, V):
     torch.testing.assert_close(dpos, dx.view(B, T, C).sum(0), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("sort", [1, 0])
 @pytest.mark.parametrize("B,T,C,V", [(2, 256, 256, 900), (64, 256, 256, 900), (16, 1024, 512, 5), (64, 256, 256, 13),
                                      (8, 512, 256, 144), (3, 4, 32, 3), (1, 64, 64, 200), (4, 256, 1024, 900),
-                                     (2, 96, 64, 5000)])
-def test_embedding_bwd_scratch(B, T, C, V):
-    """Token-table gradient with per-chunk partial tables (mmt_op_embedding_bwd_ws: the engine's
-    path) against torch index_add, accumulating into a non-zero dtok. (1, 64, 64, 200): the tables
-    do not fit B*T*C floats, so the atomic flush runs; (2, 96, 64, 5000): a table too large for a
-    4-float LDS slab takes direct atomics."""
+                                     (2, 96, 64, 5000), (1, 100, 96, 16384), (2, 33, 40, 7)])
+def test_embedding_bwd_scratch(B, T, C, V, sort):
+    """Token-table gradient of the scratch path (mmt_op_embedding_bwd_ws: the engine's) against torch
+    index_add, accumulating into a non-zero dtok. sort=1 (default): counting sort of the rows by token
+    + per-run sums (incl. the largest vocabulary the histogram holds, ragged row counts and column
+    widths); sort=0: the LDS-privatised slabs with per-chunk partial tables ((1, 64, 64, 200): the
+    tables do not fit B*T*C floats, so the atomic flush runs; (2, 96, 64, 5000): a table too large
+    for a 4-float LDS slab takes direct atomics)."""
+    L0 = ML.lib()
+    old = L0.mmt_emb_set_sort(sort)
+    try:
+        _embedding_bwd_scratch(B, T, C, V)
+    finally:
+        L0.mmt_emb_set_sort(old)
+
+
+def _embedding_bwd_scratch(B, T, C, V):
     torch.manual_seed(B + T + C + V)
     idx = torch.randint(0, V, (B, T), device=DEV)
     dx = torch.randn(B * T, C, device=DEV)

@@ -726,9 +726,10 @@ __global__ __launch_bounds__(256, MMT_DQ_MINB(HS)) void attn_bwd_dq_kernel(AttnB
     }
     dsa = xhalf_sum(dsa);
     dsb = xhalf_sum(dsb);
-    if (h == 0) {
-      if (oka) P.dvec[j][(int64_t)bh * T + A.tq] = dsa;
-      if (okb) P.dvec[j][(int64_t)bh * T + Bq.tq] = dsb;
+    if (h == 0) {  // D_j / drop_scale for the dK/dV pass (dkdv_tile: dS = sc (Z P dP - P D / sc))
+      const float inv = DROP ? 1.0f / P.drop_scale : 1.0f;
+      if (oka) P.dvec[j][(int64_t)bh * T + A.tq] = dsa * inv;
+      if (okb) P.dvec[j][(int64_t)bh * T + Bq.tq] = dsb * inv;
     }
     A.dsum = dsa;
     Bq.dsum = dsb;
@@ -865,16 +866,18 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
           const int tq = q0 + 8 * g + 4 * h + e4 + u;
           if (!(tk <= tq && tq < T)) pv = 0.f;
         }
-        float dp = dpacc[e];
-        if (DROP) {  // Z.P without the 1/(1-p) (applied to dV at the end), dS = P.(Z.dP - D)
+        const float dp = dpacc[e];
+        if (DROP) {
+          // Z.P without the 1/(1-p) (applied to dV at the end); dS = P (Z dP sc - D) = sc (Z P dP - P D'),
+          // D' = D / sc (the dQ pass stores it so), the factor sc applied to dK at the end: one VALU
+          // per element fewer than masking dP separately
           const int kb = __builtin_amdgcn_sbfe((int)mw, 8 * g + e4 + u, 1);  // all ones iff kept
           pm[u] = keep_f(pv, kb);
-          dp = keep_f(dp, kb);
+          ds[u] = __builtin_fmaf(pm[u], dp, pv * d4[g][e4 + u]);  // dS[q][key] / sc
         } else {
           pm[u] = pv;
+          ds[u] = pv * (dp + d4[g][e4 + u]);  // dS[q][key]
         }
-        const float sc = DROP ? P.drop_scale : 1.f;
-        ds[u] = pv * __builtin_fmaf(dp, sc, d4[g][e4 + u]);  // dS[q][key]
       }
       pp[2 * g + e4 / 2] = pack2bf(pm[0], pm[1]);
       dd[2 * g + e4 / 2] = pack2bf(ds[0], ds[1]);
@@ -1024,12 +1027,13 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
     if (live) {
       bf16_t* et = ept + w * (2 * 32 * EPW);
       const int k0 = kt * 32;
+      const float dks = DROP ? scale * P.drop_scale : scale;  // dS was accumulated divided by drop_scale
 #pragma unroll
       for (int dt = 0; dt < G::ND; ++dt) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-          et[kr * EPW + r] = f2bf(dk[dt][e] * scale);
+          et[kr * EPW + r] = f2bf(dk[dt][e] * dks);
           et[32 * EPW + kr * EPW + r] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
         }
 #pragma unroll

@@ -280,15 +280,17 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
             const int tq = qt * 32 + 8 * gg + 4 * h + e4 + u;
             if (!(tk <= tq && tq < T)) pv = 0.f;
           }
-          float dp = dpacc[e];
+          const float dp = dpacc[e];
           if (DROP) {
+            // dS = P (Z dP sc - D) = sc (Z P dP - P D'), D' = D / sc as the dQ pass stores it; sc is
+            // applied to dK at the end (one VALU per element fewer than masking dP separately)
             const int kbit = __builtin_amdgcn_sbfe((int)mw, 8 * gg + e4 + u, 1);  // all ones iff kept
             pm[u] = keep_f(pv, kbit);
-            dp = keep_f(dp, kbit);
+            ds[u] = __builtin_fmaf(pm[u], dp, -(pv * d4[e4 + u]));  // dS[q][key] / sc
           } else {
             pm[u] = pv;
+            ds[u] = pv * (dp - d4[e4 + u]);  // dS[q][key]
           }
-          ds[u] = pv * __builtin_fmaf(dp, dsc, -d4[e4 + u]);  // dS[q][key]
         }
         pp[2 * gg + e4 / 2] = pack2bf(pm[0], pm[1]);
         dd[2 * gg + e4 / 2] = pack2bf(ds[0], ds[1]);
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(64 * NWV, OCC) void attn_bwd_dkdv_ring64(AttnBatch 
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-        et[kr * EPW + r] = f2bf(dk[dt][e] * scale);
+        et[kr * EPW + r] = f2bf(DROP ? dk[dt][e] * (scale * P.drop_scale) : dk[dt][e] * scale);
         et[32 * EPW + kr * EPW + r] = f2bf(DROP ? dv[dt][e] * P.drop_scale : dv[dt][e]);
       }
 #pragma unroll
@@ -421,8 +423,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
       }
       d += __shfl_xor(d, 32, 64);
       const float l2 = okq[u] ? P.lse[j][(int64_t)bh * T + tq[u]] : 0.f;
-      if (h == 0) {
-        if (okq[u]) P.dvec[j][(int64_t)bh * T + tq[u]] = d;
+      if (h == 0) {  // D_j / drop_scale for the dK/dV pass (its dS = sc (Z P dP - P D / sc))
+        if (okq[u]) P.dvec[j][(int64_t)bh * T + tq[u]] = DROP ? d / P.drop_scale : d;
         tab[(u * MMT_MAX_STREAMS + j) * 64 + 2 * r] = l2;
         tab[(u * MMT_MAX_STREAMS + j) * 64 + 2 * r + 1] = d;
       }

@@ -400,6 +400,140 @@ __global__ __launch_bounds__(256) void embed_pos_bwd_kernel(EmbBatch batch, int 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Token-table gradient by a counting sort of the rows (round 5; the engine's path, EmbProblem::part
+// as int scratch): the LDS-privatised slabs above scatter-add every element with ds_add_f32, and LDS
+// float atomics serialise (C1: 127 + 28 us live for 67 MB of dx, 14x its HBM time; the last kernels
+// of the step). Here no float atomic touches LDS:
+//  * emb_sort_kernel, one workgroup per modality: token histogram (LDS integer atomics), exclusive
+//    scan, scatter of the row ids into token order -> perm [R] (order inside a token's bucket is
+//    the arrival order: the float sum order of dtok varies run to run, as with the atomics before);
+//  * emb_segsum_kernel: a wave walks 64 consecutive sorted rows (each dx row read once, 1 KiB per
+//    wave-load), sums runs of equal tokens in registers and adds each run to dtok with one atomic per
+//    column (a few runs per wave: ~V + waves adds per column in all).
+// ---------------------------------------------------------------------------------------------
+#define EMB_SORT_VMAX 16384
+__global__ __launch_bounds__(1024) void emb_sort_kernel(EmbBatch batch, int R) {
+  const EmbProblem& P = batch.p[blockIdx.z];
+  const int V = P.V;
+  int* perm = reinterpret_cast<int*>(P.part);
+  __shared__ int cnt[EMB_SORT_VMAX];
+  __shared__ int wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int v = tid; v < V; v += 1024) cnt[v] = 0;
+  __syncthreads();
+  for (int r = tid; r < R; r += 1024) {
+    int64_t t = P.idx[r];
+    t = t < 0 ? 0 : (t >= V ? V - 1 : t);
+    atomicAdd(&cnt[t], 1);
+  }
+  __syncthreads();
+  // exclusive scan: thread tid owns entries [tid * per, tid * per + per)
+  const int per = (V + 1023) / 1024;
+  const int b0 = tid * per, b1 = min(V, b0 + per);
+  int s = 0;
+  for (int v = b0; v < b1; ++v) s += cnt[v];
+  int incl = s;  // inclusive wave scan of the per-thread sums
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int wbase = 0;
+  for (int u = 0; u < w; ++u) wbase += wsum[u];
+  int run = wbase + incl - s;  // exclusive prefix of this thread's first entry
+  for (int v = b0; v < b1; ++v) {
+    const int c = cnt[v];
+    cnt[v] = run;  // now the bucket's next free slot
+    run += c;
+  }
+  __syncthreads();
+  for (int r = tid; r < R; r += 1024) {
+    int64_t t = P.idx[r];
+    t = t < 0 ? 0 : (t >= V ? V - 1 : t);
+    perm[atomicAdd(&cnt[t], 1)] = r;
+  }
+}
+
+// grid (ceil(R / 64) * halves / 4, 1, problems), 256 threads: wave -> (64-row range, column half);
+// lane c4 holds float4 column 4 c4 of its half (C <= 512: halves = C / 256 rounded up)
+__global__ __launch_bounds__(256) void emb_segsum_kernel(EmbBatch batch, int R, int C) {
+  const EmbProblem& P = batch.p[blockIdx.z];
+  const int V = P.V;
+  const int* perm = reinterpret_cast<const int*>(P.part);
+  const int halves = (C + 255) / 256;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int range = gw / halves, hf = gw % halves;
+  const int p0 = range * 64;
+  if (p0 >= R) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const int c4 = hf * 64 + lane;       // float4 column of this lane
+  const bool col_ok = 4 * c4 < C;
+  const int n = min(64, R - p0);
+  // lane l fetches sorted row p0 + l and its token; the walk reads them back by readlane
+  int myrow = 0, mytok = 0;
+  if (lane < n) {
+    myrow = perm[p0 + lane];
+    int64_t t = P.idx[myrow];
+    mytok = (int)(t < 0 ? 0 : (t >= V ? V - 1 : t));
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int cur = __builtin_amdgcn_readlane(mytok, 0);
+  constexpr int U = 8;  // rows in flight
+  for (int k0 = 0; k0 < n; k0 += U) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u;
+      const int row = __builtin_amdgcn_readlane(myrow, k < n ? k : 0);
+      v[u] = (k < n && col_ok) ? reinterpret_cast<const f32x4*>(P.dx + (int64_t)row * C)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u;
+      if (k >= n) break;  // wave-uniform
+      const int t = __builtin_amdgcn_readlane(mytok, k);
+      if (t != cur) {  // wave-uniform: a run of token cur ends
+        if (col_ok) {
+          float* d = P.dtok + (int64_t)cur * C + 4 * c4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) atomicAdd(d + e, acc[e]);
+        }
+        acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        cur = t;
+      }
+      acc += v[u];
+    }
+  }
+  if (col_ok) {
+    float* d = P.dtok + (int64_t)cur * C + 4 * c4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicAdd(d + e, acc[e]);
+  }
+}
+
+// the sorted path applies when every problem has int scratch for the permutation and a vocabulary
+// the histogram holds (MMT_EMB_SORT=0: the LDS-slab kernels, A/B)
+static int g_emb_sort = [] {
+  const char* e = getenv("MMT_EMB_SORT");
+  return e ? atoi(e) : 1;
+}();
+extern "C" int mmt_emb_set_sort(int on) {
+  const int old = g_emb_sort;
+  g_emb_sort = on;
+  return old;
+}
+static bool emb_sorted_ok(const EmbBatch& b, int R, int C) {
+  if (!g_emb_sort || C > 1024) return false;
+  for (int g = 0; g < b.count; ++g) {
+    const EmbProblem& P = b.p[g];
+    if (!P.part || P.V < 1 || P.V > EMB_SORT_VMAX || (int64_t)R * C < R) return false;
+  }
+  return true;
+}
+
 hipError_t mmt_launch_embed_fwd(const EmbBatch& b, int B, int T, int C, hipStream_t s) {
   if (C % 4 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
   const int64_t n = (int64_t)B * T * (C / 4);
@@ -412,6 +546,16 @@ hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStrea
   if (C % 4 || b.count == 0) return C % 4 ? hipErrorInvalidValue : hipSuccess;
   const int R = B * T;
   if (C % 4 || C > 1024) return hipErrorInvalidValue;
+  if (emb_sorted_ok(b, R, C)) {
+    for (int g = 1; g < b.count; ++g)
+      if (b.p[g].dpos != b.p[0].dpos) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(emb_sort_kernel, dim3(1, 1, b.count), dim3(1024), 0, s, b, R);
+    const int halves = (C + 255) / 256;
+    const int waves = ((R + 63) / 64) * halves;
+    hipLaunchKernelGGL(emb_segsum_kernel, dim3((waves + 3) / 4, 1, b.count), dim3(256), 0, s, b, R, C);
+    hipLaunchKernelGGL(embed_pos_bwd_kernel, dim3(T, EMB_POS_SPLIT), dim3(256), 0, s, b, B, T, C);
+    return hipGetLastError();
+  }
   // grid: the largest (slabs x row chunks) over the problems
   bool all_part = true;
   for (int g = 0; g < b.count; ++g) all_part = all_part && b.p[g].part != nullptr;
