@@ -70,6 +70,7 @@ struct ActLM {  // byte offsets of one (layer, modality)'s saved activations in 
   // MX-fp8 copies of the fp8 GEMMs' A operands (precision fp8): LN1 / LN2 / LNc outputs and the
   // FFN hidden, e4m3fn bytes + E8M0 exponents
   size_t a8 = 0, as8 = 0, c8 = 0, cs8 = 0, f8 = 0, fs8 = 0, d8 = 0, ds8 = 0;
+  size_t fm = 0;  // ReLU bits of the FFN hidden [R][4C / 8] (the ffn2 data gradient's ReLU')
 };
 
 struct Plan {
@@ -413,6 +414,7 @@ void make_plan(mmt_ctx* c, int B) {
       a.p1 = A(R * ldp * b2); a.x1 = A(R * C * f4);
       a.c = A(R * C * b2); a.mean2 = A(R * f4); a.rstd2 = A(R * f4);
       a.f = A(R * 4 * C * b2); a.x2 = A(R * C * f4);
+      a.fm = A(R * (4 * C / 8));
       a.x2h = c->any_cross ? A(R * C * b2) : 0;
       a.dm = mbytes ? A(mbytes) : 0;
       if (c->fp8) {
@@ -836,6 +838,13 @@ struct Runner {
 // -------------------------------------------------------------------------------------------
 // forward
 // -------------------------------------------------------------------------------------------
+// the FFN's ReLU' as bits written by ffn0 (16x fewer bytes than the bf16 hidden the ffn2 data
+// gradient read back; MMT_RELU_BITS=0: the bf16 aux)
+static const bool relu_bits = [] {
+  const char* e = getenv("MMT_RELU_BITS");
+  return e ? atoi(e) != 0 : true;
+}();
+
 int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t* const* tgt, float* const* logits,
                 float* losses) {
   const int M = c->M, C = c->C, H = c->H, hs = c->hs, R = r.R, B = r.B, T = c->T;
@@ -1022,10 +1031,12 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].c8), C, r.W<uint8_t>(a[i].cs8), ldsC, w8, x[i].F0, R)
                   : gp_fwd(r.W<bf16_t>(a[i].c), C, wpk, x[i].F0, R);
       g.p[i].bias = r.P(x[i].bf0); g.p[i].o16 = r.W<bf16_t>(a[i].f); g.p[i].ldo16 = 4 * C;
+      if (relu_bits) { g.p[i].mask8 = r.W<uint8_t>(a[i].fm); g.p[i].ldm8 = 4 * C / 8; }
       if (f8) { g.p[i].o8 = r.W<uint8_t>(a[i].f8); g.p[i].ld8 = 4 * C; g.p[i].s8 = r.W<uint8_t>(a[i].fs8); g.p[i].lds8 = ldsF; }
     }
     if (f8) r.gemm8(g, EPI_BIAS_RELU_BF16, "ffn0");
     else r.gemm(g, true, true, EPI_BIAS_RELU_BF16, 1, "ffn0");
+    for (int i = 0; i < M; ++i) g.p[i].mask8 = nullptr;  // g is reused
     for (int i = 0; i < M; ++i) {
       g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].f8), 4 * C, r.W<uint8_t>(a[i].fs8), ldsF, w8, x[i].F2, R)
                   : gp_fwd(r.W<bf16_t>(a[i].f), 4 * C, wpk, x[i].F2, R);
@@ -1574,6 +1585,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     dx.p[i] = gp_dx(g, C, wpk, x[i].F2, R);
     dx.p[i].aux = r.W<bf16_t>(a[i].f); dx.p[i].ldaux = 4 * C; dx.p[i].o16 = r.W<bf16_t>(p.gbig[par][i]); dx.p[i].ldo16 = 4 * C;
     dx.p[i].dbias = grads + x[i].bf0;
+    if (relu_bits) { dx.p[i].mask8 = r.W<uint8_t>(a[i].fm); dx.p[i].ldm8 = 4 * C / 8; }  // ReLU' from bits
   }
   r.dwgemm(dw, "ffn2_dw");
   r.gemm(dx, true, false, EPI_DRELU_BF16, 1, "ffn2_dx");

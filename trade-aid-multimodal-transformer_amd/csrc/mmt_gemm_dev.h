@@ -135,7 +135,11 @@ __device__ __forceinline__ float epi_scalar(const GemmProblem& P, float* o32, fl
   if (!PRE && EPI == EPI_BIAS_TANH_BF16) r = fast_tanh(r);
   if (EPI == EPI_BIAS_RELU_BF16) r = fmaxf(r, 0.0f);
   if (EPI == EPI_DTANH_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r *= (1.0f - t * t); }
-  if (EPI == EPI_DRELU_BF16) { const float t = bf2f(P.aux[(int64_t)m * P.ldaux + n]); r = t > 0.0f ? r : 0.0f; }
+  if (EPI == EPI_DRELU_BF16) {
+    const bool keep = P.mask8 ? ((P.mask8[(int64_t)m * P.ldm8 + (n >> 3)] >> (n & 7)) & 1) != 0
+                              : bf2f(P.aux[(int64_t)m * P.ldaux + n]) > 0.0f;
+    r = keep ? r : 0.0f;
+  }
   if (EPI == EPI_BIAS_RESID_F32) {
     if (P.drop_thr)
       r = mmt_keep(mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)n >> 1), (uint32_t)n, P.drop_thr) ? r * P.drop_scale : 0.0f;
@@ -296,12 +300,17 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
   // epilogue alone 110-150 us of a 260 us launch). The pass barriers are raw s_barriers behind an LDS
   // wait: __syncthreads() would also drain those loads (and the previous pass's stores) at every pass.
   u32x4 auxn[IT];
+  uint32_t mskn[IT];  // EPI_DRELU_BF16 with mask8: the 8 ReLU bits of this thread's columns
+  const bool use_m8 = EPI == EPI_DRELU_BF16 && P.mask8 != nullptr;
   auto load_aux = [&](int pass_) {
     if (!(n + 8 <= N && vec_ok)) return;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int m = m0 + pass_ * EPI_ROWS + it * RPI + rsub;
-      if (m < M) auxn[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
+      if (m < M) {
+        if (use_m8) mskn[it] = P.mask8[(int64_t)m * P.ldm8 + (n >> 3)];
+        else auxn[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
+      }
     }
   };
   if constexpr (HAS_AUX) load_aux(0);
@@ -393,10 +402,14 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
     } else if (n + 8 <= N && vec_ok) {
       // issue every operand load of this thread's rows first (memory-level parallelism)
       u32x4 auxv[IT];
+      uint32_t mskv[IT];
       f32x4 resv[IT][2];
       if constexpr (HAS_AUX) {
 #pragma unroll
-        for (int it = 0; it < IT; ++it) auxv[it] = auxn[it];
+        for (int it = 0; it < IT; ++it) {
+          auxv[it] = auxn[it];
+          mskv[it] = mskn[it];
+        }
         if (pass + 1 < GBM / EPI_ROWS) load_aux(pass + 1);
       }
 #pragma unroll
@@ -433,16 +446,21 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
           for (int e = 0; e < 8; ++e) r[e] = fmaxf(r[e], 0.0f);
         }
         if (HAS_AUX) {
-          const u32x4 a = auxv[it];
+          if (EPI == EPI_DRELU_BF16 && use_m8) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float t0 = bf2f(a[q] & 0xffff), t1 = bf2f(a[q] >> 16);
-            if (EPI == EPI_DTANH_BF16) {
-              r[2 * q] *= (1.0f - t0 * t0);
-              r[2 * q + 1] *= (1.0f - t1 * t1);
-            } else {
-              r[2 * q] = t0 > 0.0f ? r[2 * q] : 0.0f;
-              r[2 * q + 1] = t1 > 0.0f ? r[2 * q + 1] : 0.0f;
+            for (int e = 0; e < 8; ++e) r[e] = ((mskv[it] >> e) & 1u) ? r[e] : 0.0f;
+          } else {
+            const u32x4 a = auxv[it];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float t0 = bf2f(a[q] & 0xffff), t1 = bf2f(a[q] >> 16);
+              if (EPI == EPI_DTANH_BF16) {
+                r[2 * q] *= (1.0f - t0 * t0);
+                r[2 * q + 1] *= (1.0f - t1 * t1);
+              } else {
+                r[2 * q] = t0 > 0.0f ? r[2 * q] : 0.0f;
+                r[2 * q + 1] = t1 > 0.0f ? r[2 * q + 1] : 0.0f;
+              }
             }
           }
         }
@@ -515,8 +533,18 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
             if (c8 == 0) { P.lnf_mean[m] = mean; P.lnf_rstd[m] = rstd; }
           }
         } else {
-          *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
-              u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+          const u32x4 packed = {pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
+          *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) = packed;
+          if (EPI == EPI_BIAS_RELU_BF16 && P.mask8) {  // bit e: the stored bf16 value is > 0
+            uint32_t mb = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t lo = packed[q] & 0xffffu, hi = packed[q] >> 16;
+              mb |= (uint32_t)(lo != 0 && lo < 0x8000u) << (2 * q);
+              mb |= (uint32_t)(hi != 0 && hi < 0x8000u) << (2 * q + 1);
+            }
+            P.mask8[(int64_t)m * P.ldm8 + (n >> 3)] = (uint8_t)mb;
+          }
           if (MX_OUT && P.o8) {
             // MX-fp8 copy: the 32-column block of this row is 4 consecutive threads (c8 & ~3)
             float am = 0.f;
@@ -543,12 +571,19 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
         const int ml = it * RPI + rsub;
         const int m = mb + ml;
         if (m >= M) continue;
+        uint32_t mb = 0;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float v = ct[ml * CT + 8 * c8 + e];
-          if (n + e < N) cs[e] += epi_scalar<EPI, PRE>(P, o32, alpha, m, n + e, v);
-          else epi_pad<EPI>(P, m, n + e);
+          if (n + e < N) {
+            const float o = epi_scalar<EPI, PRE>(P, o32, alpha, m, n + e, v);
+            cs[e] += o;
+            if (EPI == EPI_BIAS_RELU_BF16) mb |= (uint32_t)(bf2f(f2bf(o)) > 0.0f) << e;
+          } else {
+            epi_pad<EPI>(P, m, n + e);
+          }
         }
+        if (EPI == EPI_BIAS_RELU_BF16 && P.mask8) P.mask8[(int64_t)m * P.ldm8 + (n >> 3)] = (uint8_t)mb;
       }
     }
   }

@@ -89,6 +89,11 @@ struct GemmProblem {
   const float* qkv2_w2;
   bf16_t* qkv2_out;
   int qkv2_ld, qkv2_hh;
+  // ReLU masks as bits (round 5): EPI_BIAS_RELU_BF16 also writes mask8[m * ldm8 + n / 8] bit n % 8 =
+  // (stored bf16 output > 0); EPI_DRELU_BF16 with mask8 set (aux null) reads those bits instead of
+  // the bf16 aux rows (16x fewer bytes). SWAP epilogues only; null: off
+  uint8_t* mask8;
+  int ldm8;
 };
 
 struct GemmBatch {
