@@ -668,8 +668,10 @@ def test_colsum(R, N, ld):
     assert rel(out - 2.0, 0.5 * x.float()[:, :N].sum(0)) < 1e-5
 
 
-@pytest.mark.parametrize("R,V", [(1000, 900), (77, 13), (64, 2), (33, 1), (500, 144)])
+@pytest.mark.parametrize("R,V", [(1000, 900), (77, 13), (64, 2), (33, 1), (500, 144), (20000, 900), (4097, 5), (9000, 1500)])
 def test_cross_entropy(R, V):
+    """Loss and dlogits against torch; R > 2048 makes every wave walk several rows (the next row's
+    loads in flight, ragged last rows), V = 1500 takes the three-pass form."""
     torch.manual_seed(R + V)
     logits = torch.randn(R, V, device=DEV) * 2
     tgt = torch.randint(0, V, (R,), device=DEV)

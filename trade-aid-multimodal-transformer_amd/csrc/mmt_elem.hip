@@ -598,6 +598,49 @@ hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStrea
 // grid-strided rows so each block adds its loss share with ONE atomic (a per-4-row atomic on
 // the single loss address serialised ~16 k atomics per launch)
 // ============================================================================================
+// rows of one problem with KV logits per lane: two rows per wave in flight (the next row's loads
+// are issued before this row's reductions), so a wave's row-after-row latency chain halves
+template <int KV>
+__device__ __forceinline__ float ce_rows(const CeProblem& P, int R, int lane, int first, int stride) {
+  const int V = P.V;
+  float contrib = 0.f;
+  float v[KV], nv[KV];
+  auto load = [&](int row, float (&dst)[KV]) {
+    const float* x = P.logits + (int64_t)row * V;
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+      const int i = lane + 64 * k;
+      dst[k] = (row < R && i < V) ? x[i] : -INFINITY;
+    }
+  };
+  if (first < R) load(first, v);
+  for (int row = first; row < R; row += stride) {
+    const int t = (int)P.tgt[row];
+    const float xt = P.logits[(int64_t)row * V + t];
+    if (row + stride < R) load(row + stride, nv);
+    float m = v[0];
+#pragma unroll
+    for (int k = 1; k < KV; ++k) m = fmaxf(m, v[k]);
+    m = warp_max(m);
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < KV; ++k) sum += __expf(v[k] - m);  // exp(-inf) = 0 for the padding
+    const float lse = m + __logf(warp_sum(sum));
+    contrib += lse - xt;
+    bf16_t* d = P.dlogits + (int64_t)row * P.ld_d;
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+      const int i = lane + 64 * k;
+      if (i < P.ld_d) d[i] = f2bf(i < V ? __expf(v[k] - lse) - (i == t ? 1.f : 0.f) : 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < KV; ++k) v[k] = nv[k];
+  }
+  return contrib;
+}
+
+// KV: the largest vocabulary's logits per lane (64 k + lane); each problem runs the smallest
+// instantiation that holds its own vocabulary (the V = 5 head no longer walks 16 masked groups)
 template <int KV>
 __global__ __launch_bounds__(256) void ce_fwd_kernel(CeBatch batch, int R) {
   const CeProblem& P = batch.p[blockIdx.z];
@@ -606,32 +649,19 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(CeBatch batch, int R) {
   const int V = P.V;
   __shared__ float part[4];
   float contrib = 0.f;
-  for (int row = blockIdx.x * 4 + wave; row < R; row += gridDim.x * 4) {
-    const float* x = P.logits + (int64_t)row * V;
-    const int t = (int)P.tgt[row];
-    bf16_t* d = P.dlogits + (int64_t)row * P.ld_d;
-    if (KV > 0) {
-      float v[KV > 0 ? KV : 1];
-#pragma unroll
-      for (int k = 0; k < KV; ++k) {
-        const int i = lane + 64 * k;
-        v[k] = i < V ? x[i] : -INFINITY;
-      }
-      float m = v[0];
-#pragma unroll
-      for (int k = 1; k < KV; ++k) m = fmaxf(m, v[k]);
-      m = warp_max(m);
-      float sum = 0.f;
-#pragma unroll
-      for (int k = 0; k < KV; ++k) sum += __expf(v[k] - m);  // exp(-inf) = 0 for the padding
-      const float lse = m + __logf(warp_sum(sum));
-      contrib += lse - x[t];
-#pragma unroll
-      for (int k = 0; k < KV; ++k) {
-        const int i = lane + 64 * k;
-        if (i < P.ld_d) d[i] = f2bf(i < V ? __expf(v[k] - lse) - (i == t ? 1.f : 0.f) : 0.f);
-      }
-    } else {  // V > 1024: three passes over the row
+  const int first = blockIdx.x * 4 + wave, stride = gridDim.x * 4;
+  if (KV > 0) {
+    const int kv = (V + 63) / 64;  // uniform per problem
+    if (kv <= 1) contrib = ce_rows<1>(P, R, lane, first, stride);
+    else if (kv <= 2 && KV >= 2) contrib = ce_rows<2>(P, R, lane, first, stride);
+    else if (kv <= 4 && KV >= 4) contrib = ce_rows<4>(P, R, lane, first, stride);
+    else if (kv <= 8 && KV >= 8) contrib = ce_rows<8>(P, R, lane, first, stride);
+    else contrib = ce_rows<(KV > 0 ? KV : 1)>(P, R, lane, first, stride);
+  } else {  // V > 1024: three passes over the row
+    for (int row = first; row < R; row += stride) {
+      const float* x = P.logits + (int64_t)row * V;
+      const int t = (int)P.tgt[row];
+      bf16_t* d = P.dlogits + (int64_t)row * P.ld_d;
       float m = -INFINITY;
       for (int i = lane; i < V; i += 64) m = fmaxf(m, x[i]);
       m = warp_max(m);
