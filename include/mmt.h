@@ -284,6 +284,15 @@ int mmt_op_embedding_bwd_ws(void* stream, int32_t B, int32_t T, int32_t C, int32
 // env MMT_EMB_SORT) = counting sort of the rows by token + run sums (no LDS float atomics), 0 = the
 // LDS-privatised slabs with per-chunk partial tables; returns the previous value (tests, A/B)
 int mmt_emb_set_sort(int on);
+// per-head Q/K/V stage-2 backward at hs 32 / 64 (mmt_op_qkv2_bwd, the engine's): bit 0 (hs 32) / bit 1
+// (hs 64) set = each load instruction reads whole row slices and the tile is redistributed through
+// LDS, clear = loads in the MFMA fragment layout; default 2 (env MMT_QKV2_COAL); returns the previous
+// value (tests, A/B)
+int mmt_qkv2_set_coal(int on);
+// ping-pong 256 x 256 GEMM: first-generation blocks on every other CU of an XCD sleep units x 127 x 64
+// cycles before their first tile, so the CUs' epilogue store bursts do not line up (env
+// MMT_GEMM8_STAGGER, default 0 = off); returns the previous value (benchmarks, A/B)
+int mmt_gemm8_set_stagger(int units);
 
 /* ---- MX-fp8 primitives (C4's fp8 path; BASELINE configs[4]) --------------------------------
  * MX-fp8 = OCP e4m3fn bytes + one E8M0 exponent byte (bias 127) per 32 consecutive K elements of a

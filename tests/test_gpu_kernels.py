@@ -589,11 +589,23 @@ def test_attention_hs64_backward_variants(B, T, H, ns, ring):
 
 
 # ------------------------------------------------------------------------------ small kernels
+@pytest.mark.parametrize("coal", [3, 0])
 @pytest.mark.parametrize("R,H,hs", [(1000, 8, 32), (77, 4, 16), (300, 2, 64), (50, 4, 8), (5000, 8, 32),
-                                    (3000, 16, 64)])
-def test_qkv2(R, H, hs):
-    """Per-head stage 2 forward / backward vs torch; the last two shapes span several row blocks of
-    the hs 32 / 64 backward (1024 rows each: dW2 partials added by atomics) with a ragged tail."""
+                                    (3000, 16, 64), (33, 2, 64), (1055, 3, 32)])
+def test_qkv2(R, H, hs, coal):
+    """Per-head stage 2 forward / backward vs torch; the last shapes span several row blocks of
+    the hs 32 / 64 backward (1024 rows each: dW2 partials added by atomics) with a ragged tail, or
+    end one row into a 32-row tile. coal: the backward's row-slice loads through LDS (3: at hs
+    32 and 64; the engine's default takes them at hs 64) or loads in the MFMA fragment layout (0)."""
+    L0 = ML.lib()
+    old = L0.mmt_qkv2_set_coal(coal)
+    try:
+        _qkv2(R, H, hs)
+    finally:
+        L0.mmt_qkv2_set_coal(old)
+
+
+def _qkv2(R, H, hs):
     torch.manual_seed(R + H + hs)
     nblk, hh = 3 * H, hs // 2
     ld_h1, ld_out = r8(nblk * hh), nblk * hs

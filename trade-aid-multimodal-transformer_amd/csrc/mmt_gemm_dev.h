@@ -543,7 +543,18 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
               mb |= (uint32_t)(lo != 0 && lo < 0x8000u) << (2 * q);
               mb |= (uint32_t)(hi != 0 && hi < 0x8000u) << (2 * q + 1);
             }
-            P.mask8[(int64_t)m * P.ldm8 + (n >> 3)] = (uint8_t)mb;
+            // 8 consecutive threads (one row, 64 columns) join their bytes: one 8-byte store instead
+            // of eight byte stores (byte stores cost ffn0 8 % at the target)
+            const int g0 = n - 8 * (c8 & 7);  // first column of this thread's group
+            if (g0 + 64 <= N && (P.ldm8 & 7) == 0) {  // uniform across the group
+              uint32_t wv = mb;
+              wv |= (uint32_t)__shfl_down((int)wv, 1, 64) << 8;
+              wv |= (uint32_t)__shfl_down((int)wv, 2, 64) << 16;
+              const uint32_t w2 = (uint32_t)__shfl_down((int)wv, 4, 64);
+              if ((c8 & 7) == 0) *reinterpret_cast<u32x2*>(P.mask8 + (int64_t)m * P.ldm8 + (g0 >> 3)) = u32x2{wv, w2};
+            } else {
+              P.mask8[(int64_t)m * P.ldm8 + (n >> 3)] = (uint8_t)mb;
+            }
           }
           if (MX_OUT && P.o8) {
             // MX-fp8 copy: the 32-column block of this row is 4 consecutive threads (c8 & ~3)

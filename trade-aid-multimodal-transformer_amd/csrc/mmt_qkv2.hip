@@ -6,6 +6,7 @@
 //           dW2[o][i]  += sum_r dout[r][o] h1[r][i]        K = rows, operands by transposed LDS reads
 // blk = kind*H + head; h1 / dh1 rows hold nblk*hs/2 columns, out / dout rows nblk*hs columns.
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "mmt_common.h"
@@ -294,7 +295,11 @@ __global__ __launch_bounds__(256) void qkv2_bwd_mfma(Qkv2Batch batch, int R, int
 constexpr int QKV2B_TILES = 8;  // 32-row tiles per wave (a block of 4 waves: 1024 rows)
 __device__ __forceinline__ int q2_swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int HS>
+// COAL: each load instruction reads whole row slices (lane l: row l / CPR, 16-B chunk l % CPR), so one
+// instruction touches 64 / CPR rows instead of 32 row pieces; the tile goes through the wave's LDS
+// images (which the dW2 product reads anyway) and the MFMA fragments are read back from there. At
+// hs 64 the dh1 tile is restaged the same way before its store.
+template <int HS, bool COAL>
 __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
   constexpr int HH = HS / 2;
   constexpr int NOT = HS / 32;  // 32-column output tiles of dout (o)
@@ -333,10 +338,27 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
 #pragma unroll
   for (int e = 0; e < 16; ++e) z[e] = 0.f;
 
+  constexpr int CPR = HS / 8, RPI = 64 / CPR;  // COAL: dout chunks per row, rows per load instruction
+  constexpr int HPR = HH / 8, HRPI = 64 / HPR;  // the same for h1 / dh1
+  static_assert(!COAL || (KSO * RPI == 32 && NI * HRPI == 32), "coalesced loads cover the 32-row tile");
   u32x4 dv[KSO], hv[NI];
-  auto load = [&](int row) {
-    const bool ok = row < R;
+  auto load = [&](int row0) {  // row0: the tile's first row
     const u32x4 zz = {0u, 0u, 0u, 0u};
+    if (COAL) {
+#pragma unroll
+      for (int s = 0; s < KSO; ++s) {
+        const int rr = row0 + s * RPI + lane / CPR;
+        dv[s] = rr < R ? *reinterpret_cast<const u32x4*>(P.dout + (int64_t)rr * ld_out + blk * HS + 8 * (lane % CPR)) : zz;
+      }
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const int rr = row0 + q * HRPI + lane / HPR;
+        hv[q] = rr < R ? *reinterpret_cast<const u32x4*>(P.h1 + (int64_t)rr * ld_h1 + blk * HH + 8 * (lane % HPR)) : zz;
+      }
+      return;
+    }
+    const int row = row0 + r;
+    const bool ok = row < R;
     const bf16_t* d = P.dout + (int64_t)row * ld_out + blk * HS + 8 * h;
     const bf16_t* hp = P.h1 + (int64_t)row * ld_h1 + blk * HH + 8 * h;
 #pragma unroll
@@ -345,17 +367,32 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
     for (int q = 0; q < NI; ++q) hv[q] = ok ? *reinterpret_cast<const u32x4*>(hp + 16 * q) : zz;
   };
   const int r0 = rb * RPB + w * 32 * QKV2B_TILES;
-  load(r0 + r);
+  load(r0);
 #pragma unroll 1
   for (int t = 0; t < QKV2B_TILES; ++t) {
     const int row = r0 + 32 * t + r;
     if (r0 + 32 * t >= R) break;  // wave-uniform
     u32x4 dc[KSO], hc[NI];
+    if (COAL) {  // rows past R hold zeros (their loads returned 0)
 #pragma unroll
-    for (int s = 0; s < KSO; ++s) dc[s] = dv[s];
+      for (int s = 0; s < KSO; ++s) {
+        const int c = lane % CPR;
+        *reinterpret_cast<u32x4*>(img + (c >> 2) * 2048 + q2_swz(s * RPI + lane / CPR, c & 3)) = dv[s];
+      }
 #pragma unroll
-    for (int q = 0; q < NI; ++q) hc[q] = hv[q];
-    if (t + 1 < QKV2B_TILES) load(row + 32);  // the next tile's loads fly while this one computes
+      for (int q = 0; q < NI; ++q) *reinterpret_cast<u32x4*>(himg + q2_swz(q * HRPI + lane / HPR, lane % HPR)) = hv[q];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int s = 0; s < KSO; ++s) dc[s] = *reinterpret_cast<const u32x4*>(img + (s >> 1) * 2048 + q2_swz(r, 2 * (s & 1) + h));
+#pragma unroll
+      for (int q = 0; q < NI; ++q) hc[q] = *reinterpret_cast<const u32x4*>(himg + q2_swz(r, 2 * q + h));
+    } else {
+#pragma unroll
+      for (int s = 0; s < KSO; ++s) dc[s] = dv[s];
+#pragma unroll
+      for (int q = 0; q < NI; ++q) hc[q] = hv[q];
+    }
+    if (t + 1 < QKV2B_TILES) load(r0 + 32 * t + 32);  // the next tile's loads fly while this one computes
     // dh1 (accumulator rows = i in the permuted order: lane (r, h) gets i = 8 h + e, 16 + 8 h + e - 8)
     f32x16 acc = z;
 #pragma unroll
@@ -374,16 +411,19 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
       if (row < R) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[8 * q + e] += t8[e];
-        *reinterpret_cast<u32x4*>(P.dh1 + (int64_t)row * ld_h1 + blk * HH + 16 * q + 8 * h) = dz[q];
+        if (!(COAL && HPR >= 4))
+          *reinterpret_cast<u32x4*>(P.dh1 + (int64_t)row * ld_h1 + blk * HH + 16 * q + 8 * h) = dz[q];
       }
     }
     // dW2 over this tile's 32 rows: LDS images (rows past R hold zeros: their loads returned 0)
+    if (!COAL) {
 #pragma unroll
-    for (int s = 0; s < KSO; ++s)  // dout columns 16 s + 8 h: sub-image s / 2, chunk 2 (s & 1) + h
-      *reinterpret_cast<u32x4*>(img + (s >> 1) * 2048 + q2_swz(r, 2 * (s & 1) + h)) = dc[s];
+      for (int s = 0; s < KSO; ++s)  // dout columns 16 s + 8 h: sub-image s / 2, chunk 2 (s & 1) + h
+        *reinterpret_cast<u32x4*>(img + (s >> 1) * 2048 + q2_swz(r, 2 * (s & 1) + h)) = dc[s];
 #pragma unroll
-    for (int q = 0; q < NI; ++q) *reinterpret_cast<u32x4*>(himg + q2_swz(r, 2 * q + h)) = hc[q];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own wave's writes visible to its reads
+      for (int q = 0; q < NI; ++q) *reinterpret_cast<u32x4*>(himg + q2_swz(r, 2 * q + h)) = hc[q];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own wave's writes visible to its reads
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {  // rows 16 ks .. 16 ks + 15
       // tr read: lane gets column (l & 31) and rows 16 ks + 8 h + 0..7 of an image
@@ -398,6 +438,17 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
       const bf16x8 bh = trd(himg);
 #pragma unroll
       for (int ot = 0; ot < NOT; ++ot) dw[ot] = mfma32(trd(img + ot * 2048), bh, dw[ot]);
+    }
+    if (COAL && HPR >= 4) {  // dh1 through the h1 image (its reads above come first: LDS is in order per wave)
+#pragma unroll
+      for (int q = 0; q < NI; ++q) *reinterpret_cast<u32x4*>(himg + q2_swz(r, 2 * q + h)) = dz[q];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const int rr = r0 + 32 * t + q * HRPI + lane / HPR;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(himg + q2_swz(q * HRPI + lane / HPR, lane % HPR));
+        if (rr < R) *reinterpret_cast<u32x4*>(P.dh1 + (int64_t)rr * ld_h1 + blk * HH + 8 * (lane % HPR)) = v;
+      }
     }
   }
   // block reductions: db1 (column sums) and dW2, then one atomic per element per block
@@ -441,13 +492,28 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
   for (int q = tid; q < HS * HH; q += 256) atomicAdd(P.dw2 + (int64_t)blk * HS * HH + q, red[q]);
 }
 
+static int g_qkv2_coal = [] {
+  const char* e = getenv("MMT_QKV2_COAL");
+  return e ? atoi(e) : 2;  // bit 0: hs 32, bit 1: hs 64 (hs 32: C1 +0.13 %, hs 64: target -0.25 %, r5y)
+}();
+extern "C" int mmt_qkv2_set_coal(int on) {
+  const int old = g_qkv2_coal;
+  g_qkv2_coal = on;
+  return old;
+}
+
 template <int HS>
 static void qkv2_launch(const Qkv2Batch& b, int R, int nblk, int ld_h1, int ld_out, bool bwd, hipStream_t s) {
   constexpr int RPB = 4 * 32 * QKV2B_TILES;
   // (v2 against qkv2_bwd_mfma in the step: C1 8.818 vs 8.832 ms, target 20.39 vs 20.48: profiles/r4k_ab.txt)
-  if (bwd && (HS == 32 || HS == 64))
-    hipLaunchKernelGGL(qkv2_bwd_v2<HS == 64 ? 64 : 32>, dim3((R + RPB - 1) / RPB * nblk, 1, b.count), dim3(256), 0, s, b,
-                       R, ld_h1, ld_out);
+  constexpr int HV = HS == 64 ? 64 : 32;
+  if (bwd && (HS == 32 || HS == 64)) {
+    const dim3 grid((R + RPB - 1) / RPB * nblk, 1, b.count);
+    if (g_qkv2_coal & (HV == 64 ? 2 : 1))
+      hipLaunchKernelGGL((qkv2_bwd_v2<HV, true>), grid, dim3(256), 0, s, b, R, ld_h1, ld_out);
+    else
+      hipLaunchKernelGGL((qkv2_bwd_v2<HV, false>), grid, dim3(256), 0, s, b, R, ld_h1, ld_out);
+  }
   else if (bwd)
     hipLaunchKernelGGL(qkv2_bwd_mfma<HS>, dim3((R + QKV2_BWD_ROWS - 1) / QKV2_BWD_ROWS * nblk, 1, b.count), dim3(256), 0, s,
                        b, R, ld_h1, ld_out);
