@@ -289,10 +289,6 @@ int mmt_emb_set_sort(int on);
 // LDS, clear = loads in the MFMA fragment layout; default 2 (env MMT_QKV2_COAL); returns the previous
 // value (tests, A/B)
 int mmt_qkv2_set_coal(int on);
-// ping-pong 256 x 256 GEMM: first-generation blocks on every other CU of an XCD sleep units x 127 x 64
-// cycles before their first tile, so the CUs' epilogue store bursts do not line up (env
-// MMT_GEMM8_STAGGER, default 0 = off); returns the previous value (benchmarks, A/B)
-int mmt_gemm8_set_stagger(int units);
 
 /* ---- MX-fp8 primitives (C4's fp8 path; BASELINE configs[4]) --------------------------------
  * MX-fp8 = OCP e4m3fn bytes + one E8M0 exponent byte (bias 127) per 32 consecutive K elements of a

@@ -128,17 +128,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="-1,0,6")
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--stagger", default="", help="comma list of gemm8 stagger units (mmt_gemm8_set_stagger)")
     args = ap.parse_args()
-    staggers = [int(x) for x in args.stagger.split(",")] if args.stagger else [None]
-    for st in staggers:
-        if st is not None:
-            ML.lib().mmt_gemm8_set_stagger(st)
-        tag = "" if st is None else f" stagger {st}"
-        for v in [int(x, 0) for x in args.variants.split(",")]:
-            res = run(v, args.reps)
-            for k, (us, tf) in res.items():
-                print(f"variant {v}{tag}: {k:22s} {us:8.1f} us {tf:7.1f} TF/s", flush=True)
+    for v in [int(x, 0) for x in args.variants.split(",")]:
+        res = run(v, args.reps)
+        for k, (us, tf) in res.items():
+            print(f"variant {v}: {k:22s} {us:8.1f} us {tf:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,6 @@
 // 256 x 256 ping-pong bf16 GEMM for gfx950 (round 5; launched by mmt_gemm.hip's launch_t).
 #include "mmt_gemm_dev.h"
 
-#include <cstdlib>
 #include <type_traits>
 
 // ---------------------------------------------------------------------------------------------
@@ -95,8 +94,6 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmBatch batch) {
     const int x = tile % 8, q = nwg / 8, rr = nwg % 8;
     tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + tile / 8;
   }
-  if (batch.stagger > 0 && blockIdx.x < 256 && blockIdx.y == 0 && blockIdx.z == 0 && ((blockIdx.x >> 3) & 1))
-    for (int i = 0; i < batch.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   const GemmProblem& P = batch.p[prob];
   // (readfirstlane: keep them in SGPRs -- the compiler re-loads kernel-argument values inside the K loop
   // otherwise, and each such s_load's lgkmcnt(0) wait also drains the phase's LDS fragment reads)
@@ -225,25 +222,9 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmBatch batch) {
   epilogue_swap<TL, EPI, EPI_ROWS>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
 }
 
-static int g_gemm8_stagger = [] {
-  const char* e = getenv("MMT_GEMM8_STAGGER");
-  return e ? atoi(e) : 0;
-}();
-extern "C" int mmt_gemm8_set_stagger(int units) {
-  const int old = g_gemm8_stagger;
-  g_gemm8_stagger = units;
-  return old;
-}
-
 template <int EPI, bool A_KC, bool B_KC>
 static hipError_t launch8(const GemmBatch& b, dim3 grid, hipStream_t s) {
-  if (g_gemm8_stagger != b.stagger) {
-    GemmBatch bb = b;
-    bb.stagger = g_gemm8_stagger;
-    hipLaunchKernelGGL((gemm8_kernel<EPI, A_KC, B_KC>), grid, dim3(512), 0, s, bb);
-  } else {
-    hipLaunchKernelGGL((gemm8_kernel<EPI, A_KC, B_KC>), grid, dim3(512), 0, s, b);
-  }
+  hipLaunchKernelGGL((gemm8_kernel<EPI, A_KC, B_KC>), grid, dim3(512), 0, s, b);
   return hipGetLastError();
 }
 

@@ -100,9 +100,6 @@ struct GemmBatch {
   GemmProblem p[MMT_MAX_GROUP];
   int count;
   int xcd_plane;  // split-K launches: 1 = XCD-major remap of the whole (tile, split) plane
-  // gemm8_kernel: first-generation blocks on every other CU of an XCD sleep stagger x 127 x 64 cycles
-  // first, so the CUs' epilogue bursts stop lining up (set by its launcher; 0: off)
-  int stagger;
   // diagnostic builds only (-DMMT_GEMM_STAMPS, tools/gemm_stamps.py): per-block s_memtime stamps
   unsigned long long* stamps;
 };

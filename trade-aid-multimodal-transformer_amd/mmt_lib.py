@@ -87,7 +87,6 @@ _SIGS = {
     "mmt_attn_set_ring": (c_i32, [ctypes.c_int]),
     "mmt_emb_set_sort": (c_i32, [ctypes.c_int]),
     "mmt_qkv2_set_coal": (c_i32, [ctypes.c_int]),
-    "mmt_gemm8_set_stagger": (c_i32, [ctypes.c_int]),
     "mmt_gemm_set_variant": (c_i32, [ctypes.c_int]),
     "mmt_op_gemm": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp,
                             c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_f32]),
