@@ -286,6 +286,16 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
     gam0 = *reinterpret_cast<const f32x4*>(P.ln_gamma + n);
     gam1 = *reinterpret_cast<const f32x4*>(P.ln_gamma + n + 4);
   }
+  // the fused next-LayerNorm's weight and bias columns, once (loaded per row they were re-read after
+  // every row's stores, which the compiler cannot move them past)
+  constexpr bool LNF = EPI == EPI_BIAS_RESID_F32 && (GBN == 256 || GBN == 512);
+  f32x4 lg0 = {0.f, 0.f, 0.f, 0.f}, lg1 = lg0, lb0 = lg0, lb1 = lg0;
+  if (LNF && P.lnf_y && n + 8 <= N) {
+    lg0 = *reinterpret_cast<const f32x4*>(P.lnf_gamma + n);
+    lg1 = *reinterpret_cast<const f32x4*>(P.lnf_gamma + n + 4);
+    lb0 = *reinterpret_cast<const f32x4*>(P.lnf_beta + n);
+    lb1 = *reinterpret_cast<const f32x4*>(P.lnf_beta + n + 4);
+  }
   // 16-B vector accesses need bf16 leading dimensions % 8 and fp32 ones % 4 (bias pointers are
   // 64-B aligned by the parameter layout)
   const bool vec_ok = ((P.ldo16 | P.ldaux) & 7) == 0 && ((P.ldc | P.ldres) & 3) == 0;
@@ -314,6 +324,25 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
     }
   };
   if constexpr (HAS_AUX) load_aux(0);
+  // EPI_LN_BWD_F32: the operands of the next row this thread handles (LN input, accumulated gradient,
+  // row statistics) are loaded while it finishes the current one -- across pass boundaries too -- so
+  // the 16 row iterations of a tile expose one load latency instead of one each
+  struct LnRow { f32x4 x0, x1, d0, d1; float mu, rs; };
+  LnRow lnp = {};
+  auto ln_load = [&](int pass_, int it_) {
+    const int m = m0 + pass_ * EPI_ROWS + it_ * RPI + rsub;
+    if (m < M && n + 8 <= N) {
+      const float* xp = P.resid + (int64_t)m * P.ldres + n;
+      const float* dp = o32 + (int64_t)m * P.ldc + n;
+      lnp.x0 = *reinterpret_cast<const f32x4*>(xp);
+      lnp.x1 = *reinterpret_cast<const f32x4*>(xp + 4);
+      lnp.d0 = *reinterpret_cast<const f32x4*>(dp);
+      lnp.d1 = *reinterpret_cast<const f32x4*>(dp + 4);
+      lnp.mu = P.ln_mean[m];
+      lnp.rs = P.ln_rstd[m];
+    }
+  };
+  if constexpr (LNB) ln_load(0, 0);
   auto lds_barrier = [] {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -328,26 +357,19 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
     const int mb = m0 + pass * EPI_ROWS;
     if constexpr (LNB) {
       // a row's GBN columns are TPR = 32 consecutive threads (one half wave): row sums by 5 xor
-      // shuffles inside the half. Loads per row (all IT rows' loads up front spill next to the
-      // accumulators still live for the later passes)
+      // shuffles inside the half. One row's loads ahead (ln_load; all IT rows' loads up front spill
+      // next to the accumulators still live for the later passes)
       const float invn = 1.0f / (float)N;
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
         const int ml = it * RPI + rsub;
         const int m = mb + ml;
+        const LnRow cur = lnp;
+        if (it + 1 < IT) ln_load(pass, it + 1);
+        else if (pass + 1 < GBM / EPI_ROWS) ln_load(pass + 1, 0);
         if (m >= M) continue;  // a whole half wave (one row) at once: the shuffles stay inside it
-        f32x4 xv[1][2], dv[1][2];
-        float mu[1], rs[1];
-        {
-          const float* xp = P.resid + (int64_t)m * P.ldres + n;
-          const float* dp = o32 + (int64_t)m * P.ldc + n;
-          xv[0][0] = *reinterpret_cast<const f32x4*>(xp);
-          xv[0][1] = *reinterpret_cast<const f32x4*>(xp + 4);
-          dv[0][0] = *reinterpret_cast<const f32x4*>(dp);
-          dv[0][1] = *reinterpret_cast<const f32x4*>(dp + 4);
-          mu[0] = P.ln_mean[m];
-          rs[0] = P.ln_rstd[m];
-        }
+        const f32x4 xv[1][2] = {{cur.x0, cur.x1}}, dv[1][2] = {{cur.d0, cur.d1}};
+        const float mu[1] = {cur.mu}, rs[1] = {cur.rs};
         const f32x4 v0 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8);
         const f32x4 v1 = *reinterpret_cast<const f32x4*>(ct + ml * CT + 8 * c8 + 4);
         float dy[8], xh[8], gd[8];
@@ -518,10 +540,7 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
 #pragma unroll
             for (int o = 1; o < TPR; o <<= 1) q += __shfl_xor(q, o, 64);
             const float rstd = rsqrtf(q * (1.0f / (float)GBN) + 1e-5f);
-            const f32x4 g0 = *reinterpret_cast<const f32x4*>(P.lnf_gamma + n);
-            const f32x4 g1 = *reinterpret_cast<const f32x4*>(P.lnf_gamma + n + 4);
-            const f32x4 b0 = *reinterpret_cast<const f32x4*>(P.lnf_beta + n);
-            const f32x4 b1 = *reinterpret_cast<const f32x4*>(P.lnf_beta + n + 4);
+            const f32x4 g0 = lg0, g1 = lg1, b0 = lb0, b1 = lb1;
             float y[8];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {

@@ -33,6 +33,9 @@ struct MlpCfg {
   static constexpr int S1_ST = 3;
   static constexpr int S2_STAGE = N2 * MLP_BK * 2;              // W2 image per K-step
   static constexpr int S2_ST = 2;
+  // the forward's W2 ring: a third slot where it fits inside the stage-1 ring (C = 256), so two slices
+  // stream ahead of the stage-2 MFMAs
+  static constexpr int S2F_ST = 3 * S2_STAGE <= S1_ST * S1_STAGE ? 3 : 2;
   static constexpr int EPI_ROWS = 32;
   static constexpr int CTILE = EPI_ROWS * (N2 + 4) * 4;
   static constexpr int RING = cmax(cmax(S1_ST * S1_STAGE, S2_ST * S2_STAGE), CTILE);
@@ -137,20 +140,33 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
   auto issue2 = [&](int slot, int t) {
     issue_tile<BK, true, N2, 8>(rw2, lds + slot * CF::S2_STAGE, ldw2, N2, K2, 0, t * BK, wave, lane);
   };
+  constexpr int S2F = CF::S2F_ST;
+  // with the 3-slot ring the stage-1 bias is loaded before the W2 slices: loads issued after them would
+  // make the first wait for the bias drain the slices too (vmcnt counts in issue order). The 2-slot ring
+  // (C = 512) loads it in the epilogue as before (held across the barrier it measured 2-5 us slower)
+  f32x4 bvs[TN1][4];
+  if constexpr (S2F > 2) {
+#pragma unroll
+    for (int i = 0; i < TN1; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        bvs[i][g] = *reinterpret_cast<const f32x4*>(P1.bias + wn * TN1 * 32 + 32 * i + 8 * g + 4 * h);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // every wave's last stage-1 fragment reads are done: the ring is free
-  issue2(0, 0);
+#pragma unroll
+  for (int t = 0; t < S2F - 1; ++t)
+    if (t < nk2) issue2(t, t);
 
   // stage-1 epilogue: h = tanh(acc1 + b0) -> bf16 -> the LDS image (lane (r, h) of sub-tile (i, j) holds
   // rows m = wm 64 + 32 j + r, hidden n = wn TN1 32 + 32 i + 8 g + 4 h + e)
   {
-    const float* b0 = P1.bias;
 #pragma unroll
     for (int i = 0; i < TN1; ++i) {
       const int nb = wn * TN1 * 32 + 32 * i;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(b0 + nb + 8 * g + 4 * h);
+        const f32x4 bv = S2F > 2 ? bvs[i][g] : *reinterpret_cast<const f32x4*>(P1.bias + nb + 8 * g + 4 * h);
 #pragma unroll
         for (int j = 0; j < TM; ++j) {
           const int m = wm * 64 + 32 * j + r;
@@ -174,10 +190,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
     // (the h image is published by the first step's barrier)
     auto step2 = [&](int t, auto UC) {
       constexpr int U = decltype(UC)::value;
-      wait_vm(0);
+      wait_vm(PIECES2 * min(S2F - 2, nk2 - 1 - t));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // slice t landed for every wave; slice t - 1's reads are done
-      if (t + 1 < nk2) issue2(U ^ 1, t + 1);
+      if (t + S2F - 1 < nk2) issue2((U + S2F - 1) % S2F, t + S2F - 1);
       const char* imgW = lds + U * CF::S2_STAGE;
 #pragma unroll
       for (int s = 0; s < BK / 16; ++s) {
@@ -197,9 +213,12 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
       }
     };
 #pragma unroll
-    for (int t = 0; t < nk2; t += 2) {
+    for (int t = 0; t < nk2; t += S2F) {
       step2(t, std::integral_constant<int, 0>{});
       if (t + 1 < nk2) step2(t + 1, std::integral_constant<int, 1>{});
+      if constexpr (S2F > 2) {
+        if (t + 2 < nk2) step2(t + 2, std::integral_constant<int, (S2F > 2 ? 2 : 0)>{});
+      }
     }
   }
 
