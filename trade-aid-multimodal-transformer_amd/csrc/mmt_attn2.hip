@@ -449,21 +449,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
   const int prow = lane >> 1;
   const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
   const int per = 2 + (DROP && w == 0 ? 1 : 0);
-  auto issue = [&](int slot, int sl) {
+  // the issuing stream's K / V / keep-bit descriptors, rebuilt when the walk enters a new stream (built
+  // per slice, their kernel-argument loads put an s_load latency in front of every slice's DMA)
+  i32x4 rk, rv, rm;
+  int jr = -1;
+  auto set_stream = [&](int j) {
+    rk = make_rsrc(P.k[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+    rv = make_rsrc(P.v[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+    rm = make_rsrc(DROP ? P.dmask[j] + (ntiles + (int64_t)bh * ntri) * 32 : P.dmask[0], ntri * 128);
+    jr = j;
+  };
+  // the K / V row stride as a VGPR: as a kernel argument the compiler re-loaded it (s_load + a full
+  // lgkmcnt wait) in front of each slice's DMA pieces rather than keep it in an SGPR
+  int kvld = P.kv_ld;
+  asm volatile("" : "+v"(kvld));
+  auto issue = [&](int slot, int j, int kt) {  // slice (stream j, key tile kt)
     char* sb = lds + slot * SLOT;
-    const int j = sl / nk, kt = sl % nk;
     const int grow = kt * 32 + prow;
-    const i32x4 rk = make_rsrc(P.k[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
-    const i32x4 rv = make_rsrc(P.v[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+    if (j != jr) set_stream(j);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int piece = 2 * w + u;  // 0..3: K column block, 4..7: V
       const int op = piece >> 2, cb = piece & 3;
-      const int voff = grow < T ? (grow * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
+      const int voff = grow < T ? (grow * kvld + cb * 16 + pcol) * 2 : OOB;
       dma16(op ? rv : rk, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_V + cb * SUB)), voff);
     }
     if (DROP && w == 0) {  // lane words of (query tile 8 qb + u, key tile kt), u = 0..7: 8 x 128 B
-      const i32x4 rm = make_rsrc(P.dmask[j] + (ntiles + (int64_t)bh * ntri) * 32, ntri * 128);
       const int u = lane >> 3, q_ = 8 * qb + u;
       const int voff = (q_ < nt && kt <= q_) ? (q_ * (q_ + 1) / 2 + kt) * 128 + (lane & 7) * 16 : OOB;
       dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
@@ -471,7 +482,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
   };
 #pragma unroll
   for (int i = 0; i < S - 1; ++i)
-    if (i < nsl) issue(i, i);
+    if (i < nsl) issue(i, i / nk, i % nk);
 
   const int o_row = img_off(r, 0, h);
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -500,10 +511,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
       sa[e] = pv * __builtin_fmaf(dp, dsc, -dsum);  // dS^T
     }
     if (masked) {  // keys above the query (and past T) contribute nothing
+      const int tqv = tq[u];
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int key = kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (key > tq[u] || key >= T) sa[e] = 0.f;
+        if (key > tqv || key >= T) sa[e] = 0.f;
       }
     }
 #pragma unroll
@@ -515,13 +527,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ring64x2(AttnBatch batch, 
       for (int dt = 0; dt < ND; ++dt) dq[u][dt] = mfma32(ktr[s][dt], df, dq[u][dt]);
     }
   };
+  // slice indices kept as (stream, key tile) counters: no integer division per slice
+  int ji = (S - 1) / nk, kti = (S - 1) % nk, jc = 0, ktc = 0;
 #pragma unroll 1
   for (int i = 0; i < nsl; ++i) {
     wait_vm(per * min(S - 2, nsl - 1 - i));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (i + S - 1 < nsl) issue((i + S - 1) % S, i + S - 1);
-    const int j = i / nk, kt = i % nk;
+    if (i + S - 1 < nsl) {
+      issue((i + S - 1) % S, ji, kti);
+      if (++kti == nk) { kti = 0; ++ji; }
+    }
+    const int j = jc, kt = ktc;
+    if (++ktc == nk) { ktc = 0; ++jc; }
     // tile B (the later one) may lie past the sequence's last tile while A does not
     const bool needA = live[0] && kt <= qt[0], needB = live[1] && kt <= qt[1];
     if (needA || needB) {
@@ -618,21 +636,30 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ring64x2(AttnBatch batch, int
   const int prow = lane >> 1;
   const int pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
   const int per = 2 + (DROP && w == 0 ? 1 : 0);
-  auto issue = [&](int slot, int sl) {
+  // as the dQ pass: the issuing stream's descriptors rebuilt only when the walk enters a new stream,
+  // the K / V row stride in a VGPR (no kernel-argument loads in front of each slice's DMA)
+  i32x4 rk, rv, rm;
+  int jr = -1;
+  auto set_stream = [&](int j) {
+    rk = make_rsrc(P.k[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+    rv = make_rsrc(P.v[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+    rm = make_rsrc(DROP ? P.dmask[j] + (ntiles + (int64_t)bh * ntri) * 32 : P.dmask[0], ntri * 128);
+    jr = j;
+  };
+  int kvld = P.kv_ld;
+  asm volatile("" : "+v"(kvld));
+  auto issue = [&](int slot, int j, int kt) {  // slice (stream j, key tile kt)
     char* sb = lds + slot * SLOT;
-    const int j = sl / nk, kt = sl % nk;
     const int grow = kt * 32 + prow;
-    const i32x4 rk = make_rsrc(P.k[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
-    const i32x4 rv = make_rsrc(P.v[j] + rowbase * P.kv_ld + head * P.kv_hstride, (int64_t)T * P.kv_ld * 2);
+    if (j != jr) set_stream(j);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int piece = 2 * w + u;  // 0..3: K column block, 4..7: V
       const int op = piece >> 2, cb = piece & 3;
-      const int voff = grow < T ? (grow * P.kv_ld + cb * 16 + pcol) * 2 : OOB;
+      const int voff = grow < T ? (grow * kvld + cb * 16 + pcol) * 2 : OOB;
       dma16(op ? rv : rk, __builtin_amdgcn_readfirstlane(lds_u32(sb + op * OFF_V + cb * SUB)), voff);
     }
     if (DROP && w == 0) {  // lane words of (query tile 8 qb + u, key tile kt), u = 0..7: 8 x 128 B
-      const i32x4 rm = make_rsrc(P.dmask[j] + (ntiles + (int64_t)bh * ntri) * 32, ntri * 128);
       const int u = lane >> 3, q_ = 8 * qb + u;
       const int voff = (q_ < nt && kt <= q_) ? (q_ * (q_ + 1) / 2 + kt) * 128 + (lane & 7) * 16 : OOB;
       dma16(rm, __builtin_amdgcn_readfirstlane(lds_u32(sb + OFF_M)), voff);
@@ -640,7 +667,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ring64x2(AttnBatch batch, int
   };
 #pragma unroll
   for (int i = 0; i < S - 1; ++i)
-    if (i < nsl) issue(i, i);
+    if (i < nsl) issue(i, i / nk, i % nk);
 
   const int o_row = img_off(r, 0, h);
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -704,13 +731,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_ring64x2(AttnBatch batch, int
         for (int pr = 0; pr < 2; ++pr) *reinterpret_cast<u32x4*>(dst + dt * 32 + 16 * pr + 8 * h) = ov[dt][pr];
     }
   };
+  int ji = (S - 1) / nk, kti = (S - 1) % nk, jc = 0, ktc = 0;  // slice counters (no division per slice)
 #pragma unroll 1
   for (int i = 0; i < nsl; ++i) {
     wait_vm(per * min(S - 2, nsl - 1 - i));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (i + S - 1 < nsl) issue((i + S - 1) % S, i + S - 1);
-    const int j = i / nk, kt = i % nk;
+    if (i + S - 1 < nsl) {
+      issue((i + S - 1) % S, ji, kti);
+      if (++kti == nk) { kti = 0; ++ji; }
+    }
+    const int j = jc, kt = ktc;
+    if (++ktc == nk) { ktc = 0; ++jc; }
     if (kt == 0) {  // a stream's walk starts
 #pragma unroll
       for (int u = 0; u < 2; ++u) {

@@ -671,6 +671,8 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
   }();
   // (a 256 x 128 tile at two blocks per CU won standalone on the target ffn0, 214 -> 194 us, but not in
   // the step beside the side stream, 20.21 -> 20.37 ms: profiles/r3y_tilem_ab.txt; removed in round 4)
+  // (the ReLU' epilogue reading bits has no 16-B aux operand left, but at 3 blocks per CU it measured
+  // neutral: C1 8.558 vs 8.555, target 19.937 vs 19.935 ms, profiles/r5ac_drelu_occ3_ab.txt)
   const int var = EPI == EPI_ATOMIC_F32 ? g_gemm_variant_dw
                   : (!A_KC && !B_KC && env_dw >= 0) ? env_dw
                   : (g_gemm_variant >= 0 ? g_gemm_variant : occ3 ? MMT_OCC3_VARIANT : MMT_DEF_VARIANT);

@@ -309,8 +309,7 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
   // before the first staging: its HBM latency was exposed once per pass (ffn2 dX at the target: the
   // epilogue alone 110-150 us of a 260 us launch). The pass barriers are raw s_barriers behind an LDS
   // wait: __syncthreads() would also drain those loads (and the previous pass's stores) at every pass.
-  u32x4 auxn[IT];
-  uint32_t mskn[IT];  // EPI_DRELU_BF16 with mask8: the 8 ReLU bits of this thread's columns
+  u32x4 auxn[IT];  // (EPI_DRELU_BF16 with mask8: word 0 holds the 8 ReLU bits of this thread's columns)
   const bool use_m8 = EPI == EPI_DRELU_BF16 && P.mask8 != nullptr;
   auto load_aux = [&](int pass_) {
     if (!(n + 8 <= N && vec_ok)) return;
@@ -318,7 +317,7 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
     for (int it = 0; it < IT; ++it) {
       const int m = m0 + pass_ * EPI_ROWS + it * RPI + rsub;
       if (m < M) {
-        if (use_m8) mskn[it] = P.mask8[(int64_t)m * P.ldm8 + (n >> 3)];
+        if (use_m8) auxn[it][0] = P.mask8[(int64_t)m * P.ldm8 + (n >> 3)];
         else auxn[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
       }
     }
@@ -424,14 +423,10 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
     } else if (n + 8 <= N && vec_ok) {
       // issue every operand load of this thread's rows first (memory-level parallelism)
       u32x4 auxv[IT];
-      uint32_t mskv[IT];
       f32x4 resv[IT][2];
       if constexpr (HAS_AUX) {
 #pragma unroll
-        for (int it = 0; it < IT; ++it) {
-          auxv[it] = auxn[it];
-          mskv[it] = mskn[it];
-        }
+        for (int it = 0; it < IT; ++it) auxv[it] = auxn[it];
         if (pass + 1 < GBM / EPI_ROWS) load_aux(pass + 1);
       }
 #pragma unroll
@@ -470,7 +465,7 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
         if (HAS_AUX) {
           if (EPI == EPI_DRELU_BF16 && use_m8) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) r[e] = ((mskv[it] >> e) & 1u) ? r[e] : 0.0f;
+            for (int e = 0; e < 8; ++e) r[e] = ((auxv[it][0] >> e) & 1u) ? r[e] : 0.0f;
           } else {
             const u32x4 a = auxv[it];
 #pragma unroll
