@@ -22,7 +22,13 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.j
 
 # per-file flags: the attention softmax keeps scalar fp32 ops (packed v_pk_*_f32 issue slower
 # beside MFMAs, MI355X_MICROARCH.md), so the SLP vectoriser must not re-pack them
-FILE_FLAGS = {"mmt_attn.hip": ["-fno-slp-vectorize"], "mmt_attn2.hip": ["-fno-slp-vectorize"]}
+# mmt_attn.hip / mmt_qkv2.hip: MFMAs in the VGPR form. By default the compiler picks the AGPR form and then
+# reads every accumulator the loop consumes back with v_accvgpr_read (32 per tile in the hs-32 dK/dV pass,
+# 16 in the qkv2 backward): 213 -> 182 instructions per dK/dV tile, no spills, occupancy equal or higher.
+# Not for mmt_attn2.hip (the one-pass kernel needs 512 registers at one wave) or the GEMM files.
+VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+FILE_FLAGS = {"mmt_attn.hip": ["-fno-slp-vectorize"] + VGPR_FORM, "mmt_attn2.hip": ["-fno-slp-vectorize"],
+              "mmt_qkv2.hip": VGPR_FORM}
 
 
 def _deps_mtime():
