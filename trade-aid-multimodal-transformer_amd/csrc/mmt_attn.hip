@@ -871,7 +871,9 @@ __device__ __forceinline__ void dkdv_tile(const bf16_t* qs, const bf16_t* dos, c
           // Z.P without the 1/(1-p) (applied to dV at the end); dS = P (Z dP sc - D) = sc (Z P dP - P D'),
           // D' = D / sc (the dQ pass stores it so), the factor sc applied to dK at the end: one VALU
           // per element fewer than masking dP separately
-          const int kb = __builtin_amdgcn_sbfe((int)mw, 8 * g + e4 + u, 1);  // all ones iff kept
+          int kb = __builtin_amdgcn_sbfe((int)mw, 8 * g + e4 + u, 1);  // all ones iff kept
+          // (opaque to the compiler: seen as a one-bit test it lowered bfe + and into and + cmp + cndmask)
+          asm volatile("" : "+v"(kb));
           pm[u] = keep_f(pv, kb);
           ds[u] = __builtin_fmaf(pm[u], dp, pv * d4[g][e4 + u]);  // dS[q][key] / sc
         } else {
