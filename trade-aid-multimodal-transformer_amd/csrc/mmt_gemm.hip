@@ -221,7 +221,10 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
     prob = l2 / (gridDim.x * nsplit);
   }
   const GemmProblem& P = batch.p[prob];
-  const int M = P.M, N = P.N, K = P.K;
+  // (readfirstlane: values the compiler cannot rematerialise by re-loading the kernel argument; as plain
+  // P.* reads it re-loaded lda in front of every K-step's DMA, an s_load plus a full lgkmcnt wait)
+  const int M = __builtin_amdgcn_readfirstlane(P.M), N = __builtin_amdgcn_readfirstlane(P.N);
+  const int K = __builtin_amdgcn_readfirstlane(P.K);
   const int tiles_n = (N + GBN - 1) / GBN;
   const int tiles_m = (M + GBM - 1) / GBM;
   const int ntiles = tiles_m * tiles_n;
@@ -283,12 +286,21 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   }
 
   if (ks0 < ks1) {
+    const int lda = __builtin_amdgcn_readfirstlane(P.lda), ldb = __builtin_amdgcn_readfirstlane(P.ldb);
+    // (the operand base pointers likewise: an MN-contiguous operand's descriptor is rebuilt per K-step)
+    auto sgpr_ptr = [](const bf16_t* q) {
+      const uint64_t v = (uint64_t)(uintptr_t)q;
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+      return (const bf16_t*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    };
+    const bf16_t* const Ap = sgpr_ptr(P.A);
+    const bf16_t* const Bp = sgpr_ptr(P.B);
     // buffer descriptors (range-checked: OOB pieces read 0) from the tile's first row for a
     // K-contiguous operand; an MN-contiguous operand's descriptor is made per K-step (op_rsrc)
-    const i32x4 ra_kc = A_KC ? op_rsrc<true>(P.A, P.lda, M, K, m0, 0) : i32x4{0, 0, 0, 0};
-    const i32x4 rb_kc = B_KC ? op_rsrc<true>(P.B, P.ldb, N, K, n0, 0) : i32x4{0, 0, 0, 0};
-    auto ra = [&](int k0) { return A_KC ? ra_kc : op_rsrc<false>(P.A, P.lda, M, K, m0, k0); };
-    auto rb = [&](int k0) { return B_KC ? rb_kc : op_rsrc<false>(P.B, P.ldb, N, K, n0, k0); };
+    const i32x4 ra_kc = A_KC ? op_rsrc<true>(Ap, lda, M, K, m0, 0) : i32x4{0, 0, 0, 0};
+    const i32x4 rb_kc = B_KC ? op_rsrc<true>(Bp, ldb, N, K, n0, 0) : i32x4{0, 0, 0, 0};
+    auto ra = [&](int k0) { return A_KC ? ra_kc : op_rsrc<false>(Ap, lda, M, K, m0, k0); };
+    auto rb = [&](int k0) { return B_KC ? rb_kc : op_rsrc<false>(Bp, ldb, N, K, n0, k0); };
     const int nk = ks1 - ks0;
     // one K-step: stage U of the ring holds K-step tt (tt % ST == U), the step prefetches K-step
     // tt + ST - 1 into stage (U + ST - 1) % ST. U is a compile-time constant (the loop below is
@@ -305,8 +317,8 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
       if (tt + ST - 1 < nk) {
         char* st = lds + ((U + ST - 1) % ST) * STAGE_BYTES;
         const int k0 = (ks0 + tt + ST - 1) * BK;
-        issue_tile<BK, A_KC, GBM, NW>(ra(k0), st, P.lda, M, K, m0, k0, wave, lane);
-        issue_tile<BK, B_KC, GBN, NW>(rb(k0), st + IMG_A, P.ldb, N, K, n0, k0, wave, lane);
+        issue_tile<BK, A_KC, GBM, NW>(ra(k0), st, lda, M, K, m0, k0, wave, lane);
+        issue_tile<BK, B_KC, GBN, NW>(rb(k0), st + IMG_A, ldb, N, K, n0, k0, wave, lane);
       }
       const char* imgA = lds + U * STAGE_BYTES;
       const char* imgB = imgA + IMG_A;
@@ -331,8 +343,8 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
       if (t < nk) {
         char* st = lds + t * STAGE_BYTES;
         const int k0 = (ks0 + t) * BK;
-        issue_tile<BK, A_KC, GBM, NW>(ra(k0), st, P.lda, M, K, m0, k0, wave, lane);
-        issue_tile<BK, B_KC, GBN, NW>(rb(k0), st + IMG_A, P.ldb, N, K, n0, k0, wave, lane);
+        issue_tile<BK, A_KC, GBM, NW>(ra(k0), st, lda, M, K, m0, k0, wave, lane);
+        issue_tile<BK, B_KC, GBN, NW>(rb(k0), st + IMG_A, ldb, N, K, n0, k0, wave, lane);
       }
     GEMM_STAMP(1);
     int t = 0;
@@ -825,6 +837,10 @@ struct SlabBatch {
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SlabBatch b) {
   const SlabProblem& P = b.p[blockIdx.y];
   const bool vec = (P.N % 4 == 0) && (P.ldc % 4 == 0) && (((uintptr_t)P.out & 15) == 0);
+  // kernel arguments the split loop reads, as values (read through P they were re-loaded per split group)
+  const int splits = __builtin_amdgcn_readfirstlane(b.splits);
+  const int64_t stride = P.stride;
+  const float* const slab = P.slab;
   if (vec) {
     const int64_t n4 = (int64_t)P.M * P.N / 4;
     const int N4 = P.N / 4;
@@ -834,11 +850,11 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(SlabBatch b) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
       int sp = 0;
-      for (; sp + 8 <= b.splits; sp += 8) {
+      for (; sp + 8 <= splits; sp += 8) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) part[u] += reinterpret_cast<const f32x4*>(P.slab + (sp + u) * P.stride)[i];
+        for (int u = 0; u < 8; ++u) part[u] += reinterpret_cast<const f32x4*>(slab + (sp + u) * stride)[i];
       }
-      for (; sp < b.splits; ++sp) part[0] += reinterpret_cast<const f32x4*>(P.slab + sp * P.stride)[i];
+      for (; sp < splits; ++sp) part[0] += reinterpret_cast<const f32x4*>(slab + sp * stride)[i];
       const f32x4 acc = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
       const int m = (int)(i / N4), c = (int)(i % N4) * 4;
       float* o = P.out + (int64_t)m * P.ldc + c;
