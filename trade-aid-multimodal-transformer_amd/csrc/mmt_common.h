@@ -84,6 +84,18 @@ __device__ __forceinline__ bf16x8 join4(s16x4 lo, s16x4 hi) {
 // give each XCD a contiguous run of logical tiles so neighbouring tiles that read the two halves of
 // the same cache lines (adjacent heads / Q-K-V blocks of one row) run on one XCD at nearly the
 // same time. Returns the logical tile of hardware block `bid` out of `nwg`.
+// Kernel-argument values pinned as wave-uniform VALUES (readfirstlane): read through the kernel-argument
+// struct inside a loop, hipcc re-loads them (s_load + an lgkmcnt wait) every iteration instead of keeping
+// them in SGPRs
+template <class T>
+__device__ __forceinline__ T* sgpr_ptr(T* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t sgpr_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ float sgpr_f32(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+
 __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
   const int x = bid % 8, q = nwg / 8, rr = nwg % 8;
   return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + bid / 8;

@@ -481,6 +481,8 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(EmbBatch batch, int R, 
   }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   int cur = __builtin_amdgcn_readlane(mytok, 0);
+  const float* const dx = sgpr_ptr(P.dx);
+  float* const dtok = sgpr_ptr(P.dtok);
   constexpr int U = 8;  // rows in flight
   for (int k0 = 0; k0 < n; k0 += U) {
     f32x4 v[U];
@@ -488,7 +490,7 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(EmbBatch batch, int R, 
     for (int u = 0; u < U; ++u) {
       const int k = k0 + u;
       const int row = __builtin_amdgcn_readlane(myrow, k < n ? k : 0);
-      v[u] = (k < n && col_ok) ? reinterpret_cast<const f32x4*>(P.dx + (int64_t)row * C)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
+      v[u] = (k < n && col_ok) ? reinterpret_cast<const f32x4*>(dx + (int64_t)row * C)[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -497,7 +499,7 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(EmbBatch batch, int R, 
       const int t = __builtin_amdgcn_readlane(mytok, k);
       if (t != cur) {  // wave-uniform: a run of token cur ends
         if (col_ok) {
-          float* d = P.dtok + (int64_t)cur * C + 4 * c4;
+          float* d = dtok + (int64_t)cur * C + 4 * c4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) atomicAdd(d + e, acc[e]);
         }
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(EmbBatch batch, int R, 
     }
   }
   if (col_ok) {
-    float* d = P.dtok + (int64_t)cur * C + 4 * c4;
+    float* d = dtok + (int64_t)cur * C + 4 * c4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) atomicAdd(d + e, acc[e]);
   }
@@ -822,6 +824,10 @@ __global__ __launch_bounds__(256) void drop_copy_kernel(DropCopyBatch batch, int
   constexpr int RPI = 4;  // rows per wave per iteration, loads issued together
   __shared__ float red[4][1024];
   const int stride = gridDim.x * 4;
+  const f32x4* const src = reinterpret_cast<const f32x4*>(sgpr_ptr(P.src));
+  u32x2* const dst = reinterpret_cast<u32x2*>(sgpr_ptr(P.dst));
+  const uint32_t dkey = sgpr_u32(P.drop_key), dthr = sgpr_u32(P.drop_thr);
+  const float dscale = sgpr_f32(P.drop_scale);
   for (int cb = 0; cb < C4; cb += 64) {
     const int q = cb + lane;
     f32x4 sm = {0.f, 0.f, 0.f, 0.f};
@@ -831,21 +837,21 @@ __global__ __launch_bounds__(256) void drop_copy_kernel(DropCopyBatch batch, int
 #pragma unroll
         for (int u = 0; u < RPI; ++u) {
           const int row = row0 + u * stride;
-          o[u] = row < R ? reinterpret_cast<const f32x4*>(P.src)[(int64_t)row * C4 + q] : f32x4{0.f, 0.f, 0.f, 0.f};
+          o[u] = row < R ? src[(int64_t)row * C4 + q] : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int u = 0; u < RPI; ++u) {
           const int row = row0 + u * stride;
           if (row >= R) break;
-          if (P.drop_thr) {
+          if (dthr) {
 #pragma unroll
             for (int pq = 0; pq < 2; ++pq) {
-              const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)row, (uint32_t)(2 * q + pq));
-              o[u][2 * pq] = mmt_keep(hq, 0, P.drop_thr) ? o[u][2 * pq] * P.drop_scale : 0.f;
-              o[u][2 * pq + 1] = mmt_keep(hq, 1, P.drop_thr) ? o[u][2 * pq + 1] * P.drop_scale : 0.f;
+              const uint32_t hq = mmt_hash(dkey, (uint32_t)row, (uint32_t)(2 * q + pq));
+              o[u][2 * pq] = mmt_keep(hq, 0, dthr) ? o[u][2 * pq] * dscale : 0.f;
+              o[u][2 * pq + 1] = mmt_keep(hq, 1, dthr) ? o[u][2 * pq + 1] * dscale : 0.f;
             }
           }
-          reinterpret_cast<u32x2*>(P.dst)[(int64_t)row * C4 + q] =
+          dst[(int64_t)row * C4 + q] =
               u32x2{pack2bf(o[u][0], o[u][1]), pack2bf(o[u][2], o[u][3])};
           sm += o[u];
         }

@@ -298,6 +298,43 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
   }
   // 16-B vector accesses need bf16 leading dimensions % 8 and fp32 ones % 4 (bias pointers are
   // 64-B aligned by the parameter layout)
+  // the kernel-argument fields the row loops read, pinned as wave-uniform values: read through P,
+  // hipcc re-loaded them (s_load + lgkmcnt wait) in every row iteration -- up to 40 scalar loads per
+  // pass in the LayerNorm-backward and ReLU epilogues. Not for the residual / accumulate epilogues
+  // (pinned, the residual + LayerNorm-forward one spilled 40 VGPRs and the accumulate one re-loaded
+  // more) nor ReLU' (its bf16-aux form measured 101 -> 117 us standalone at C1 pinned)
+  // (EA(f): the pinned copy, or P.f read as before)
+  constexpr bool PIN = !(EPI == EPI_BIAS_RESID_F32 || EPI == EPI_ACC_F32 || EPI == EPI_DRELU_BF16);
+  struct {
+    const float* resid; int ldres, ldc; bf16_t* o16; int ldo16; const bf16_t* aux; int ldaux;
+    uint32_t drop_key, drop_thr; float drop_scale; uint8_t* mask8; int ldm8;
+    const float* ln_mean; const float* ln_rstd; bf16_t* lnf_y; float* lnf_mean; float* lnf_rstd;
+    uint8_t* o8; uint8_t* s8; int ld8, lds8;
+  } ea{};
+  if constexpr (PIN) {
+    ea.resid = sgpr_ptr(P.resid);
+    ea.ldres = __builtin_amdgcn_readfirstlane(P.ldres);
+    ea.ldc = __builtin_amdgcn_readfirstlane(P.ldc);
+    ea.o16 = sgpr_ptr(P.o16);
+    ea.ldo16 = __builtin_amdgcn_readfirstlane(P.ldo16);
+    ea.aux = sgpr_ptr(P.aux);
+    ea.ldaux = __builtin_amdgcn_readfirstlane(P.ldaux);
+    ea.drop_key = sgpr_u32(P.drop_key);
+    ea.drop_thr = sgpr_u32(P.drop_thr);
+    ea.drop_scale = sgpr_f32(P.drop_scale);
+    ea.mask8 = sgpr_ptr(P.mask8);
+    ea.ldm8 = __builtin_amdgcn_readfirstlane(P.ldm8);
+    ea.ln_mean = sgpr_ptr(P.ln_mean);
+    ea.ln_rstd = sgpr_ptr(P.ln_rstd);
+    ea.lnf_y = sgpr_ptr(P.lnf_y);
+    ea.lnf_mean = sgpr_ptr(P.lnf_mean);
+    ea.lnf_rstd = sgpr_ptr(P.lnf_rstd);
+    ea.o8 = sgpr_ptr(P.o8);
+    ea.s8 = sgpr_ptr(P.s8);
+    ea.ld8 = __builtin_amdgcn_readfirstlane(P.ld8);
+    ea.lds8 = __builtin_amdgcn_readfirstlane(P.lds8);
+  }
+#define EA(f) (PIN ? ea.f : P.f)
   const bool vec_ok = ((P.ldo16 | P.ldaux) & 7) == 0 && ((P.ldc | P.ldres) & 3) == 0;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x4 bias0 = {0.f, 0.f, 0.f, 0.f}, bias1 = {0.f, 0.f, 0.f, 0.f};
@@ -317,8 +354,8 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
     for (int it = 0; it < IT; ++it) {
       const int m = m0 + pass_ * EPI_ROWS + it * RPI + rsub;
       if (m < M) {
-        if (use_m8) auxn[it][0] = P.mask8[(int64_t)m * P.ldm8 + (n >> 3)];
-        else auxn[it] = *reinterpret_cast<const u32x4*>(P.aux + (int64_t)m * P.ldaux + n);
+        if (use_m8) auxn[it][0] = EA(mask8)[(int64_t)m * EA(ldm8) + (n >> 3)];
+        else auxn[it] = *reinterpret_cast<const u32x4*>(EA(aux) + (int64_t)m * EA(ldaux) + n);
       }
     }
   };
@@ -331,14 +368,14 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
   auto ln_load = [&](int pass_, int it_) {
     const int m = m0 + pass_ * EPI_ROWS + it_ * RPI + rsub;
     if (m < M && n + 8 <= N) {
-      const float* xp = P.resid + (int64_t)m * P.ldres + n;
-      const float* dp = o32 + (int64_t)m * P.ldc + n;
+      const float* xp = EA(resid) + (int64_t)m * EA(ldres) + n;
+      const float* dp = o32 + (int64_t)m * EA(ldc) + n;
       lnp.x0 = *reinterpret_cast<const f32x4*>(xp);
       lnp.x1 = *reinterpret_cast<const f32x4*>(xp + 4);
       lnp.d0 = *reinterpret_cast<const f32x4*>(dp);
       lnp.d1 = *reinterpret_cast<const f32x4*>(dp + 4);
-      lnp.mu = P.ln_mean[m];
-      lnp.rs = P.ln_rstd[m];
+      lnp.mu = EA(ln_mean)[m];
+      lnp.rs = EA(ln_rstd)[m];
     }
   };
   if constexpr (LNB) ln_load(0, 0);
@@ -402,19 +439,19 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
           r[e] = dv[0][0][e] + rs[0] * (gd[e] - s1 - xh[e] * s2);
           r[e + 4] = dv[0][1][e] + rs[0] * (gd[e + 4] - s1 - xh[e + 4] * s2);
         }
-        float* op = o32 + (int64_t)m * P.ldc + n;
+        float* op = o32 + (int64_t)m * EA(ldc) + n;
         *reinterpret_cast<f32x4*>(op) = f32x4{r[0], r[1], r[2], r[3]};
         *reinterpret_cast<f32x4*>(op + 4) = f32x4{r[4], r[5], r[6], r[7]};
-        if (P.o16) {
-          if (P.drop_thr) {
+        if (EA(o16)) {
+          if (EA(drop_thr)) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {  // n is even: one hash per column pair (as ln_bwd_kernel)
-              const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n >> 1) + q);
-              r[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? r[2 * q] * P.drop_scale : 0.0f;
-              r[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? r[2 * q + 1] * P.drop_scale : 0.0f;
+              const uint32_t hq = mmt_hash(EA(drop_key), (uint32_t)m, (uint32_t)(n >> 1) + q);
+              r[2 * q] = mmt_keep(hq, 0, EA(drop_thr)) ? r[2 * q] * EA(drop_scale) : 0.0f;
+              r[2 * q + 1] = mmt_keep(hq, 1, EA(drop_thr)) ? r[2 * q + 1] * EA(drop_scale) : 0.0f;
             }
           }
-          *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+          *reinterpret_cast<u32x4*>(EA(o16) + (int64_t)m * EA(ldo16) + n) =
               u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[e] += r[e];
@@ -433,8 +470,8 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
       for (int it = 0; it < IT; ++it) {
         const int m = mb + it * RPI + rsub;
         if (m < M) {
-          const float* rp = EPI == EPI_BIAS_RESID_F32 ? P.resid + (int64_t)m * P.ldres + n
-                                                      : o32 + (int64_t)m * P.ldc + n;
+          const float* rp = EPI == EPI_BIAS_RESID_F32 ? EA(resid) + (int64_t)m * EA(ldres) + n
+                                                      : o32 + (int64_t)m * EA(ldc) + n;
           if (HAS_RES) {
             resv[it][0] = *reinterpret_cast<const f32x4*>(rp);
             resv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
@@ -481,12 +518,12 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
             }
           }
         }
-        if (EPI == EPI_BIAS_RESID_F32 && P.drop_thr) {  // dropout on the branch output, then residual add
+        if (EPI == EPI_BIAS_RESID_F32 && EA(drop_thr)) {  // dropout on the branch output, then residual add
 #pragma unroll
           for (int q = 0; q < 4; ++q) {  // n is even: one hash per column pair
-            const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n >> 1) + q);
-            r[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? r[2 * q] * P.drop_scale : 0.0f;
-            r[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? r[2 * q + 1] * P.drop_scale : 0.0f;
+            const uint32_t hq = mmt_hash(EA(drop_key), (uint32_t)m, (uint32_t)(n >> 1) + q);
+            r[2 * q] = mmt_keep(hq, 0, EA(drop_thr)) ? r[2 * q] * EA(drop_scale) : 0.0f;
+            r[2 * q + 1] = mmt_keep(hq, 1, EA(drop_thr)) ? r[2 * q + 1] * EA(drop_scale) : 0.0f;
           }
         }
         if (HAS_RES) {
@@ -497,29 +534,29 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
           }
         }
         if (EPI == EPI_BIAS_RESID_F32 || EPI == EPI_STORE_F32 || EPI == EPI_ACC_F32) {
-          float* op = o32 + (int64_t)m * P.ldc + n;
+          float* op = o32 + (int64_t)m * EA(ldc) + n;
           *reinterpret_cast<f32x4*>(op) = f32x4{r[0], r[1], r[2], r[3]};
           *reinterpret_cast<f32x4*>(op + 4) = f32x4{r[4], r[5], r[6], r[7]};
-          if (EPI == EPI_BIAS_RESID_F32 && P.o16)
-            *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+          if (EPI == EPI_BIAS_RESID_F32 && EA(o16))
+            *reinterpret_cast<u32x4*>(EA(o16) + (int64_t)m * EA(ldo16) + n) =
                 u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
-          if (EPI == EPI_ACC_F32 && P.o16) {
+          if (EPI == EPI_ACC_F32 && EA(o16)) {
             // the dropout-masked bf16 copy of the accumulated rows (the consuming branch's dY) and
             // its column sums (that branch's output-bias gradient), as drop_copy_kernel
-            if (P.drop_thr) {
+            if (EA(drop_thr)) {
 #pragma unroll
               for (int q = 0; q < 4; ++q) {  // n is even: one hash per column pair
-                const uint32_t hq = mmt_hash(P.drop_key, (uint32_t)m, (uint32_t)(n >> 1) + q);
-                r[2 * q] = mmt_keep(hq, 0, P.drop_thr) ? r[2 * q] * P.drop_scale : 0.0f;
-                r[2 * q + 1] = mmt_keep(hq, 1, P.drop_thr) ? r[2 * q + 1] * P.drop_scale : 0.0f;
+                const uint32_t hq = mmt_hash(EA(drop_key), (uint32_t)m, (uint32_t)(n >> 1) + q);
+                r[2 * q] = mmt_keep(hq, 0, EA(drop_thr)) ? r[2 * q] * EA(drop_scale) : 0.0f;
+                r[2 * q + 1] = mmt_keep(hq, 1, EA(drop_thr)) ? r[2 * q + 1] * EA(drop_scale) : 0.0f;
               }
             }
-            *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) =
+            *reinterpret_cast<u32x4*>(EA(o16) + (int64_t)m * EA(ldo16) + n) =
                 u32x4{pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
 #pragma unroll
             for (int e = 0; e < 8; ++e) cs[e] += r[e];
           }
-          if (EPI == EPI_BIAS_RESID_F32 && (GBN == 256 || GBN == 512) && P.lnf_y) {
+          if (EPI == EPI_BIAS_RESID_F32 && (GBN == 256 || GBN == 512) && EA(lnf_y)) {
             // the next LayerNorm on this row (whole rows per block: N == GBN, mmt_launch_gemm_resid_ln;
             // lnf_y is uniform per problem and m < M per half wave, so every lane of the row's half
             // wave takes the shuffles): mean, then the centred sum of squares (as ln_fwd_kernel)
@@ -542,14 +579,14 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
               y[e] = (r[e] - mean) * rstd * g0[e] + b0[e];
               y[e + 4] = (r[e + 4] - mean) * rstd * g1[e] + b1[e];
             }
-            *reinterpret_cast<u32x4*>(P.lnf_y + (int64_t)m * N + n) =
+            *reinterpret_cast<u32x4*>(EA(lnf_y) + (int64_t)m * N + n) =
                 u32x4{pack2bf(y[0], y[1]), pack2bf(y[2], y[3]), pack2bf(y[4], y[5]), pack2bf(y[6], y[7])};
-            if (c8 == 0) { P.lnf_mean[m] = mean; P.lnf_rstd[m] = rstd; }
+            if (c8 == 0) { EA(lnf_mean)[m] = mean; EA(lnf_rstd)[m] = rstd; }
           }
         } else {
           const u32x4 packed = {pack2bf(r[0], r[1]), pack2bf(r[2], r[3]), pack2bf(r[4], r[5]), pack2bf(r[6], r[7])};
-          *reinterpret_cast<u32x4*>(P.o16 + (int64_t)m * P.ldo16 + n) = packed;
-          if (EPI == EPI_BIAS_RELU_BF16 && P.mask8) {  // bit e: the stored bf16 value is > 0
+          *reinterpret_cast<u32x4*>(EA(o16) + (int64_t)m * EA(ldo16) + n) = packed;
+          if (EPI == EPI_BIAS_RELU_BF16 && EA(mask8)) {  // bit e: the stored bf16 value is > 0
             uint32_t mb = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -560,17 +597,17 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
             // 8 consecutive threads (one row, 64 columns) join their bytes: one 8-byte store instead
             // of eight byte stores (byte stores cost ffn0 8 % at the target)
             const int g0 = n - 8 * (c8 & 7);  // first column of this thread's group
-            if (g0 + 64 <= N && (P.ldm8 & 7) == 0) {  // uniform across the group
+            if (g0 + 64 <= N && (EA(ldm8) & 7) == 0) {  // uniform across the group
               uint32_t wv = mb;
               wv |= (uint32_t)__shfl_down((int)wv, 1, 64) << 8;
               wv |= (uint32_t)__shfl_down((int)wv, 2, 64) << 16;
               const uint32_t w2 = (uint32_t)__shfl_down((int)wv, 4, 64);
-              if ((c8 & 7) == 0) *reinterpret_cast<u32x2*>(P.mask8 + (int64_t)m * P.ldm8 + (g0 >> 3)) = u32x2{wv, w2};
+              if ((c8 & 7) == 0) *reinterpret_cast<u32x2*>(EA(mask8) + (int64_t)m * EA(ldm8) + (g0 >> 3)) = u32x2{wv, w2};
             } else {
-              P.mask8[(int64_t)m * P.ldm8 + (n >> 3)] = (uint8_t)mb;
+              EA(mask8)[(int64_t)m * EA(ldm8) + (n >> 3)] = (uint8_t)mb;
             }
           }
-          if (MX_OUT && P.o8) {
+          if (MX_OUT && EA(o8)) {
             // MX-fp8 copy: the 32-column block of this row is 4 consecutive threads (c8 & ~3)
             float am = 0.f;
 #pragma unroll
@@ -579,10 +616,10 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
             am = fmaxf(am, __shfl_xor(am, 2, 64));
             const int ex = mx_exp(am);
             const float inv = mx_inv(ex);
-            *reinterpret_cast<u32x2*>(P.o8 + (int64_t)m * P.ld8 + n) =
+            *reinterpret_cast<u32x2*>(EA(o8) + (int64_t)m * EA(ld8) + n) =
                 u32x2{pack4fp8(r[0] * inv, r[1] * inv, r[2] * inv, r[3] * inv),
                       pack4fp8(r[4] * inv, r[5] * inv, r[6] * inv, r[7] * inv)};
-            if ((c8 & 3) == 0) P.s8[(int64_t)m * P.lds8 + (n >> 5)] = (uint8_t)(ex + 127);
+            if ((c8 & 3) == 0) EA(s8)[(int64_t)m * EA(lds8) + (n >> 5)] = (uint8_t)(ex + 127);
           }
           if (CAN_DB) {
 #pragma unroll
@@ -608,13 +645,14 @@ __device__ __forceinline__ void epilogue_swap(const GemmProblem& P, ACC& acc, ch
             epi_pad<EPI>(P, m, n + e);
           }
         }
-        if (EPI == EPI_BIAS_RELU_BF16 && P.mask8) P.mask8[(int64_t)m * P.ldm8 + (n >> 3)] = (uint8_t)mb;
+        if (EPI == EPI_BIAS_RELU_BF16 && EA(mask8)) EA(mask8)[(int64_t)m * EA(ldm8) + (n >> 3)] = (uint8_t)mb;
       }
     }
   }
   // column sums: rows of a column group live in lanes l, l^TPR, ... of every wave: fold those, then
   // the waves via LDS (the staged tile is dead: every thread has read its own rows), one atomic per
   // column
+#undef EA
   auto flush_colsums = [&](float (&v)[8], float* dst) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)

@@ -341,6 +341,13 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
   constexpr int CPR = HS / 8, RPI = 64 / CPR;  // COAL: dout chunks per row, rows per load instruction
   constexpr int HPR = HH / 8, HRPI = 64 / HPR;  // the same for h1 / dh1
   static_assert(!COAL || (KSO * RPI == 32 && NI * HRPI == 32), "coalesced loads cover the 32-row tile");
+  // kernel arguments of the tile loop pinned (read through P they were re-loaded on every tile)
+  const bf16_t* const dout = sgpr_ptr(P.dout);
+  const bf16_t* const h1 = sgpr_ptr(P.h1);
+  bf16_t* const dh1 = sgpr_ptr(P.dh1);
+  ld_h1 = __builtin_amdgcn_readfirstlane(ld_h1);
+  ld_out = __builtin_amdgcn_readfirstlane(ld_out);
+  R = __builtin_amdgcn_readfirstlane(R);
   u32x4 dv[KSO], hv[NI];
   auto load = [&](int row0) {  // row0: the tile's first row
     const u32x4 zz = {0u, 0u, 0u, 0u};
@@ -348,19 +355,19 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
 #pragma unroll
       for (int s = 0; s < KSO; ++s) {
         const int rr = row0 + s * RPI + lane / CPR;
-        dv[s] = rr < R ? *reinterpret_cast<const u32x4*>(P.dout + (int64_t)rr * ld_out + blk * HS + 8 * (lane % CPR)) : zz;
+        dv[s] = rr < R ? *reinterpret_cast<const u32x4*>(dout + (int64_t)rr * ld_out + blk * HS + 8 * (lane % CPR)) : zz;
       }
 #pragma unroll
       for (int q = 0; q < NI; ++q) {
         const int rr = row0 + q * HRPI + lane / HPR;
-        hv[q] = rr < R ? *reinterpret_cast<const u32x4*>(P.h1 + (int64_t)rr * ld_h1 + blk * HH + 8 * (lane % HPR)) : zz;
+        hv[q] = rr < R ? *reinterpret_cast<const u32x4*>(h1 + (int64_t)rr * ld_h1 + blk * HH + 8 * (lane % HPR)) : zz;
       }
       return;
     }
     const int row = row0 + r;
     const bool ok = row < R;
-    const bf16_t* d = P.dout + (int64_t)row * ld_out + blk * HS + 8 * h;
-    const bf16_t* hp = P.h1 + (int64_t)row * ld_h1 + blk * HH + 8 * h;
+    const bf16_t* d = dout + (int64_t)row * ld_out + blk * HS + 8 * h;
+    const bf16_t* hp = h1 + (int64_t)row * ld_h1 + blk * HH + 8 * h;
 #pragma unroll
     for (int s = 0; s < KSO; ++s) dv[s] = ok ? *reinterpret_cast<const u32x4*>(d + 16 * s) : zz;
 #pragma unroll
@@ -412,7 +419,7 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[8 * q + e] += t8[e];
         if (!(COAL && HPR >= 4))
-          *reinterpret_cast<u32x4*>(P.dh1 + (int64_t)row * ld_h1 + blk * HH + 16 * q + 8 * h) = dz[q];
+          *reinterpret_cast<u32x4*>(dh1 + (int64_t)row * ld_h1 + blk * HH + 16 * q + 8 * h) = dz[q];
       }
     }
     // dW2 over this tile's 32 rows: LDS images (rows past R hold zeros: their loads returned 0)
@@ -447,7 +454,7 @@ __global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int l
       for (int q = 0; q < NI; ++q) {
         const int rr = r0 + 32 * t + q * HRPI + lane / HPR;
         const u32x4 v = *reinterpret_cast<const u32x4*>(himg + q2_swz(q * HRPI + lane / HPR, lane % HPR));
-        if (rr < R) *reinterpret_cast<u32x4*>(P.dh1 + (int64_t)rr * ld_h1 + blk * HH + 8 * (lane % HPR)) = v;
+        if (rr < R) *reinterpret_cast<u32x4*>(dh1 + (int64_t)rr * ld_h1 + blk * HH + 8 * (lane % HPR)) = v;
       }
     }
   }
