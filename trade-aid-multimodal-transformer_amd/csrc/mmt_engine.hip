@@ -839,10 +839,12 @@ struct Runner {
 // forward
 // -------------------------------------------------------------------------------------------
 // the FFN's ReLU' as bits written by ffn0 (16x fewer bytes than the bf16 hidden the ffn2 data
-// gradient read back; MMT_RELU_BITS=0: the bf16 aux)
+// gradient reads back). MMT_RELU_BITS=1 turns it on; off by default: on the final round-5 build the
+// bf16 aux measured faster (same box, profiles/r5am_relu_bits_final_ab.txt: C1 8.502 -> 8.477 ms,
+// target 19.770 -> 19.505 ms), where the first version had been 0.1-0.7 % faster than the aux
 static const bool relu_bits = [] {
   const char* e = getenv("MMT_RELU_BITS");
-  return e ? atoi(e) != 0 : true;
+  return e ? atoi(e) != 0 : false;
 }();
 
 int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t* const* tgt, float* const* logits,
