@@ -16,9 +16,9 @@ batch per GPU). Launched by torch.distributed.run (the driver's line), or, when 
 given without it, this process starts that launcher itself (launch_plan) before touching a GPU.
 
 Roofline: the engine times every launch matching the probe patterns (default: all weight-gradient
-GEMMs, attention forward / backward, ffn0, the ffn2 data gradient) with HIP events on the stream it
-runs on, one step in eight, and reports each family's algorithmic flops / bytes per launch over
-that time; `roofline` is the family with the largest measured time per step, `kernels` all of them.
+GEMMs, attention forward / backward, ffn0, the ffn2 data gradient, the other data gradients) with HIP
+events on the stream it runs on, over --probe-steps live steps run AFTER the timed region (the timed
+steps carry no events), and reports each family's algorithmic flops / bytes per launch over that time; `roofline` is the family with the largest measured time per step, `kernels` all of them.
 """
 import argparse
 import ctypes
@@ -224,6 +224,8 @@ def main():
                     help="compute precision (default: fp8 for c4 as BASELINE configs[4] names it, else bf16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--probe-steps", type=int, default=8,
+                    help="probed live steps after the timed region (per-family kernel times, roofline)")
     ap.add_argument("--serial-steps", type=int, default=8,
                     help="probed steps run with the side stream off after the main run (serial per-kernel rates)")
     ap.add_argument("--exact-steps", type=int, default=20,
@@ -288,18 +290,13 @@ def main():
     torch.cuda.synchronize()
     L_ = ML.lib()
     probes = [p for p in args.probe.split(",") if p]
-    L_.mmt_probe_set(model._ctx, ",".join(probes).encode())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # the timed steps carry no probe events (each event record is a queue barrier): the per-family
+    # kernel times come from separate probed steps after the timed region
     t0 = time.perf_counter()
-    sampled = 0
     for i in range(args.steps):
-        # the probes' HIP events are recorded on one step in eight (each event record is a queue
-        # barrier; their pairs are made by mmt_probe_set, outside this loop)
-        on = i % 8 == 0
-        sampled += on
-        L_.mmt_probe_enable(model._ctx, 1 if on else 0)
         losses = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -311,9 +308,17 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     peaks = {lb: PEAK_TFLOPS_FP8 for lb in FP8_LABELS} if precision == "fp8" else {}
-    kernels = read_probes(L_, model._ctx, probes, sampled, args.config, peaks)
-    L_.mmt_probe_set(model._ctx, None)
     final_loss = float(sum(l.item() for l in losses))
+    # live per-family kernel times: every launch whose label matches a probe pattern bracketed by HIP
+    # events on the stream it runs on, over --probe-steps steps (side stream on, as in the timed loop;
+    # the event pairs are made by mmt_probe_set, outside these steps)
+    L_.mmt_probe_set(model._ctx, ",".join(probes).encode())
+    L_.mmt_probe_enable(model._ctx, 1)
+    for _ in range(args.probe_steps):
+        step()
+    torch.cuda.synchronize()
+    kernels = read_probes(L_, model._ctx, probes, args.probe_steps, args.config, peaks)
+    L_.mmt_probe_set(model._ctx, None)
     if args.serial_steps > 0 and world == 1:
         # the same families with the side stream off (weight gradients and keep bits on the main
         # stream): each launch has the chip to itself, so these are the per-kernel rates the live

@@ -289,6 +289,14 @@ int mmt_emb_set_sort(int on);
 // LDS, clear = loads in the MFMA fragment layout; default 2 (env MMT_QKV2_COAL); returns the previous
 // value (tests, A/B)
 int mmt_qkv2_set_coal(int on);
+// FFN ReLU' as bits (the ffn0 epilogue writes one bit per hidden element, the ffn2 data gradient reads
+// them instead of the bf16 hidden rows): 1 = on, 0 = off (default, env MMT_RELU_BITS). Latched by
+// mmt_create (the bit rows are part of that context's workspace); returns the previous value (tests, A/B)
+int mmt_set_relu_bits(int on);
+// the FFN backward's dropout-masked bf16 residual-gradient copy and FFN output-bias gradient: 1 (default,
+// env MMT_DROP_COPY_FUSE) = in the epilogue of the last cross-attention K/V data-gradient GEMM that
+// accumulates into that residual gradient, 0 = a separate pass; returns the previous value (tests, A/B)
+int mmt_set_drop_copy_fuse(int on);
 
 /* ---- MX-fp8 primitives (C4's fp8 path; BASELINE configs[4]) --------------------------------
  * MX-fp8 = OCP e4m3fn bytes + one E8M0 exponent byte (bias 127) per 32 consecutive K elements of a

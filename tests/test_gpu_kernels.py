@@ -588,6 +588,21 @@ def test_attention_hs64_backward_variants(B, T, H, ns, ring):
         L.mmt_attn_set_ring(old)
 
 
+@pytest.mark.parametrize("ring", [79, 15])
+@pytest.mark.parametrize("B,T,H,ns", [(2, 256, 8, 1), (3, 37, 2, 1), (1, 1, 2, 1), (2, 255, 1, 1), (1, 33, 4, 1),
+                                      (4, 224, 2, 1), (2, 256, 2, 2), (1, 300, 2, 1)])
+def test_attention_hs32_backward_variants(B, T, H, ns, ring):
+    """The one-pass hs-32 backward (mmt_attn_set_ring bit 6, default: T <= 256 and one KV stream) and
+    the two-pass pair (ring 15) against the same torch reference: full, ragged, single-position and
+    one-tile sequences; the multi-stream and T > 256 cases take the two-pass pair under either knob."""
+    L = ML.lib()
+    old = L.mmt_attn_set_ring(ring)
+    try:
+        test_attention_fwd_bwd(B, T, H, 32, ns)
+    finally:
+        L.mmt_attn_set_ring(old)
+
+
 # ------------------------------------------------------------------------------ small kernels
 @pytest.mark.parametrize("coal", [3, 0])
 @pytest.mark.parametrize("R,H,hs", [(1000, 8, 32), (77, 4, 16), (300, 2, 64), (50, 4, 8), (5000, 8, 32),

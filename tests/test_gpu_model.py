@@ -143,6 +143,22 @@ def test_dropout_fused_hs64_backward_matches_oracle(C, H, T, cross, p):
         L.mmt_attn_set_ring(old)
 
 
+@pytest.mark.parametrize("ring", [79, 15])
+@pytest.mark.parametrize("C,H,T,cross,p", [(64, 2, 256, [True, False], 0.1), (64, 2, 37, [False, True], 0.2),
+                                             (96, 3, 200, [True, False], 0.1), (64, 2, 31, [True, False], 0.1)])
+def test_dropout_hs32_one_pass_backward_matches_oracle(C, H, T, cross, p, ring):
+    """The one-pass hs-32 attention backward (mmt_attn_set_ring bit 6, default; T <= 256 and one KV
+    stream, so both the self-attention and -- at two modalities -- the one-stream cross-attention take
+    it) under dropout against the oracle's hash masks, at full, ragged and single-position T; ring 15
+    is the two-pass pair on the same cases."""
+    L = ML.lib()
+    old = L.mmt_attn_set_ring(ring)
+    try:
+        test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p)
+    finally:
+        L.mmt_attn_set_ring(old)
+
+
 @pytest.mark.parametrize("C,H,T,cross,p", [(64, 2, 288, [True, False], 0.2), (128, 2, 160, [False, True], 0.1),
                                              (128, 2, 300, [True, False], 0.1)])
 def test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p):

@@ -26,6 +26,8 @@
 // bit per element. 1/(1-p) is folded into the output normalisation / dV write-out.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "mmt_common.h"
@@ -1054,17 +1056,335 @@ __global__ __launch_bounds__(256, MMT_DKDV1_MINB(HS)) void attn_bwd_dkdv1_kernel
   }
 }
 
+// =============================================================================================
+// One-pass backward at hs 32 for T <= 256 and one KV stream (C1's self-attention; round 6).
+// grid (B*H, 1, problems): one workgroup (4 waves; two workgroups per CU) per (batch, head) owns all
+// nt <= 8 key tiles, so S and dP -- and their softmax / dropout VALU -- are computed ONCE per tile
+// (the two-pass kernels above recompute both in the dQ pass: 14 products per tile instead of 10)
+// and dQ needs no sum across workgroups:
+//  * Q and dO of the whole sequence land in LDS by LDS-DMA as slice images (SliceImg: conflict-free
+//    row AND transposed reads); D = rowsum(dO O) and the negated log2-domain LSE of every query go
+//    into LDS tables (thread t: query t);
+//  * wave w owns key tiles w and 7 - w (9 tile pairs of the causal walk each at nt = 8): their K / V
+//    rows (keys on lanes: the B operands of S and dP) and K^T (the A operand of dQ, transposed once
+//    through the wave's LDS slot) stay in registers, and so do their dK / dV accumulators;
+//  * all waves walk the query tiles in step, one barrier per tile: for each owned key tile kt <= qt,
+//    S = Q K^T, dP = dO V^T, P = exp2(c2 S - LSE2), dS = P (Z dP - D); dV += (Z P)^T dO and
+//    dK += dS^T Q take P and dS straight from the accumulators as A operands (keys on lanes); dS
+//    crosses the wave's LDS slot once and dQ_w^T += K^T dS^T runs on MFMA;
+//  * each wave's fp32 dQ partial of the step goes to an LDS tile (double-buffered by step parity, so
+//    one barrier per step suffices); after the barrier wave w sums rows 8w .. 8w+7 over the waves
+//    that had tiles, scales, converts and stores them.
+// LDS 78 KiB (two workgroups per CU): Q / dO images 2 x 18 KiB, tables 2 KiB, slots 4 x 2 KiB, dQ
+// partials 2 x 4 x 4 KiB. dS is accumulated divided by the dropout scale sc (as the dK/dV pass:
+// dS / sc = Z P dP - P D'), so dK and dQ take the factor sc at the end.
+// =============================================================================================
+namespace {
+typedef int32_t ai32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ ai32x4 a_rsrc(const void* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  ai32x4 rs;
+  rs[0] = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)a);
+  rs[1] = __builtin_amdgcn_readfirstlane((int32_t)((a >> 32) & 0xffffu));
+  rs[2] = __builtin_amdgcn_readfirstlane((int32_t)min(bytes, (int64_t)0x7ffffff0));
+  rs[3] = 0x00020000;
+  return rs;
+}
+__device__ __forceinline__ uint32_t a_lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+// 16 B per lane: LDS[lds + 16 lane] = buffer[voff] (zeros when voff is out of range)
+__device__ __forceinline__ void a_dma16(const ai32x4& rsrc, uint32_t lds, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" : : "s"(lds), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+constexpr int A_OOB = 0x7fffffff;
+}  // namespace
+
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int T, int H, float scale) {
+  constexpr int IMG = 8 * SL_SLICE;               // 256 rows x 32 columns as slice images
+  constexpr int OFF_DO = IMG, OFF_TAB = 2 * IMG;  // tables: -LSE2 [256], -D (-D / sc under dropout) [256]
+  constexpr int OFF_DS = OFF_TAB + 2048;          // per-wave [32][32] bf16 transpose slots
+  constexpr int OFF_DQ = OFF_DS + 4 * 2048;       // dQ partials [2 steps][4 waves][32 q][32 d] fp32
+  constexpr int BYTES = OFF_DQ + 8 * 4096;
+  static_assert(2 * BYTES <= 160 * 1024, "two workgroups per CU");
+  constexpr int EPW = 40;                          // epilogue transpose row stride (bf16)
+  static_assert(4 * 2 * 32 * EPW * 2 <= 2 * IMG, "epilogue transposes alias the Q / dO images");
+  __shared__ __attribute__((aligned(1024))) char lds[BYTES];
+  const AttnProblem& P = batch.p[blockIdx.z];
+  const int nt = (T + 31) / 32;
+  const int bh = xcd_tile(blockIdx.x, gridDim.x);
+  const int b = bh / H, head = bh % H;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t rowbase = (int64_t)b * T;
+  const float c2 = scale * kLog2e;
+  const bool ragged = (T & 31) != 0;
+  const int kts[2] = {w, 7 - w};
+
+  // Q (waves 0, 2) and dO (waves 1, 3) images: wave w streams column half w >> 1 of every slice
+  {
+    const int op = w & 1, cb = w >> 1;
+    const int ld = op ? P.dout_ld : P.q_ld;
+    const ai32x4 rs = a_rsrc((op ? P.dout : P.q) + rowbase * ld + head * 32, (int64_t)T * ld * 2);
+    const int prow = lane >> 1, pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
+    char* dst = lds + op * OFF_DO + cb * SL_SUB;
+    for (int sl = 0; sl < nt; ++sl) {
+      const int grow = sl * 32 + prow;
+      const int voff = grow < T ? (grow * ld + cb * 16 + pcol) * 2 : A_OOB;
+      a_dma16(rs, __builtin_amdgcn_readfirstlane(a_lds_u32(dst + sl * SL_SLICE)), voff);
+    }
+  }
+  // K / V rows of the wave's key tiles (keys on lanes)
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int tk = kts[t] * 32 + r;
+    const bool ok = kts[t] < nt && tk < T;
+    const bf16_t* kp = P.k[0] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
+    const bf16_t* vp = P.v[0] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kf[t][s] = ld8(kp + 16 * s + 8 * h, ok);
+      vf[t][s] = ld8(vp + 16 * s + 8 * h, ok);
+    }
+  }
+  // the LSE / D tables: thread t holds query t
+  float* tab = reinterpret_cast<float*>(lds + OFF_TAB);
+  {
+    float nl = 0.f, dsum = 0.f;
+    if (tid < T) {
+      nl = -P.lse[0][(int64_t)bh * T + tid];
+      const bf16_t* orow = P.o + (rowbase + tid) * P.o_ld + head * 32;
+      const bf16_t* drow = P.dout + (rowbase + tid) * P.dout_ld + head * 32;
+      u32x4 ov[4], dv4[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        ov[c] = *reinterpret_cast<const u32x4*>(orow + 8 * c);
+        dv4[c] = *reinterpret_cast<const u32x4*>(drow + 8 * c);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          dsum += bf2f(ov[c][e] & 0xffff) * bf2f(dv4[c][e] & 0xffff);
+          dsum += bf2f(ov[c][e] >> 16) * bf2f(dv4[c][e] >> 16);
+        }
+    }
+    tab[tid] = nl;
+    tab[256 + tid] = DROP ? -dsum / P.drop_scale : -dsum;
+  }
+  // K^T of the wave's key tiles (d on lanes, keys in the permuted k order of the transposed reads),
+  // through the wave's slot: the [key][q] dS image of the dQ product uses the same layout (8-B chunk c
+  // of row k at chunk c ^ ((k >> 1) & 7)) and the same reads, so the two operands' k orders agree
+  char* slot = lds + OFF_DS + w * 2048;
+  const int g4 = lane >> 4, qq = (lane >> 2) & 3, p4 = lane & 3;
+  const int ra0 = 4 * (g4 >> 1) + qq, ra1 = ra0 + 8;
+  const int o_da0 = ra0 * 64 + (((4 * (g4 & 1) + p4) ^ ((ra0 >> 1) & 7)) << 3);
+  const int o_da1 = ra1 * 64 + (((4 * (g4 & 1) + p4) ^ ((ra1 >> 1) & 7)) << 3);
+  auto sw = [&](int c) { return r * 64 + ((c ^ ((r >> 1) & 7)) << 3); };  // 8-B chunk c of row r
+  bf16x8 ktf[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const u32x4 v = __builtin_bit_cast(u32x4, kf[t][s]);
+      *reinterpret_cast<u32x2*>(slot + sw(4 * s + 2 * h)) = u32x2{v[0], v[1]};
+      *reinterpret_cast<u32x2*>(slot + sw(4 * s + 2 * h + 1)) = u32x2{v[2], v[3]};
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int s = 0; s < 2; ++s) ktf[t][s] = join4(lds_tr16(slot + o_da0 + 1024 * s), lds_tr16(slot + o_da1 + 1024 * s));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces landed
+  __syncthreads();                                  // everyone's pieces and table entries
+
+  // element e of a tile accumulator is query row (e & 3) + 8 (e >> 2) + 4 h of the tile, key r: bit e
+  // of m_diag keeps the diagonal tile's causal half, bit e of m_rows the rows of a ragged last query
+  // tile that lie before T (its keys past T then lie above the diagonal)
+  uint32_t m_diag = 0, m_rows = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+    m_diag |= (uint32_t)(r <= row) << e;
+    m_rows |= (uint32_t)((nt - 1) * 32 + row < T) << e;
+  }
+  const bf16_t* qimg = reinterpret_cast<const bf16_t*>(lds);
+  const bf16_t* dimg = reinterpret_cast<const bf16_t*>(lds + OFF_DO);
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) { zero16(dk[t]); zero16(dv[t]); }
+
+  // one owned key tile (t) against query tile qt; mw: the tile's keep bits (key r, this lane's half),
+  // mk: the causal / ragged mask bits of a MASKED tile
+  auto tile = [&](auto mc, int qt, int t, uint32_t mw, uint32_t mk, f32x16& dqp) {
+    constexpr bool MASKED = decltype(mc)::value;
+    asm volatile("" ::: "memory");  // the slot's previous reads stay ahead of this tile's writes
+    const int q0 = qt * 32;
+    bf16x8 qr[2], dr[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qr[s] = sl_row(qimg, q0, r, s, h);
+      dr[s] = sl_row(dimg, q0, r, s, h);
+    }
+    f32x16 sacc, dpacc;
+    zero16(sacc);
+    zero16(dpacc);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      sacc = mfma32(qr[s], kf[t][s], sacc);    // S[q][key]
+      dpacc = mfma32(dr[s], vf[t][s], dpacc);  // dP[q][key]
+    }
+    uint32_t pp[8], dd[8];  // packed bf16 pairs of Z P (dV operand) and dS / sc (dK operand)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(tab + q0 + 8 * gg + 4 * h);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(tab + 256 + q0 + 8 * gg + 4 * h);
+#pragma unroll
+      for (int e4 = 0; e4 < 4; e4 += 2) {
+        float pm[2], ds[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int e = 4 * gg + e4 + u;
+          float pv = ex2(__builtin_fmaf(sacc[e], c2, l4[e4 + u]));
+          if (MASKED) pv = keep_f(pv, __builtin_amdgcn_sbfe((int)mk, e, 1));
+          if (DROP) {
+            int kb = __builtin_amdgcn_sbfe((int)mw, 8 * gg + e4 + u, 1);  // all ones iff kept
+            asm volatile("" : "+v"(kb));
+            pm[u] = keep_f(pv, kb);
+            ds[u] = __builtin_fmaf(pm[u], dpacc[e], pv * d4[e4 + u]);  // Z P dP - P D'
+          } else {
+            pm[u] = pv;
+            ds[u] = pv * (dpacc[e] + d4[e4 + u]);  // P (dP - D)
+          }
+        }
+        pp[2 * gg + e4 / 2] = pack2bf(pm[0], pm[1]);
+        dd[2 * gg + e4 / 2] = pack2bf(ds[0], ds[1]);
+      }
+    }
+    // dS -> the slot as [key][q] rows (lane (r, h): queries 8 gg + 4 h .. + 3 of key r)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) *reinterpret_cast<u32x2*>(slot + sw(2 * gg + h)) = u32x2{dd[2 * gg], dd[2 * gg + 1]};
+    bf16x8 dot[2], qtr[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      dot[s] = sl_tr(dimg, q0, s, lane);
+      qtr[s] = sl_tr(qimg, q0, s, lane);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, u32x4{pp[4 * s], pp[4 * s + 1], pp[4 * s + 2], pp[4 * s + 3]});
+      const bf16x8 df = __builtin_bit_cast(bf16x8, u32x4{dd[4 * s], dd[4 * s + 1], dd[4 * s + 2], dd[4 * s + 3]});
+      dv[t] = mfma32(pf, dot[s], dv[t]);
+      dk[t] = mfma32(df, qtr[s], dk[t]);
+    }
+    // dQ_w^T[d][q] += K^T[d][key] dS^T[key][q]: both fragments in the permuted k order of the slot reads
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 da = join4(lds_tr16(slot + o_da0 + 1024 * s), lds_tr16(slot + o_da1 + 1024 * s));
+      dqp = mfma32(ktf[t][s], da, dqp);
+    }
+  };
+
+  // keep-bit dwords of a tile (key-major record of attn_mask_kernel), prefetched one step ahead
+  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+  const uint32_t* mrec = DROP ? P.dmask[0] + (int64_t)bh * ntri * 32 + key_dword(r) : nullptr;
+  auto mword = [&](int qt, int kt) -> uint32_t {
+    return (DROP && kt <= qt && kt < nt) ? mrec[(qt * (qt + 1) / 2 + kt) * 32] : 0u;
+  };
+  uint32_t mwA = mword(0, kts[0]), mwB = mword(0, kts[1]);
+  const float dqs = DROP ? scale * P.drop_scale : scale;
+  const int R = 8 * w + (lane >> 3), cq = lane & 7;  // this wave's dQ rows / 16-B column chunk
+#pragma unroll 1
+  for (int qt = 0; qt < nt; ++qt) {
+    const uint32_t cA = mwA >> (4 * h), cB = mwB >> (4 * h);
+    if (qt + 1 < nt) {
+      mwA = mword(qt + 1, kts[0]);
+      mwB = mword(qt + 1, kts[1]);
+    }
+    f32x16 dqp;
+    zero16(dqp);
+    const bool last_ragged = ragged && qt == nt - 1;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kt = kts[t];
+      if (kt < nt && kt <= qt) {
+        const uint32_t mw = t ? cB : cA;
+        if (kt == qt || last_ragged) {
+          const uint32_t mk = (kt == qt ? m_diag : 0xffffu) & (last_ragged ? m_rows : 0xffffu);
+          tile(std::true_type{}, qt, t, mw, mk, dqp);
+        } else {
+          tile(std::false_type{}, qt, t, mw, 0xffffu, dqp);
+        }
+      }
+    }
+    char* part = lds + OFF_DQ + ((qt & 1) * 4 + w) * 4096;
+    if (w <= qt) {  // this wave had a tile in the step (its key tile w is the lower one)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+        *reinterpret_cast<f32x4*>(part + r * 128 + (((2 * gg + h) ^ (r & 7)) << 4)) =
+            f32x4{dqp[4 * gg], dqp[4 * gg + 1], dqp[4 * gg + 2], dqp[4 * gg + 3]};
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every partial of step qt is written
+    {
+      const int nw = min(qt + 1, 4);
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < nw; ++u)
+        a += *reinterpret_cast<const f32x4*>(lds + OFF_DQ + ((qt & 1) * 4 + u) * 4096 + R * 128 + ((cq ^ (R & 7)) << 4));
+      const int tq = qt * 32 + R;
+      if (tq < T)
+        *reinterpret_cast<u32x2*>(P.dq + (rowbase + tq) * P.dq_ld + head * 32 + 4 * cq) =
+            u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)};
+    }
+  }
+
+  // dK / dV of the wave's key tiles, transposed through its LDS slot (in the Q / dO images, which
+  // no wave reads after the last step's barrier) into row-major 16-B pieces, as the dK/dV pass
+  const float dks = DROP ? scale * P.drop_scale : scale;
+  const float dvs = DROP ? P.drop_scale : 1.f;
+  bf16_t* et = reinterpret_cast<bf16_t*>(lds) + w * (2 * 32 * EPW);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int kt = kts[t];
+    if (kt >= nt) continue;
+    const int k0 = kt * 32;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+      et[kr * EPW + r] = f2bf(dk[t][e] * dks);
+      et[32 * EPW + kr * EPW + r] = f2bf(dv[t][e] * dvs);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = i * 16 + (lane >> 2), d0 = (lane & 3) * 8;
+      const u32x4 vk = *reinterpret_cast<const u32x4*>(et + row * EPW + d0);
+      const u32x4 vv = *reinterpret_cast<const u32x4*>(et + 32 * EPW + row * EPW + d0);
+      if (k0 + row < T) {
+        const int64_t off = (rowbase + k0 + row) * P.dkv_ld + d0;
+        *reinterpret_cast<u32x4*>(P.dk[0] + head * P.dkv_hstride + off) = vk;
+        *reinterpret_cast<u32x4*>(P.dv[0] + head * P.dkv_hstride + off) = vv;
+      }
+    }
+  }
+}
+
 // attention variant knob (bit 0: the slice-streamed hs-64 dK/dV pass, bit 1: its dQ pass, bit 2: the
 // dK/dV pass at 3 waves per SIMD, bit 3: the slice-streamed hs-64 forward, bit 5: the one-pass hs-64
-// backward at T <= 512 with one KV stream): MMT_ATTN_RING, or
-// mmt_attn_set_ring() for in-process A/B
+// backward at T <= 512 with one KV stream, bit 6: the one-pass hs-32 backward at T <= 256 with one KV
+// stream): MMT_ATTN_RING, or mmt_attn_set_ring() for in-process A/B
 static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
   // both hs-64 passes on the rings (dQ: two query tiles per wave), dK/dV at 3 waves per SIMD
   // (standalone backward: target 277 -> 273 us, C3 cross-attention 2461 -> 2298, C4 2237 -> 2116;
   // C3 step -1.5 %: profiles/r3u_ring_ab.txt), and the forward on the ring too (round 4: target
   // 20.42 -> 20.34 ms, C3 157.3 -> 153.8 ms same box, profiles/r4m_ab.txt)
-  return e ? atoi(e) : 15;
+  // bit 6 (round 6): the one-pass hs-32 backward
+  return e ? atoi(e) : 15 | 64;
 }();
 extern "C" int mmt_attn_set_ring(int v) {
   const int old = g_attn_ring;
@@ -1107,6 +1427,22 @@ static hipError_t attn_launch(const AttnBatch& bt, int B, int T, int H, float sc
     const bool ring = HS == 64 && ring64_fits(bt, T);
     // knob bit 5: dQ, dK, dV in one pass (mmt_attn2.hip) for T <= 512 and one KV stream
     if (ring && (g_attn_ring & 32) && T <= 512 && ns == 1) return mmt_attn_bwd_fused64(bt, B, T, H, scale, drop, s);
+    // knob bit 6: dQ, dK, dV in one pass at hs 32 for T <= 256 and one KV stream (Q / dO rows by LDS-DMA:
+    // 16-B aligned rows, and sequences whose span fits a buffer descriptor)
+    if (HS == 32 && (g_attn_ring & 64) && T <= 256 && ns == 1) {
+      bool ok = true;
+      for (int g = 0; g < bt.count; ++g) {
+        const AttnProblem& P = bt.p[g];
+        ok = ok && !(P.q_ld & 7) && !(P.dout_ld & 7) && !((uintptr_t)P.q & 15) && !((uintptr_t)P.dout & 15) &&
+             !(P.kv_ld & 7) && !(P.kv_hstride & 7) && (int64_t)T * std::max(P.q_ld, P.dout_ld) * 2 < ((int64_t)1 << 31);
+      }
+      if (ok) {
+        const dim3 grid(B * H, 1, bt.count);
+        if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true>), grid, dim3(256), 0, s, bt, T, H, scale);
+        else hipLaunchKernelGGL((attn_bwd_fused32<false>), grid, dim3(256), 0, s, bt, T, H, scale);
+        return hipGetLastError();
+      }
+    }
     if (ring && (g_attn_ring & 2)) {
       const hipError_t e = mmt_attn_bwd_dq_ring64(bt, B, T, H, scale, drop, s);
       if (e != hipSuccess) return e;  // (hipGetLastError cleared it: report it here)

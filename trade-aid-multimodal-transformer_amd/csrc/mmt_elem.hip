@@ -405,21 +405,52 @@ __global__ __launch_bounds__(256) void embed_pos_bwd_kernel(EmbBatch batch, int 
 // as int scratch): the LDS-privatised slabs above scatter-add every element with ds_add_f32, and LDS
 // float atomics serialise (C1: 127 + 28 us live for 67 MB of dx, 14x its HBM time; the last kernels
 // of the step). Here no float atomic touches LDS:
-//  * emb_sort_kernel, one workgroup per modality: token histogram (LDS integer atomics), exclusive
-//    scan, scatter of the row ids into token order -> perm [R] (order inside a token's bucket is
-//    the arrival order: the float sum order of dtok varies run to run, as with the atomics before);
+//  * emb_sort_kernel, one workgroup per modality: the row ids in token order -> perm [R], STABLE
+//    (rows of one token in increasing row order) for R <= EMB_SORT_RMAX: a bitonic sort of the keys
+//    token << 14 | row in LDS, so the run sums below add a token's rows in a fixed order (round 6:
+//    the round-5 histogram scatter placed a bucket's rows in atomic arrival order, so dtok's float
+//    sums changed run to run). Larger R keeps that scatter (order inside a bucket = arrival order);
 //  * emb_segsum_kernel: a wave walks 64 consecutive sorted rows (each dx row read once, 1 KiB per
 //    wave-load), sums runs of equal tokens in registers and adds each run to dtok with one atomic per
 //    column (a few runs per wave: ~V + waves adds per column in all).
 // ---------------------------------------------------------------------------------------------
 #define EMB_SORT_VMAX 16384
+#define EMB_SORT_RMAX 16384  // rows of the stable (bitonic) form: keys tok << 14 | row
 __global__ __launch_bounds__(1024) void emb_sort_kernel(EmbBatch batch, int R) {
   const EmbProblem& P = batch.p[blockIdx.z];
   const int V = P.V;
-  int* perm = reinterpret_cast<int*>(P.part);
-  __shared__ int cnt[EMB_SORT_VMAX];
+  int* perm = P.perm ? P.perm : reinterpret_cast<int*>(P.part);
+  __shared__ int cnt[EMB_SORT_VMAX];  // stable form: the keys (EMB_SORT_RMAX == EMB_SORT_VMAX)
   __shared__ int wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (R <= EMB_SORT_RMAX) {
+    static_assert(EMB_SORT_RMAX <= EMB_SORT_VMAX, "the key array reuses the histogram");
+    uint32_t* key = reinterpret_cast<uint32_t*>(cnt);
+    int N = 2;
+    while (N < R) N <<= 1;
+    for (int r = tid; r < N; r += 1024) {
+      uint32_t k = 0xffffffffu;  // padding sorts last
+      if (r < R) {
+        int64_t t = P.idx[r];
+        t = t < 0 ? 0 : (t >= V ? V - 1 : t);
+        k = ((uint32_t)t << 14) | (uint32_t)r;
+      }
+      key[r] = k;
+    }
+    __syncthreads();
+    // keys are distinct (the row is in the low bits), so the result is the unique sorted order
+    for (int k = 2; k <= N; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int p = tid; p < (N >> 1); p += 1024) {
+          const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+          const uint32_t a = key[i], b = key[i + j];
+          if ((a > b) == ((i & k) == 0)) { key[i] = b; key[i + j] = a; }
+        }
+        __syncthreads();
+      }
+    for (int r = tid; r < R; r += 1024) perm[r] = (int)(key[r] & 0x3fffu);
+    return;
+  }
   for (int v = tid; v < V; v += 1024) cnt[v] = 0;
   __syncthreads();
   for (int r = tid; r < R; r += 1024) {
@@ -462,7 +493,7 @@ __global__ __launch_bounds__(1024) void emb_sort_kernel(EmbBatch batch, int R) {
 __global__ __launch_bounds__(256) void emb_segsum_kernel(EmbBatch batch, int R, int C) {
   const EmbProblem& P = batch.p[blockIdx.z];
   const int V = P.V;
-  const int* perm = reinterpret_cast<const int*>(P.part);
+  const int* perm = P.perm ? P.perm : reinterpret_cast<const int*>(P.part);
   const int halves = (C + 255) / 256;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int range = gw / halves, hf = gw % halves;
@@ -531,9 +562,21 @@ static bool emb_sorted_ok(const EmbBatch& b, int R, int C) {
   if (!g_emb_sort || C > 1024) return false;
   for (int g = 0; g < b.count; ++g) {
     const EmbProblem& P = b.p[g];
-    if (!P.part || P.V < 1 || P.V > EMB_SORT_VMAX || (int64_t)R * C < R) return false;
+    if ((!P.part && !P.perm) || P.V < 1 || P.V > EMB_SORT_VMAX || (int64_t)R * C < R) return false;
   }
   return true;
+}
+
+// the row sort alone, into every problem's perm (the engine runs it early, on the side stream: it
+// reads only the token ids); false (nothing launched) when the sorted path does not apply
+bool mmt_emb_sort_ok(const EmbBatch& b, int R, int C) {
+  for (int g = 0; g < b.count; ++g)
+    if (!b.p[g].perm) return false;
+  return b.count > 0 && C % 4 == 0 && emb_sorted_ok(b, R, C);
+}
+hipError_t mmt_launch_emb_sort(const EmbBatch& b, int R, hipStream_t s) {
+  hipLaunchKernelGGL(emb_sort_kernel, dim3(1, 1, b.count), dim3(1024), 0, s, b, R);
+  return hipGetLastError();
 }
 
 hipError_t mmt_launch_embed_fwd(const EmbBatch& b, int B, int T, int C, hipStream_t s) {
@@ -551,7 +594,10 @@ hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStrea
   if (emb_sorted_ok(b, R, C)) {
     for (int g = 1; g < b.count; ++g)
       if (b.p[g].dpos != b.p[0].dpos) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(emb_sort_kernel, dim3(1, 1, b.count), dim3(1024), 0, s, b, R);
+    // perm set on every problem: mmt_launch_emb_sort already ran (same stream order or an event)
+    bool sorted = true;
+    for (int g = 0; g < b.count; ++g) sorted = sorted && b.p[g].perm;
+    if (!sorted) hipLaunchKernelGGL(emb_sort_kernel, dim3(1, 1, b.count), dim3(1024), 0, s, b, R);  // into perm / part
     const int halves = (C + 255) / 256;
     const int waves = ((R + 63) / 64) * halves;
     hipLaunchKernelGGL(emb_segsum_kernel, dim3((waves + 3) / 4, 1, b.count), dim3(256), 0, s, b, R, C);
@@ -679,7 +725,8 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(CeBatch batch, int R) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const float blk = (part[0] + part[1] + part[2] + part[3]) / (float)R;
-    atomicAdd(P.loss, blk);
+    if (P.part) P.part[blockIdx.x] = blk;  // summed in block order by ce_loss_kernel
+    else atomicAdd(P.loss, blk);
     // failure detection: a non-finite loss raises this problem's bit in a device
     // flag word the host reads when it syncs anyway (reference guard: main.py:606)
     if (P.flag && !__builtin_isfinite(blk)) {
@@ -689,10 +736,28 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(CeBatch batch, int R) {
   }
 }
 
+// the block shares of ce_fwd_kernel (CeProblem::part) added to the loss in block order: lane l sums
+// blocks l, l + 64, ... in order, then a fixed xor tree over the lanes (no atomics: the loss is the
+// same bits on every run)
+__global__ __launch_bounds__(64) void ce_loss_kernel(CeBatch batch, int blocks) {
+  const CeProblem& P = batch.p[blockIdx.z];
+  if (!P.part) return;
+  const int lane = threadIdx.x;
+  float s = 0.f;
+  for (int b = lane; b < blocks; b += 64) s += P.part[b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) *P.loss += s;
+}
+
 hipError_t mmt_launch_ce_fwd(const CeBatch& b, int R, hipStream_t s) {
   if (b.count == 0) return hipSuccess;
   int maxv = 1;
-  for (int g = 0; g < b.count; ++g) maxv = b.p[g].V > maxv ? b.p[g].V : maxv;
+  bool any_part = false;
+  for (int g = 0; g < b.count; ++g) {
+    maxv = b.p[g].V > maxv ? b.p[g].V : maxv;
+    any_part = any_part || b.p[g].part;
+  }
   int blocks = (R + 3) / 4;
   if (blocks > 512) blocks = 512;
   dim3 grid(blocks, 1, b.count);
@@ -703,6 +768,7 @@ hipError_t mmt_launch_ce_fwd(const CeBatch& b, int R, hipStream_t s) {
   else if (kv <= 8) hipLaunchKernelGGL(ce_fwd_kernel<8>, grid, dim3(256), 0, s, b, R);
   else if (kv <= 16) hipLaunchKernelGGL(ce_fwd_kernel<16>, grid, dim3(256), 0, s, b, R);
   else hipLaunchKernelGGL(ce_fwd_kernel<0>, grid, dim3(256), 0, s, b, R);
+  if (any_part) hipLaunchKernelGGL(ce_loss_kernel, dim3(1, 1, b.count), dim3(64), 0, s, b, blocks);
   return hipGetLastError();
 }
 

@@ -94,6 +94,8 @@ struct Plan {
   size_t dres16[8][MAXM];
   size_t dvec[MAXM][MAXM];
   size_t dkv[2][MAXM][MAXM];
+  size_t celoss[MAXM];  // float [512]: the cross-entropy blocks' loss shares (summed in block order)
+  size_t eperm[MAXM];  // int [R]: the rows in token order for the token-table gradient (mmt_launch_emb_sort)
   // KV-cache decode (generate): compact [B, *] rows of ONE new position per sequence
   struct Dec {
     size_t x0, a16, mean, rstd, h1, qkv, o16, p1, f, x2h, d16, qc, oc, pc, lnf16, hh;
@@ -103,6 +105,33 @@ struct Plan {
 };
 
 }  // namespace
+
+// the FFN's ReLU' as bits written by ffn0 (16x fewer bytes than the bf16 hidden the ffn2 data
+// gradient reads back). MMT_RELU_BITS=1 or mmt_set_relu_bits(1) before mmt_create turns it on (latched
+// per context: the bit rows are allocated only then); off by default: on the final round-5 build the
+// bf16 aux measured faster (same box, profiles/r5am_relu_bits_final_ab.txt: C1 8.502 -> 8.477 ms,
+// target 19.770 -> 19.505 ms), where the first version had been 0.1-0.7 % faster than the aux
+static int g_relu_bits = [] {
+  const char* e = getenv("MMT_RELU_BITS");
+  return e ? atoi(e) : 0;
+}();
+extern "C" int mmt_set_relu_bits(int on) {
+  const int old = g_relu_bits;
+  g_relu_bits = on;
+  return old;
+}
+// the FFN backward's dropout-masked bf16 residual-gradient copy (+ FFN output-bias gradient) in the
+// epilogue of the last cross-attention K/V dX launch into that gradient (1, default, env
+// MMT_DROP_COPY_FUSE) or a separate drop_copy pass (0)
+static int g_drop_copy_fuse = [] {
+  const char* e = getenv("MMT_DROP_COPY_FUSE");
+  return e ? atoi(e) : 1;
+}();
+extern "C" int mmt_set_drop_copy_fuse(int on) {
+  const int old = g_drop_copy_fuse;
+  g_drop_copy_fuse = on;
+  return old;
+}
 
 struct mmt_ctx {
   mmt_config cfg;
@@ -127,6 +156,11 @@ struct mmt_ctx {
   MxSeg* d_mxsegs = nullptr;
   int tables_device = -1;
   bool fp8 = false;
+  bool relu_bits = false;  // g_relu_bits at mmt_create
+  // token-table gradient: the rows' sort runs at backward stage 0 on the side stream (it reads only the
+  // forward's token ids); emb_ev marks its end for the embedding stage
+  hipEvent_t emb_ev = nullptr;
+  bool emb_sorted = false;
   int64_t pack_elems = 0;
   PackSeg* d_segs = nullptr;
   int* d_tasks = nullptr;
@@ -414,7 +448,7 @@ void make_plan(mmt_ctx* c, int B) {
       a.p1 = A(R * ldp * b2); a.x1 = A(R * C * f4);
       a.c = A(R * C * b2); a.mean2 = A(R * f4); a.rstd2 = A(R * f4);
       a.f = A(R * 4 * C * b2); a.x2 = A(R * C * f4);
-      a.fm = A(R * (4 * C / 8));
+      a.fm = c->relu_bits ? A(R * (4 * C / 8)) : 0;
       a.x2h = c->any_cross ? A(R * C * b2) : 0;
       a.dm = mbytes ? A(mbytes) : 0;
       if (c->fp8) {
@@ -443,6 +477,8 @@ void make_plan(mmt_ctx* c, int B) {
   }
   for (int i = 0; i < M; ++i) {
     p.dres[i] = A(R * C * f4); p.dln[i] = A(R * C * f4);
+    p.eperm[i] = A(R * 4);
+    p.celoss[i] = A(512 * 4);
     for (int k = 0; k < 8; ++k) p.dres16[k][i] = A(R * C * b2);
     p.gdo[i] = A(R * C * b2); p.gqkv[i] = A(R * 3 * C * b2);
     for (int k = 0; k < 2; ++k) {
@@ -548,7 +584,12 @@ void gemm_cost(const GemmBatch& b, int epi, double* fl, double* by) {
     x += M * N * (f32_out ? 4.0 : 2.0);
     if (epi == EPI_BIAS_RESID_F32) x += M * N * 4.0 + (P.o16 ? M * N * 2.0 : 0.0);
     if (epi == EPI_ACC_F32) x += M * N * 4.0;
-    if (epi == EPI_DTANH_BF16 || epi == EPI_DRELU_BF16) x += M * N * 2.0;
+    // tanh' / ReLU' operand: the bf16 hidden rows, or one bit per element (ReLU' bits, mask8)
+    if (epi == EPI_DTANH_BF16 || epi == EPI_DRELU_BF16) x += (epi == EPI_DRELU_BF16 && P.mask8) ? M * N / 8.0 : M * N * 2.0;
+    // ReLU' bits written by the forward (EPI_BIAS_RELU_BF16 with mask8)
+    if (epi == EPI_BIAS_RELU_BF16 && P.mask8) x += M * N / 8.0;
+    // MX-fp8 copy of the output (the next fp8 GEMM's A operand): e4m3fn bytes + one E8M0 byte per 32
+    if (P.o8) x += M * N * (1.0 + 1.0 / 32.0);
     // fused LayerNorm backward: LN input and the accumulated gradient read, that gradient (+ its bf16
     // copy) written, row statistics read
     if (epi == EPI_LN_BWD_F32) x += M * N * 8.0 + (P.o16 ? M * N * 2.0 : 0.0) + M * 8.0;
@@ -654,7 +695,8 @@ struct Runner {
     if (id >= 0) {
       double fl = 0, by = 0;
       gemm_cost(b, epi, &fl, &by);
-      for (int g = 0; g < b.count; ++g) by -= ((double)b.p[g].M + b.p[g].N) * b.p[g].K;  // 1-byte operands
+      // 1-byte operands plus one E8M0 exponent byte per 32 K elements of every row of A and B
+      for (int g = 0; g < b.count; ++g) by -= ((double)b.p[g].M + b.p[g].N) * b.p[g].K * (1.0 - 1.0 / 32.0);
       probe_end(id, s, fl, by);
     }
   }
@@ -838,15 +880,6 @@ struct Runner {
 // -------------------------------------------------------------------------------------------
 // forward
 // -------------------------------------------------------------------------------------------
-// the FFN's ReLU' as bits written by ffn0 (16x fewer bytes than the bf16 hidden the ffn2 data
-// gradient reads back). MMT_RELU_BITS=1 turns it on; off by default: on the final round-5 build the
-// bf16 aux measured faster (same box, profiles/r5am_relu_bits_final_ab.txt: C1 8.502 -> 8.477 ms,
-// target 19.770 -> 19.505 ms), where the first version had been 0.1-0.7 % faster than the aux
-static const bool relu_bits = [] {
-  const char* e = getenv("MMT_RELU_BITS");
-  return e ? atoi(e) != 0 : false;
-}();
-
 int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t* const* tgt, float* const* logits,
                 float* losses) {
   const int M = c->M, C = c->C, H = c->H, hs = c->hs, R = r.R, B = r.B, T = c->T;
@@ -1033,7 +1066,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       g.p[i] = f8 ? gp_f8(r.W<uint8_t>(a[i].c8), C, r.W<uint8_t>(a[i].cs8), ldsC, w8, x[i].F0, R)
                   : gp_fwd(r.W<bf16_t>(a[i].c), C, wpk, x[i].F0, R);
       g.p[i].bias = r.P(x[i].bf0); g.p[i].o16 = r.W<bf16_t>(a[i].f); g.p[i].ldo16 = 4 * C;
-      if (relu_bits) { g.p[i].mask8 = r.W<uint8_t>(a[i].fm); g.p[i].ldm8 = 4 * C / 8; }
+      if (r.c->relu_bits) { g.p[i].mask8 = r.W<uint8_t>(a[i].fm); g.p[i].ldm8 = 4 * C / 8; }
       if (f8) { g.p[i].o8 = r.W<uint8_t>(a[i].f8); g.p[i].ld8 = 4 * C; g.p[i].s8 = r.W<uint8_t>(a[i].fs8); g.p[i].lds8 = ldsF; }
     }
     if (f8) r.gemm8(g, EPI_BIAS_RELU_BF16, "ffn0");
@@ -1182,6 +1215,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       cb.p[i].logits = logits[i]; cb.p[i].tgt = tgt[i]; cb.p[i].dlogits = r.W<bf16_t>(p.dlog[i]);
       cb.p[i].loss = losses + i; cb.p[i].V = c->V[i]; cb.p[i].ld_d = c->ldv[i];
       cb.p[i].flag = r.W<int>(p.flag); cb.p[i].bit = 1 << i;
+      cb.p[i].part = r.W<float>(p.celoss[i]);
     }
     r.ok(mmt_launch_ce_fwd(cb, R, r.s), "ce_fwd");
   }
@@ -1401,6 +1435,22 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
   if (stage == 0) {
     c->d16 = 0;
     HIPCHK(c, hipMemsetAsync(grads, 0, sizeof(float) * c->nactive, r.s));  // the active prefix only
+    // the token-table gradient's row sort (stable: a fixed summation order) needs only the forward's
+    // token ids: it runs now on the side stream, off the critical path (27.6 us serial at C1 as the
+    // embedding stage's first launch in round 5)
+    c->emb_sorted = false;
+    {
+      EmbBatch eb{}; eb.count = M;
+      for (int i = 0; i < M; ++i) {
+        eb.p[i].idx = c->last_idx[i]; eb.p[i].V = c->V[i]; eb.p[i].perm = r.W<int>(p.eperm[i]);
+      }
+      if (mmt_emb_sort_ok(eb, R, C)) {
+        if (!c->emb_ev) HIPCHK(c, hipEventCreateWithFlags(&c->emb_ev, hipEventDisableTiming));
+        const hipStream_t ss = r.side_stream() ? r.side() : r.s;
+        if (r.ok(mmt_launch_emb_sort(eb, R, ss), "emb_sort") && r.ok(hipEventRecord(c->emb_ev, ss), "event record"))
+          c->emb_sorted = true;
+      }
+    }
     const float invR = 1.0f / (float)R;
     GemmBatch dw{}; dw.count = M;
     GemmBatch dx{}; dx.count = M;
@@ -1457,11 +1507,8 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     }
   }
   if (c->any_cross) {
-    // MMT_DROP_COPY_FUSE=0: the separate drop_copy pass for every modality (A/B)
-    static const bool fuse_copy = [] {
-      const char* e = getenv("MMT_DROP_COPY_FUSE");
-      return e ? atoi(e) != 0 : true;
-    }();
+    // MMT_DROP_COPY_FUSE=0 / mmt_set_drop_copy_fuse(0): the separate drop_copy pass for every modality
+    const bool fuse_copy = g_drop_copy_fuse != 0;
     std::vector<int> cx;
     for (int i = 0; i < M; ++i) if (x[i].cross) cx.push_back(i);
     const int nc = (int)cx.size();
@@ -1541,17 +1588,23 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     for (int i : cx)
       for (int j = 0; j < M; ++j)
         if (j != i) last_writer[j] = i;
+    // the fused copy is only right if no later launch of this stage accumulates into dres[j] (the FFN
+    // backward reads the copy): launches run in cx order and last_writer[j] is the last i of cx that
+    // writes dres[j]; copied[j] checks that invariant as the launches are built
+    std::vector<char> copied(M, 0);
     for (int i : cx) {
       GemmBatch kw{}; kw.count = 0;
       GemmBatch kx{}; kx.count = 0;
       int jj = 0;
       for (int j = 0; j < M; ++j) {
         if (j == i) continue;
+        if (copied[j]) return fail(c, MMT_ERR_STATE, "cross K/V dX: dres written after its fused bf16 copy");
         const bf16_t* g = r.W<bf16_t>(p.dkv[par][i][jj]);
         kw.p[kw.count++] = gp_dw(g, 2 * C, r.W<bf16_t>(a[j].x2h), C, grads, x[i].Wkv[jj], R);
         GemmProblem d = gp_dx(g, 2 * C, wpk, x[i].Wkv[jj], R);
         d.o32 = r.W<float>(p.dres[j]); d.ldc = C;
         if (last_writer[j] == i && fuse_copy) {
+          copied[j] = 1;
           d.o16 = d16_cur(c, r, j); d.ldo16 = C; d.dbias = grads + x[j].bf2;
           r.set_drop(d, l, j, DS_FFN);
         }
@@ -1587,7 +1640,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     dx.p[i] = gp_dx(g, C, wpk, x[i].F2, R);
     dx.p[i].aux = r.W<bf16_t>(a[i].f); dx.p[i].ldaux = 4 * C; dx.p[i].o16 = r.W<bf16_t>(p.gbig[par][i]); dx.p[i].ldo16 = 4 * C;
     dx.p[i].dbias = grads + x[i].bf0;
-    if (relu_bits) { dx.p[i].mask8 = r.W<uint8_t>(a[i].fm); dx.p[i].ldm8 = 4 * C / 8; }  // ReLU' from bits
+    if (r.c->relu_bits) { dx.p[i].mask8 = r.W<uint8_t>(a[i].fm); dx.p[i].ldm8 = 4 * C / 8; }  // ReLU' from bits
   }
   r.dwgemm(dw, "ffn2_dw");
   r.gemm(dx, true, false, EPI_DRELU_BF16, 1, "ffn2_dx");
@@ -1790,6 +1843,7 @@ mmt_ctx* mmt_create(const mmt_config* cfg) {
   }
   if (c->M - 1 > MMT_MAX_STREAMS) { g_create_err = "too many KV streams"; delete c; return nullptr; }
   c->fp8 = cfg->precision == 1;
+  c->relu_bits = g_relu_bits != 0;
   build_layout(c);
   return c;
 }
@@ -1802,6 +1856,7 @@ void mmt_destroy(mmt_ctx* c) {
   for (auto& e : c->probe_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->evpool) (void)hipEventDestroy(e);
   for (auto& e : c->stage_ev) if (e) (void)hipEventDestroy(e);
+  if (c->emb_ev) (void)hipEventDestroy(c->emb_ev);
   if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
 }
@@ -1919,7 +1974,10 @@ int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* los
       eb.p[i].idx = c->last_idx[i]; eb.p[i].dx = r.W<float>(c->plan.dres[i]);
       eb.p[i].dtok = grads + c->post[i].tok; eb.p[i].dpos = grads + c->pos_off; eb.p[i].V = c->V[i];
       eb.p[i].part = r.W<float>(c->plan.dln[i]);  // R x C fp32, free once the layers are done
+      if (c->emb_sorted) eb.p[i].perm = r.W<int>(c->plan.eperm[i]);  // sorted at stage 0
     }
+    if (c->emb_sorted) r.ok(hipStreamWaitEvent(r.s, c->emb_ev, 0), "stream wait");
+    c->emb_sorted = false;
     r.ok(mmt_launch_embed_bwd(eb, r.B, c->T, c->C, r.s), "embed_bwd");
     return r.rc;
   }

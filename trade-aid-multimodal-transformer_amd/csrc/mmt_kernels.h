@@ -294,9 +294,14 @@ struct EmbProblem {
   // there as per-chunk partial tables and one reduce pass adds them into dtok (short row chunks,
   // no global atomics); nullptr: atomic flush
   float* part;
+  // optional int [B*T]: the rows in token order (stable), written by mmt_launch_emb_sort; when every
+  // problem has it, mmt_launch_embed_bwd takes the sorted path without sorting again
+  int* perm;
   int V;
 };
 struct EmbBatch { EmbProblem p[MMT_MAX_GROUP]; int count; };
+bool mmt_emb_sort_ok(const EmbBatch& b, int R, int C);
+hipError_t mmt_launch_emb_sort(const EmbBatch& b, int R, hipStream_t s);
 hipError_t mmt_launch_embed_fwd(const EmbBatch& b, int B, int T, int C, hipStream_t s);
 hipError_t mmt_launch_embed_bwd(const EmbBatch& b, int B, int T, int C, hipStream_t s);
 
@@ -304,7 +309,10 @@ struct CeProblem {
   const float* logits;   // [R, V]
   const int64_t* tgt;    // [R]
   bf16_t* dlogits;       // [R, ld_d] = softmax - onehot (pad columns zeroed)
-  float* loss;           // scalar, atomic accumulate of mean
+  float* loss;           // scalar, accumulate (+=) of the mean
+  // nullable float [512]: each block stores its share there and one wave adds them to loss in block
+  // order (run-to-run identical losses); null: one atomic per block (arrival order)
+  float* part;
   int* flag;             // nullable: flag[0], flag[1] |= bit when this problem's loss is NaN / Inf (no trap)
   int V, ld_d, bit;
 };

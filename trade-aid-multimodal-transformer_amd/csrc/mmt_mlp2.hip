@@ -460,6 +460,19 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_kernel(Mlp2Batch batch) {
   }
 }
 
+// a field the fused kernels do not implement must be unset: the engine then falls back to the two GEMMs
+// instead of the fused launch silently dropping that output (MX-fp8 copies, ReLU bits, the fused Q/K/V
+// stage 2, split-K, and per direction the epilogue operands the other direction's kernel reads)
+static bool mlp2_unused_clear(const GemmProblem& p1, const GemmProblem& p2, bool bwd) {
+  for (const GemmProblem* p : {&p1, &p2})
+    if (p->o8 || p->s8 || p->mask8 || p->qkv2_out || p->split_stride || p->sa || p->sb || p->ln_dgamma ||
+        p->ln_dbeta)
+      return false;
+  if (bwd) return !p1.resid && !p1.bias && !p2.bias && !p2.resid && !p2.dbias && !p2.aux && !p2.o32 &&
+                  !p2.lnf_y && !p2.drop_thr;
+  return !p1.aux && !p1.resid && !p1.dbias && !p1.o32 && !p2.aux && !p2.dbias && !p1.drop_thr;
+}
+
 bool mmt_mlp2_bwd_ok(const Mlp2Batch& b) {
   if (b.count <= 0 || b.count > MMT_MLP2_GROUP) return false;
   const int n1 = b.g1[0].N;
@@ -475,6 +488,7 @@ bool mmt_mlp2_bwd_ok(const Mlp2Batch& b) {
     if (((uintptr_t)p1.A | (uintptr_t)p1.B | (uintptr_t)p2.B | (uintptr_t)p1.o16 | (uintptr_t)p2.o16) & 15) return false;
     if (((uintptr_t)p1.aux) & 7) return false;
     if (p2.alpha_ptr || p1.alpha_ptr || p2.alpha != 1.0f || p2.bias) return false;
+    if (!mlp2_unused_clear(p1, p2, true)) return false;
     if ((int64_t)513 * std::max(p1.lda, std::max(p1.ldb, p2.ldb)) * 2 >= ((int64_t)1 << 31)) return false;
   }
   return true;
@@ -502,8 +516,9 @@ bool mmt_mlp2_ok(const Mlp2Batch& b) {
         (p2.o16 && (p2.ldo16 & 7)) || p1.lda < p1.K || p1.ldb < p1.K || p2.ldb < p2.K || p1.ldo16 < n1)
       return false;
     if (((uintptr_t)p1.A | (uintptr_t)p1.B | (uintptr_t)p2.B | (uintptr_t)p1.o16 | (uintptr_t)p2.o32 |
-         (uintptr_t)p2.resid | (uintptr_t)p1.bias) & 15)
+         (uintptr_t)p2.resid | (uintptr_t)p1.bias | (uintptr_t)p2.o16) & 15)  // 16-B epilogue stores / loads
       return false;
+    if (!mlp2_unused_clear(p1, p2, false)) return false;
     if (p2.alpha_ptr || p1.alpha_ptr || p1.alpha != 1.0f) return false;
     if ((int64_t)513 * std::max(p1.lda, std::max(p1.ldb, p2.ldb)) * 2 >= ((int64_t)1 << 31)) return false;
     if (p2.lnf_y && (!p2.lnf_gamma || !p2.lnf_beta || !p2.lnf_mean || !p2.lnf_rstd ||
