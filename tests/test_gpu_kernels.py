@@ -589,7 +589,7 @@ def test_attention_hs64_backward_variants(B, T, H, ns, ring):
 
 
 @pytest.mark.parametrize("ring", [79, 15])
-@pytest.mark.parametrize("B,T,H,ns", [(2, 256, 8, 1), (3, 37, 2, 1), (1, 1, 2, 1), (2, 255, 1, 1), (1, 33, 4, 1),
+@pytest.mark.parametrize("B,T,H,ns", [(2, 256, 8, 1), (3, 37, 2, 1), (1, 2, 2, 1), (2, 255, 1, 1), (1, 33, 4, 1),
                                       (4, 224, 2, 1), (2, 256, 2, 2), (1, 300, 2, 1)])
 def test_attention_hs32_backward_variants(B, T, H, ns, ring):
     """The one-pass hs-32 backward (mmt_attn_set_ring bit 6, default: T <= 256 and one KV stream) and

@@ -1098,9 +1098,34 @@ __device__ __forceinline__ void a_dma16(const ai32x4& rsrc, uint32_t lds, int vo
   asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" : : "s"(lds), "v"(voff), "s"(rsrc)
                : "memory", "m0");
 }
+// 8 B per lane: buffer[voff] = v (dropped when voff is out of range): one store instruction whatever
+// the lanes' rows, so counted vmcnt waits can include it
+__device__ __forceinline__ void a_bst8(const ai32x4& rsrc, int voff, u32x2 v) {
+  asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" : : "v"(v), "v"(voff), "s"(rsrc) : "memory");
+}
+// counted wait on this wave's outstanding vector-memory operations (immediate operand, n <= 8)
+__device__ __forceinline__ void a_wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
 constexpr int A_OOB = 0x7fffffff;
 }  // namespace
 
+#ifndef MMT_F32_BRANCH
+#define MMT_F32_BRANCH 0
+#endif
+#ifndef MMT_F32_PAIR
+#define MMT_F32_PAIR 0  // 1: the two-tile body where both owned key tiles are active (register copies: slower)
+#endif
 template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int T, int H, float scale) {
   constexpr int IMG = 8 * SL_SLICE;               // 256 rows x 32 columns as slice images
@@ -1123,20 +1148,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
   const bool ragged = (T & 31) != 0;
   const int kts[2] = {w, 7 - w};
 
-  // Q (waves 0, 2) and dO (waves 1, 3) images: wave w streams column half w >> 1 of every slice
-  {
-    const int op = w & 1, cb = w >> 1;
-    const int ld = op ? P.dout_ld : P.q_ld;
-    const ai32x4 rs = a_rsrc((op ? P.dout : P.q) + rowbase * ld + head * 32, (int64_t)T * ld * 2);
-    const int prow = lane >> 1, pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
-    char* dst = lds + op * OFF_DO + cb * SL_SUB;
-    for (int sl = 0; sl < nt; ++sl) {
-      const int grow = sl * 32 + prow;
-      const int voff = grow < T ? (grow * ld + cb * 16 + pcol) * 2 : A_OOB;
-      a_dma16(rs, __builtin_amdgcn_readfirstlane(a_lds_u32(dst + sl * SL_SLICE)), voff);
+  // Prologue. Every global load of the kernel is issued here and waited for (pinned) BEFORE the Q / dO
+  // slices go out by LDS-DMA (the compiler counts only its own loads, so a wait it places while DMAs it
+  // cannot see are in flight would drain them): the keep-bit words of the wave's (step, tile) slots, the
+  // K / V rows of its key tiles, this thread's LSE / O / dO row. The slices then land while D, the
+  // tables and K^T are built and while the first steps run: step qt waits (counted vmcnt) only for its
+  // own piece of slice qt + 1, so the loop issues no other vector-memory operation but one dQ store per
+  // step (a buffer store with out-of-range rows dropped: the count is fixed).
+  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+  uint32_t mwq[2][8];  // keep-bit word of tile t at step q (key r; a FIFO shifted once per step)
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      mwq[t][q] = 0u;
+      if (DROP && q < nt && kts[t] <= q)
+        mwq[t][q] = P.dmask[0][((int64_t)bh * ntri + q * (q + 1) / 2 + kts[t]) * 32 + key_dword(r)];
     }
-  }
-  // K / V rows of the wave's key tiles (keys on lanes)
   bf16x8 kf[2][2], vf[2][2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1150,30 +1178,66 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
       vf[t][s] = ld8(vp + 16 * s + 8 * h, ok);
     }
   }
+  float lse_t = 0.f;
+  u32x4 ov[4], dv4[4];
+  {
+    const bool ok = tid < T;
+    const int64_t t0 = ok ? tid : 0;
+    lse_t = P.lse[0][(int64_t)bh * T + t0];
+    const bf16_t* orow = P.o + (rowbase + t0) * P.o_ld + head * 32;
+    const bf16_t* drow = P.dout + (rowbase + t0) * P.dout_ld + head * 32;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      ov[c] = *reinterpret_cast<const u32x4*>(orow + 8 * c);
+      dv4[c] = *reinterpret_cast<const u32x4*>(drow + 8 * c);
+    }
+  }
+  // pins: the compiler's waits for all of the above land here, ahead of the DMAs
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(mwq[t][q]));
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      asm volatile("" : "+v"(kf[t][s]));
+      asm volatile("" : "+v"(vf[t][s]));
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    asm volatile("" : "+v"(ov[c]));
+    asm volatile("" : "+v"(dv4[c]));
+  }
+  asm volatile("" : "+v"(lse_t));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // Q (waves 0, 2) and dO (waves 1, 3) images: wave w streams column half w >> 1 of every slice, in
+  // slice order (nt pieces: the loop's counted waits)
+  {
+    const int op = w & 1, cb = w >> 1;
+    const int ld = op ? P.dout_ld : P.q_ld;
+    const ai32x4 rs = a_rsrc((op ? P.dout : P.q) + rowbase * ld + head * 32, (int64_t)T * ld * 2);
+    const int prow = lane >> 1, pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
+    char* dst = lds + op * OFF_DO + cb * SL_SUB;
+    for (int sl = 0; sl < nt; ++sl) {
+      const int grow = sl * 32 + prow;
+      const int voff = grow < T ? (grow * ld + cb * 16 + pcol) * 2 : A_OOB;
+      a_dma16(rs, __builtin_amdgcn_readfirstlane(a_lds_u32(dst + sl * SL_SLICE)), voff);
+    }
+  }
   // the LSE / D tables: thread t holds query t
   float* tab = reinterpret_cast<float*>(lds + OFF_TAB);
   {
-    float nl = 0.f, dsum = 0.f;
-    if (tid < T) {
-      nl = -P.lse[0][(int64_t)bh * T + tid];
-      const bf16_t* orow = P.o + (rowbase + tid) * P.o_ld + head * 32;
-      const bf16_t* drow = P.dout + (rowbase + tid) * P.dout_ld + head * 32;
-      u32x4 ov[4], dv4[4];
+    float dsum = 0.f;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        ov[c] = *reinterpret_cast<const u32x4*>(orow + 8 * c);
-        dv4[c] = *reinterpret_cast<const u32x4*>(drow + 8 * c);
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dsum += bf2f(ov[c][e] & 0xffff) * bf2f(dv4[c][e] & 0xffff);
+        dsum += bf2f(ov[c][e] >> 16) * bf2f(dv4[c][e] >> 16);
       }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          dsum += bf2f(ov[c][e] & 0xffff) * bf2f(dv4[c][e] & 0xffff);
-          dsum += bf2f(ov[c][e] >> 16) * bf2f(dv4[c][e] >> 16);
-        }
-    }
-    tab[tid] = nl;
-    tab[256 + tid] = DROP ? -dsum / P.drop_scale : -dsum;
+    const bool ok = tid < T;
+    tab[tid] = ok ? -lse_t : -INFINITY;  // rows past T: P = exp2(-inf) = 0 (the ragged last tile's mask)
+    tab[256 + tid] = ok ? (DROP ? -dsum / P.drop_scale : -dsum) : 0.f;
   }
   // K^T of the wave's key tiles (d on lanes, keys in the permuted k order of the transposed reads),
   // through the wave's slot: the [key][q] dS image of the dQ product uses the same layout (8-B chunk c
@@ -1198,8 +1262,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     for (int s = 0; s < 2; ++s) ktf[t][s] = join4(lds_tr16(slot + o_da0 + 1024 * s), lds_tr16(slot + o_da1 + 1024 * s));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces landed
-  __syncthreads();                                  // everyone's pieces and table entries
+  a_wait_vm(nt - 1);  // this wave's piece of slice 0 (the younger nt - 1 pieces stay in flight)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // everyone's slice-0 pieces and table entries
 
   // element e of a tile accumulator is query row (e & 3) + 8 (e >> 2) + 4 h of the tile, key r: bit e
   // of m_diag keeps the diagonal tile's causal half, bit e of m_rows the rows of a ragged last query
@@ -1219,7 +1284,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
 
   // one owned key tile (t) against query tile qt; mw: the tile's keep bits (key r, this lane's half),
   // mk: the causal / ragged mask bits of a MASKED tile
-  auto tile = [&](auto mc, int qt, int t, uint32_t mw, uint32_t mk, f32x16& dqp) {
+  auto tile = [&](auto mc, int qt, int t, uint32_t mw, uint32_t mk, f32x16& dqp, bool diag) {
     constexpr bool MASKED = decltype(mc)::value;
     asm volatile("" ::: "memory");  // the slot's previous reads stay ahead of this tile's writes
     const int q0 = qt * 32;
@@ -1236,6 +1301,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     for (int s = 0; s < 2; ++s) {
       sacc = mfma32(qr[s], kf[t][s], sacc);    // S[q][key]
       dpacc = mfma32(dr[s], vf[t][s], dpacc);  // dP[q][key]
+    }
+    if (!MASKED && MMT_F32_BRANCH == 0 && diag) {  // wave-uniform: the diagonal tile
+      asm volatile("" ::: "memory");  // a real branch: selects on every tile cost 16 VALU
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sacc[e] = (mk >> e) & 1 ? sacc[e] : -INFINITY;
     }
     uint32_t pp[8], dd[8];  // packed bf16 pairs of Z P (dV operand) and dS / sc (dK operand)
 #pragma unroll
@@ -1288,38 +1358,140 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     }
   };
 
-  // keep-bit dwords of a tile (key-major record of attn_mask_kernel), prefetched one step ahead
-  const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
-  const uint32_t* mrec = DROP ? P.dmask[0] + (int64_t)bh * ntri * 32 + key_dword(r) : nullptr;
-  auto mword = [&](int qt, int kt) -> uint32_t {
-    return (DROP && kt <= qt && kt < nt) ? mrec[(qt * (qt + 1) / 2 + kt) * 32] : 0u;
-  };
-  uint32_t mwA = mword(0, kts[0]), mwB = mword(0, kts[1]);
-  const float dqs = DROP ? scale * P.drop_scale : scale;
-  const int R = 8 * w + (lane >> 3), cq = lane & 7;  // this wave's dQ rows / 16-B column chunk
-#pragma unroll 1
-  for (int qt = 0; qt < nt; ++qt) {
-    const uint32_t cA = mwA >> (4 * h), cB = mwB >> (4 * h);
-    if (qt + 1 < nt) {
-      mwA = mword(qt + 1, kts[0]);
-      mwB = mword(qt + 1, kts[1]);
+  // both owned key tiles against query tile qt in one straight-line body (qt >= 7 - w): the Q / dO row and
+  // transposed fragments and the LSE / D rows are read once for the two tiles, and the two tiles' S / dP ->
+  // softmax -> dV / dK chains are independent, so one's MFMAs overlap the other's VALU in the wave
+  auto tile2 = [&](int qt, uint32_t mwa, uint32_t mwb, f32x16& dqp, bool diagA, bool diagB) {
+    asm volatile("" ::: "memory");
+    const int q0 = qt * 32;
+    bf16x8 qr[2], dr[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qr[s] = sl_row(qimg, q0, r, s, h);
+      dr[s] = sl_row(dimg, q0, r, s, h);
     }
+    f32x16 sacc[2], dpacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      zero16(sacc[t]);
+      zero16(dpacc[t]);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        sacc[t] = mfma32(qr[s], kf[t][s], sacc[t]);
+        dpacc[t] = mfma32(dr[s], vf[t][s], dpacc[t]);
+      }
+    if (diagA || diagB) {  // wave-uniform
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          sacc[t][e] = ((t ? diagB : diagA) && !((m_diag >> e) & 1)) ? -INFINITY : sacc[t][e];
+    }
+    uint32_t pp[2][8], dd[2][8];
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(tab + q0 + 8 * gg + 4 * h);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(tab + 256 + q0 + 8 * gg + 4 * h);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t mw = t ? mwb : mwa;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; e4 += 2) {
+          float pm[2], ds[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int e = 4 * gg + e4 + u;
+            const float pv = ex2(__builtin_fmaf(sacc[t][e], c2, l4[e4 + u]));
+            if (DROP) {
+              int kb = __builtin_amdgcn_sbfe((int)mw, 8 * gg + e4 + u, 1);
+              asm volatile("" : "+v"(kb));
+              pm[u] = keep_f(pv, kb);
+              ds[u] = __builtin_fmaf(pm[u], dpacc[t][e], pv * d4[e4 + u]);
+            } else {
+              pm[u] = pv;
+              ds[u] = pv * (dpacc[t][e] + d4[e4 + u]);
+            }
+          }
+          pp[t][2 * gg + e4 / 2] = pack2bf(pm[0], pm[1]);
+          dd[t][2 * gg + e4 / 2] = pack2bf(ds[0], ds[1]);
+        }
+      }
+    }
+    bf16x8 dot[2], qtr[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      dot[s] = sl_tr(dimg, q0, s, lane);
+      qtr[s] = sl_tr(qimg, q0, s, lane);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      // tile t's dS through the slot (tile 1 writes after tile 0's dS^T reads: in-order LDS per wave)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+        *reinterpret_cast<u32x2*>(slot + sw(2 * gg + h)) = u32x2{dd[t][2 * gg], dd[t][2 * gg + 1]};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = __builtin_bit_cast(bf16x8, u32x4{pp[t][4 * s], pp[t][4 * s + 1], pp[t][4 * s + 2], pp[t][4 * s + 3]});
+        const bf16x8 df = __builtin_bit_cast(bf16x8, u32x4{dd[t][4 * s], dd[t][4 * s + 1], dd[t][4 * s + 2], dd[t][4 * s + 3]});
+        dv[t] = mfma32(pf, dot[s], dv[t]);
+        dk[t] = mfma32(df, qtr[s], dk[t]);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 da = join4(lds_tr16(slot + o_da0 + 1024 * s), lds_tr16(slot + o_da1 + 1024 * s));
+        dqp = mfma32(ktf[t][s], da, dqp);
+      }
+      asm volatile("" ::: "memory");
+    }
+  };
+
+  const float dqs = DROP ? scale * P.drop_scale : scale;
+  const ai32x4 rdq = a_rsrc(P.dq + rowbase * P.dq_ld + head * 32, (int64_t)T * P.dq_ld * 2);
+  const int R = 8 * w + (lane >> 3), cq = lane & 7;  // this wave's dQ rows / 16-B column chunk
+#ifndef MMT_F32_SKIP
+#define MMT_F32_SKIP 0
+#endif
+#pragma unroll 1
+  for (int qt = 0; qt < (MMT_F32_SKIP ? 0 : nt); ++qt) {
+    const uint32_t cA = mwq[0][0] >> (4 * h), cB = mwq[1][0] >> (4 * h);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < 7; ++q) mwq[t][q] = mwq[t][q + 1];
     f32x16 dqp;
     zero16(dqp);
     const bool last_ragged = ragged && qt == nt - 1;
+#if MMT_F32_PAIR
+    if (kts[1] < nt && kts[1] <= qt) {  // both tiles (kts[0] < kts[1])
+      tile2(qt, cA, cB, dqp, kts[0] == qt, kts[1] == qt);
+    } else if (kts[0] <= qt) {
+      tile(std::false_type{}, qt, 0, cA, m_diag, dqp, kts[0] == qt);
+    }
+#else
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int kt = kts[t];
       if (kt < nt && kt <= qt) {
         const uint32_t mw = t ? cB : cA;
-        if (kt == qt || last_ragged) {
-          const uint32_t mk = (kt == qt ? m_diag : 0xffffu) & (last_ragged ? m_rows : 0xffffu);
-          tile(std::true_type{}, qt, t, mw, mk, dqp);
-        } else {
-          tile(std::false_type{}, qt, t, mw, 0xffffu, dqp);
-        }
+        const uint32_t mk = (kt == qt ? m_diag : 0xffffu) & (last_ragged ? m_rows : 0xffffu);
+#if MMT_F32_BRANCH == 1
+        // separate masked / unmasked tile bodies: the accumulators then take register copies at the joins
+        if (kt == qt || last_ragged) tile(std::true_type{}, qt, t, mw, mk, dqp, false);
+        else tile(std::false_type{}, qt, t, mw, mk, dqp, false);
+#elif MMT_F32_BRANCH == 2
+        tile(std::true_type{}, qt, t, mw, mk, dqp, false);  // one body, the mask applied on every tile
+#else
+        // one body; the diagonal tile's scores above the diagonal become -inf in a branch that touches
+        // only the score accumulator (rows past T: -inf LSE-table entries)
+        tile(std::false_type{}, qt, t, mw, m_diag, dqp, kt == qt);
+#endif
       }
     }
+#endif
     char* part = lds + OFF_DQ + ((qt & 1) * 4 + w) * 4096;
     if (w <= qt) {  // this wave had a tile in the step (its key tile w is the lower one)
 #pragma unroll
@@ -1327,17 +1499,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
         *reinterpret_cast<f32x4*>(part + r * 128 + (((2 * gg + h) ^ (r & 7)) << 4)) =
             f32x4{dqp[4 * gg], dqp[4 * gg + 1], dqp[4 * gg + 2], dqp[4 * gg + 3]};
     }
+    // this wave's piece of slice qt + 1: younger are the pieces of slices qt + 2 .. nt - 1 and the dQ
+    // stores of steps 0 .. qt - 1, nt - 2 operations at every step
+    if (qt + 1 < nt) a_wait_vm(nt - 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every partial of step qt is written
+    __builtin_amdgcn_s_barrier();  // every partial of step qt is written; slice qt + 1 landed
     {
       const int nw = min(qt + 1, 4);
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
       for (int u = 0; u < nw; ++u)
         a += *reinterpret_cast<const f32x4*>(lds + OFF_DQ + ((qt & 1) * 4 + u) * 4096 + R * 128 + ((cq ^ (R & 7)) << 4));
       const int tq = qt * 32 + R;
-      if (tq < T)
-        *reinterpret_cast<u32x2*>(P.dq + (rowbase + tq) * P.dq_ld + head * 32 + 4 * cq) =
-            u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)};
+      a_bst8(rdq, tq < T ? (tq * P.dq_ld + 4 * cq) * 2 : A_OOB,
+             u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)});
     }
   }
 
