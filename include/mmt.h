@@ -264,6 +264,15 @@ int mmt_op_attention_bwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t 
                          int32_t kv_hstride, const void* o, int32_t o_ld, const void* const* oj,
                          const float* const* lse, const void* dout, int32_t dout_ld, float* const* dvec, void* dq,
                          int32_t dq_ld, void* const* dk, void* const* dv, int32_t dkv_ld, int32_t dkv_hstride);
+/* the same with a caller scratch of fp32 rows [B*T][>= H*hs] (dq32_ld % 4 == 0, 16-B aligned; contents
+ * undefined afterwards): the one-pass hs-32 backward (T <= 256) sums dQ over several KV streams there,
+ * so cross-attention takes it too (without scratch it takes the two-pass kernels) */
+int mmt_op_attention_bwd_ws(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams,
+                            const void* q, int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld,
+                            int32_t kv_hstride, const void* o, int32_t o_ld, const void* const* oj,
+                            const float* const* lse, const void* dout, int32_t dout_ld, float* const* dvec, void* dq,
+                            int32_t dq_ld, void* const* dk, void* const* dv, int32_t dkv_ld, int32_t dkv_hstride,
+                            float* dq32, int32_t dq32_ld);
 int mmt_op_qkv2_fwd(void* stream, int32_t R, int32_t nblk, int32_t hs, const void* h1, int32_t ld_h1,
                     const float* w2, void* out, int32_t ld_out);
 int mmt_op_qkv2_bwd(void* stream, int32_t R, int32_t nblk, int32_t hs, const void* h1, int32_t ld_h1,

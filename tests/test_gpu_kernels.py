@@ -494,7 +494,7 @@ def _attn_ref(q, ks, vs, scale):
                                          # longer than one LDS chunk (256 rows at hs <= 32, 128 above)
                                          (1, 300, 2, 32, 1), (1, 300, 2, 32, 3), (1, 520, 2, 64, 2),
                                          (1, 1024, 1, 64, 1), (1, 257, 1, 24, 1)])
-def test_attention_fwd_bwd(B, T, H, hs, ns):
+def test_attention_fwd_bwd(B, T, H, hs, ns, scratch=False):
     torch.manual_seed(B * 1000 + T * 10 + hs + ns)
     C = H * hs
     R = B * T
@@ -550,10 +550,15 @@ def test_attention_fwd_bwd(B, T, H, hs, ns):
         dkp, dvp = dkvs, [d[:, hs:] for d in dkvs]
         dkv_ld, dkv_hs = 2 * C, 2 * hs
     dvec = [torch.zeros(B * H * T, device=DEV) for _ in range(ns)]
-    rc = L.mmt_op_attention_bwd(_s(), B, T, H, hs, ns, ML.ptr(q), q_ld, kp, vp, kv_ld, kv_hs, ML.ptr(o), C,
-                                ML.ptr_array(oj), ML.ptr_array(lse), ML.ptr(do), C, ML.ptr_array(dvec), ML.ptr(dq_ptr),
-                                dq_ld, (ctypes.c_void_p * ns)(*[t.data_ptr() for t in dkp]),
-                                (ctypes.c_void_p * ns)(*[t.data_ptr() for t in dvp]), dkv_ld, dkv_hs)
+    args = [_s(), B, T, H, hs, ns, ML.ptr(q), q_ld, kp, vp, kv_ld, kv_hs, ML.ptr(o), C, ML.ptr_array(oj),
+            ML.ptr_array(lse), ML.ptr(do), C, ML.ptr_array(dvec), ML.ptr(dq_ptr), dq_ld,
+            (ctypes.c_void_p * ns)(*[t.data_ptr() for t in dkp]), (ctypes.c_void_p * ns)(*[t.data_ptr() for t in dvp]),
+            dkv_ld, dkv_hs]
+    if scratch:  # fp32 dQ rows for the one-pass hs-32 backward over several KV streams (poisoned: fully written)
+        dq32 = torch.full((R, C + 4), float("nan"), device=DEV)
+        rc = L.mmt_op_attention_bwd_ws(*args, ML.ptr(dq32), C + 4)
+    else:
+        rc = L.mmt_op_attention_bwd(*args)
     assert rc == 0
     _sync()
     if ns == 1:
@@ -588,17 +593,21 @@ def test_attention_hs64_backward_variants(B, T, H, ns, ring):
         L.mmt_attn_set_ring(old)
 
 
-@pytest.mark.parametrize("ring", [79, 15])
-@pytest.mark.parametrize("B,T,H,ns", [(2, 256, 8, 1), (3, 37, 2, 1), (1, 2, 2, 1), (2, 255, 1, 1), (1, 33, 4, 1),
-                                      (4, 224, 2, 1), (2, 256, 2, 2), (1, 300, 2, 1)])
-def test_attention_hs32_backward_variants(B, T, H, ns, ring):
-    """The one-pass hs-32 backward (mmt_attn_set_ring bit 6, default: T <= 256 and one KV stream) and
-    the two-pass pair (ring 15) against the same torch reference: full, ragged, single-position and
-    one-tile sequences; the multi-stream and T > 256 cases take the two-pass pair under either knob."""
+@pytest.mark.parametrize("ring", [79 | 128, 79, 15])
+@pytest.mark.parametrize("B,T,H,ns,scratch", [(2, 256, 8, 1, False), (3, 37, 2, 1, False), (1, 2, 2, 1, False),
+                                              (2, 255, 1, 1, False), (1, 33, 4, 1, False), (4, 224, 2, 1, False),
+                                              (2, 256, 2, 2, False), (1, 300, 2, 1, False), (2, 256, 2, 3, True),
+                                              (3, 37, 2, 2, True), (1, 100, 4, 7, True), (2, 64, 1, 4, True),
+                                              (1, 300, 2, 3, True)])
+def test_attention_hs32_backward_variants(B, T, H, ns, scratch, ring):
+    """The one-pass hs-32 backward (mmt_attn_set_ring bit 6, default: T <= 256; with bit 7 also several KV
+    streams when the caller passes fp32 dQ scratch, mmt_op_attention_bwd_ws) and the two-pass pair (ring 15) against the
+    same torch reference: full, ragged, two-position and one-tile sequences, up to 7 KV streams; without
+    scratch the multi-stream cases, and every T > 256 case, take the two-pass pair under either knob."""
     L = ML.lib()
     old = L.mmt_attn_set_ring(ring)
     try:
-        test_attention_fwd_bwd(B, T, H, 32, ns)
+        test_attention_fwd_bwd(B, T, H, 32, ns, scratch)
     finally:
         L.mmt_attn_set_ring(old)
 

@@ -143,14 +143,17 @@ def test_dropout_fused_hs64_backward_matches_oracle(C, H, T, cross, p):
         L.mmt_attn_set_ring(old)
 
 
-@pytest.mark.parametrize("ring", [79, 15])
+@pytest.mark.parametrize("ring", [79 | 128, 79, 15])
 @pytest.mark.parametrize("C,H,T,cross,p", [(64, 2, 256, [True, False], 0.1), (64, 2, 37, [False, True], 0.2),
-                                             (96, 3, 200, [True, False], 0.1), (64, 2, 31, [True, False], 0.1)])
+                                             (96, 3, 200, [True, False], 0.1), (64, 2, 31, [True, False], 0.1),
+                                             (64, 2, 256, [True, False, True, False], 0.1),
+                                             (64, 2, 77, [False, True, True], 0.2)])
 def test_dropout_hs32_one_pass_backward_matches_oracle(C, H, T, cross, p, ring):
     """The one-pass hs-32 attention backward (mmt_attn_set_ring bit 6, default; T <= 256 and one KV
     stream, so both the self-attention and -- at two modalities -- the one-stream cross-attention take
-    it) under dropout against the oracle's hash masks, at full, ragged and single-position T; ring 15
-    is the two-pass pair on the same cases."""
+    it; with 3-4 modalities and bit 7 the cross-attention walks 2-3 KV streams with its dQ summed in the
+    engine's fp32 scratch) under dropout against the oracle's hash masks, at full and ragged T; ring 15 is the
+    two-pass pair on the same cases."""
     L = ML.lib()
     old = L.mmt_attn_set_ring(ring)
     try:
@@ -167,7 +170,7 @@ def test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p):
     attention kernels, against the oracle's hash masks (random init, the oracle as reference)."""
     import mmt_oracle as O
     import model as mmt_model
-    V = [13, 7]
+    V = [13, 7, 5, 11][:len(cross)]
     ocfg = O.OracleConfig(C, H, 1, T, V, cross)
     g = torch.Generator().manual_seed(5)
     sd = O.init_params(ocfg, g)

@@ -22,6 +22,7 @@ import mmt_lib as ML  # noqa: E402
 SHAPES = {
     # name: (B (modalities x batch), T, H, hs, streams)
     "c1": (256, 256, 8, 32, 1),
+    "c1_ca": (64, 256, 8, 32, 3),  # C1's cross-attention: one query modality, 3 KV streams
     "target": (128, 512, 8, 64, 1),
     "c3": (128, 1024, 8, 64, 1),
     "c3_ca": (64, 1024, 8, 64, 7),
@@ -69,11 +70,13 @@ def setup(B, T, H, hs, ns):
         assert L.mmt_op_attention_fwd(s, B, T, H, hs, ns, ML.ptr(q), q_ld, vp(kptr), vp(vptr), kv_ld, kv_hs, ML.ptr(o), C,
                                       ML.ptr_array(oj), ML.ptr_array(lse)) == 0
 
+    dq32 = torch.zeros(R, C, device=dev)  # fp32 dQ rows of the one-pass hs-32 multi-stream backward (the engine's dln)
+
     def bwd():
-        assert L.mmt_op_attention_bwd(s, B, T, H, hs, ns, ML.ptr(q), q_ld, vp(kptr), vp(vptr), kv_ld, kv_hs, ML.ptr(o), C,
+        assert L.mmt_op_attention_bwd_ws(s, B, T, H, hs, ns, ML.ptr(q), q_ld, vp(kptr), vp(vptr), kv_ld, kv_hs, ML.ptr(o), C,
                                       ML.ptr_array(oj), ML.ptr_array(lse), ML.ptr(do), C, ML.ptr_array(dvec),
-                                      ML.ptr(dq), dq_ld, vp(dk), vp(dv), dkv_ld, dkv_hs) == 0
-    return fwd, bwd, keep + [o, oj, lse, dvec, do]
+                                      ML.ptr(dq), dq_ld, vp(dk), vp(dv), dkv_ld, dkv_hs, ML.ptr(dq32), C) == 0
+    return fwd, bwd, keep + [o, oj, lse, dvec, do, dq32]
 
 
 def timeit(fn, reps):

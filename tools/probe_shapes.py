@@ -16,6 +16,7 @@ import mmt_oracle as O  # noqa: E402
 
 
 def run(C, H, T=16, V=(11, 7), B=3, cross=(True, False), L=2):
+    cross = tuple(cross[:len(V)])
     import model as mmt_model
     ocfg = O.OracleConfig(C, H, L, T, list(V), list(cross))
     g = torch.Generator().manual_seed(11)
@@ -35,14 +36,22 @@ def run(C, H, T=16, V=(11, 7), B=3, cross=(True, False), L=2):
     _, rl, rg = O.forward_backward(sd, ocfg, idx, tgt)
     bad = [k for k, t in m.reference_grad_views() if t is not None and not torch.isfinite(t).all()]
     print(f"C={C} H={H}: losses {[round(float(l), 4) for l in losses]} ref {[round(float(l), 4) for l in rl]} "
-          f"logits finite {[bool(torch.isfinite(x).all()) for x in logits]} non-finite grads {len(bad)}: {bad[:6]}",
+          f"logits finite {[bool(torch.isfinite(x).all()) for x in logits]} non-finite grads {len(bad)}: {bad[-8:]}",
           flush=True)
 
 
 if __name__ == "__main__":
     for a in sys.argv[1:]:
-        c, h = (int(x) for x in a.split(","))
+        f = a.split(",")
+        c, h = int(f[0]), int(f[1])
+        kw = {}
+        if len(f) > 2:
+            kw["L"] = int(f[2])
+        if len(f) > 3:
+            kw["V"] = (11, 7)[:int(f[3])]
+        if len(f) > 4:
+            kw["T"] = int(f[4])
         try:
-            run(c, h)
+            run(c, h, **kw)
         except Exception as e:  # noqa: BLE001
             print(f"C={c} H={h}: {type(e).__name__}: {e}", flush=True)

@@ -1103,6 +1103,9 @@ __device__ __forceinline__ void a_dma16(const ai32x4& rsrc, uint32_t lds, int vo
 __device__ __forceinline__ void a_bst8(const ai32x4& rsrc, int voff, u32x2 v) {
   asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" : : "v"(v), "v"(voff), "s"(rsrc) : "memory");
 }
+__device__ __forceinline__ void a_bst16(const ai32x4& rsrc, int voff, f32x4 v) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen" : : "v"(v), "v"(voff), "s"(rsrc) : "memory");
+}
 // counted wait on this wave's outstanding vector-memory operations (immediate operand, n <= 8)
 __device__ __forceinline__ void a_wait_vm(int n) {
   switch (n) {
@@ -1123,10 +1126,13 @@ constexpr int A_OOB = 0x7fffffff;
 #ifndef MMT_F32_BRANCH
 #define MMT_F32_BRANCH 0
 #endif
+#ifndef MMT_F32_REV
+#define MMT_F32_REV 0
+#endif
 #ifndef MMT_F32_PAIR
 #define MMT_F32_PAIR 0  // 1: the two-tile body where both owned key tiles are active (register copies: slower)
 #endif
-template <bool DROP>
+template <bool DROP, bool MS>  // MS: several KV streams (cross-attention)
 __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int T, int H, float scale) {
   constexpr int IMG = 8 * SL_SLICE;               // 256 rows x 32 columns as slice images
   constexpr int OFF_DO = IMG, OFF_TAB = 2 * IMG;  // tables: -LSE2 [256], -D (-D / sc under dropout) [256]
@@ -1135,7 +1141,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
   constexpr int BYTES = OFF_DQ + 8 * 4096;
   static_assert(2 * BYTES <= 160 * 1024, "two workgroups per CU");
   constexpr int EPW = 40;                          // epilogue transpose row stride (bf16)
-  static_assert(4 * 2 * 32 * EPW * 2 <= 2 * IMG, "epilogue transposes alias the Q / dO images");
+  static_assert(4 * 32 * EPW * 2 <= 4 * 4096, "epilogue transposes alias one parity of the dQ partials");
   __shared__ __attribute__((aligned(1024))) char lds[BYTES];
   const AttnProblem& P = batch.p[blockIdx.z];
   const int nt = (T + 31) / 32;
@@ -1147,6 +1153,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
   const float c2 = scale * kLog2e;
   const bool ragged = (T & 31) != 0;
   const int kts[2] = {w, 7 - w};
+  // walk direction: MMT_F32_REV sends the second slot's workgroups of the first generation (blocks
+  // 256 .. 511: one per CU) down from the last query tile, so the two co-resident workgroups are in
+  // opposite phases of the causal imbalance (light first steps vs heavy last steps)
+  const bool rev = MMT_F32_REV && ((blockIdx.x >> 8) & 1);
+  auto step_qt = [&](int i) { return rev ? nt - 1 - i : i; };
 
   // Prologue. Every global load of the kernel is issued here and waited for (pinned) BEFORE the Q / dO
   // slices go out by LDS-DMA (the compiler counts only its own loads, so a wait it places while DMAs it
@@ -1156,22 +1167,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
   // own piece of slice qt + 1, so the loop issues no other vector-memory operation but one dQ store per
   // step (a buffer store with out-of-range rows dropped: the count is fixed).
   const int64_t ntri = (int64_t)nt * (nt + 1) / 2;
+  const int ns = MS ? P.nstreams : 1;
+  // cross-attention (several KV streams): the workgroup walks the streams one after the other with Q / dO
+  // resident; dQ sums over the streams in the caller's fp32 scratch rows (P.dq32: written by stream 0,
+  // read-added by the middle streams, read and converted into dq by the last)
+  const ai32x4 rdq32 = a_rsrc(MS ? P.dq32 + rowbase * P.dq32_ld + head * 32 : nullptr, MS ? (int64_t)T * P.dq32_ld * 4 : 0);
+#pragma unroll 1
+  for (int j = 0; j < ns; ++j) {
+  const bf16_t* const oj = MS ? P.oj[j] : P.o;
   uint32_t mwq[2][8];  // keep-bit word of tile t at step q (key r; a FIFO shifted once per step)
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      mwq[t][q] = 0u;
-      if (DROP && q < nt && kts[t] <= q)
-        mwq[t][q] = P.dmask[0][((int64_t)bh * ntri + q * (q + 1) / 2 + kts[t]) * 32 + key_dword(r)];
+    for (int i = 0; i < 8; ++i) {  // step i's query tile
+      const int q = step_qt(i);
+      mwq[t][i] = 0u;
+      if (DROP && i < nt && kts[t] <= q)
+        mwq[t][i] = P.dmask[j][((int64_t)bh * ntri + q * (q + 1) / 2 + kts[t]) * 32 + key_dword(r)];
     }
   bf16x8 kf[2][2], vf[2][2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int tk = kts[t] * 32 + r;
     const bool ok = kts[t] < nt && tk < T;
-    const bf16_t* kp = P.k[0] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
-    const bf16_t* vp = P.v[0] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
+    const bf16_t* kp = P.k[j] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
+    const bf16_t* vp = P.v[j] + head * P.kv_hstride + (rowbase + tk) * P.kv_ld;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       kf[t][s] = ld8(kp + 16 * s + 8 * h, ok);
@@ -1183,8 +1203,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
   {
     const bool ok = tid < T;
     const int64_t t0 = ok ? tid : 0;
-    lse_t = P.lse[0][(int64_t)bh * T + t0];
-    const bf16_t* orow = P.o + (rowbase + t0) * P.o_ld + head * 32;
+    lse_t = P.lse[j][(int64_t)bh * T + t0];
+    const bf16_t* orow = oj + (rowbase + t0) * P.o_ld + head * 32;
     const bf16_t* drow = P.dout + (rowbase + t0) * P.dout_ld + head * 32;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -1211,14 +1231,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
   asm volatile("" : "+v"(lse_t));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // Q (waves 0, 2) and dO (waves 1, 3) images: wave w streams column half w >> 1 of every slice, in
-  // slice order (nt pieces: the loop's counted waits)
-  {
+  // slice order (nt pieces: the loop's counted waits); once, for the first stream
+  if (j == 0) {
     const int op = w & 1, cb = w >> 1;
     const int ld = op ? P.dout_ld : P.q_ld;
     const ai32x4 rs = a_rsrc((op ? P.dout : P.q) + rowbase * ld + head * 32, (int64_t)T * ld * 2);
     const int prow = lane >> 1, pcol = 8 * ((lane & 1) ^ ((prow >> 3) & 1));
     char* dst = lds + op * OFF_DO + cb * SL_SUB;
-    for (int sl = 0; sl < nt; ++sl) {
+    for (int i = 0; i < nt; ++i) {  // in step order
+      const int sl = step_qt(i);
       const int grow = sl * 32 + prow;
       const int voff = grow < T ? (grow * ld + cb * 16 + pcol) * 2 : A_OOB;
       a_dma16(rs, __builtin_amdgcn_readfirstlane(a_lds_u32(dst + sl * SL_SLICE)), voff);
@@ -1262,9 +1283,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     for (int s = 0; s < 2; ++s) ktf[t][s] = join4(lds_tr16(slot + o_da0 + 1024 * s), lds_tr16(slot + o_da1 + 1024 * s));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  a_wait_vm(nt - 1);  // this wave's piece of slice 0 (the younger nt - 1 pieces stay in flight)
+  if (j == 0) a_wait_vm(nt - 1);  // this wave's piece of slice 0 (the younger nt - 1 pieces stay in flight)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous stream's dQ-sum stores are done
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // everyone's slice-0 pieces and table entries
+  __builtin_amdgcn_s_barrier();  // everyone's slice-0 pieces and table entries (later streams: and every
+                                 // wave is past the previous stream's epilogue)
 
   // element e of a tile accumulator is query row (e & 3) + 8 (e >> 2) + 4 h of the tile, key r: bit e
   // of m_diag keeps the diagonal tile's causal half, bit e of m_rows the rows of a ragged last query
@@ -1456,7 +1479,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
 #define MMT_F32_SKIP 0
 #endif
 #pragma unroll 1
-  for (int qt = 0; qt < (MMT_F32_SKIP ? 0 : nt); ++qt) {
+  for (int i = 0; i < (MMT_F32_SKIP ? 0 : nt); ++i) {
+    const int qt = step_qt(i);
     const uint32_t cA = mwq[0][0] >> (4 * h), cB = mwq[1][0] >> (4 * h);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -1492,7 +1516,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
       }
     }
 #endif
-    char* part = lds + OFF_DQ + ((qt & 1) * 4 + w) * 4096;
+    char* part = lds + OFF_DQ + ((i & 1) * 4 + w) * 4096;
     if (w <= qt) {  // this wave had a tile in the step (its key tile w is the lower one)
 #pragma unroll
       for (int gg = 0; gg < 4; ++gg)
@@ -1501,56 +1525,62 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     }
     // this wave's piece of slice qt + 1: younger are the pieces of slices qt + 2 .. nt - 1 and the dQ
     // stores of steps 0 .. qt - 1, nt - 2 operations at every step
-    if (qt + 1 < nt) a_wait_vm(nt - 2);
+    if (j == 0 && i + 1 < nt) a_wait_vm(nt - 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every partial of step qt is written; slice qt + 1 landed
     {
       const int nw = min(qt + 1, 4);
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
       for (int u = 0; u < nw; ++u)
-        a += *reinterpret_cast<const f32x4*>(lds + OFF_DQ + ((qt & 1) * 4 + u) * 4096 + R * 128 + ((cq ^ (R & 7)) << 4));
+        a += *reinterpret_cast<const f32x4*>(lds + OFF_DQ + ((i & 1) * 4 + u) * 4096 + R * 128 + ((cq ^ (R & 7)) << 4));
       const int tq = qt * 32 + R;
-      a_bst8(rdq, tq < T ? (tq * P.dq_ld + 4 * cq) * 2 : A_OOB,
-             u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)});
+      if (!MS || j == ns - 1) {
+        if (MS && j > 0 && tq < T) a += *reinterpret_cast<const f32x4*>(P.dq32 + (rowbase + tq) * P.dq32_ld + head * 32 + 4 * cq);
+        a_bst8(rdq, tq < T ? (tq * P.dq_ld + 4 * cq) * 2 : A_OOB,
+               u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)});
+      } else {  // running fp32 sum over the streams (stream 0: one counted store per step, as above)
+        if (j > 0 && tq < T) a += *reinterpret_cast<const f32x4*>(P.dq32 + (rowbase + tq) * P.dq32_ld + head * 32 + 4 * cq);
+        a_bst16(rdq32, tq < T ? (tq * P.dq32_ld + 4 * cq) * 4 : A_OOB, a);
+      }
     }
   }
 
-  // dK / dV of the wave's key tiles, transposed through its LDS slot (in the Q / dO images, which
-  // no wave reads after the last step's barrier) into row-major 16-B pieces, as the dK/dV pass
+  // dK / dV of the wave's key tiles, transposed through LDS into row-major 16-B pieces (as the dK/dV
+  // pass), one matrix at a time through the dQ partials of the parity the last step did not use (no
+  // wave reads them after the last step's barrier; the next stream's first barrier retires these reads)
   const float dks = DROP ? scale * P.drop_scale : scale;
   const float dvs = DROP ? P.drop_scale : 1.f;
-  bf16_t* et = reinterpret_cast<bf16_t*>(lds) + w * (2 * 32 * EPW);
+  bf16_t* et = reinterpret_cast<bf16_t*>(lds + OFF_DQ + (nt & 1) * 4 * 4096) + w * (32 * EPW);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int kt = kts[t];
     if (kt >= nt) continue;
     const int k0 = kt * 32;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-      et[kr * EPW + r] = f2bf(dk[t][e] * dks);
-      et[32 * EPW + kr * EPW + r] = f2bf(dv[t][e] * dvs);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int mtx = 0; mtx < 2; ++mtx) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = i * 16 + (lane >> 2), d0 = (lane & 3) * 8;
-      const u32x4 vk = *reinterpret_cast<const u32x4*>(et + row * EPW + d0);
-      const u32x4 vv = *reinterpret_cast<const u32x4*>(et + 32 * EPW + row * EPW + d0);
-      if (k0 + row < T) {
-        const int64_t off = (rowbase + k0 + row) * P.dkv_ld + d0;
-        *reinterpret_cast<u32x4*>(P.dk[0] + head * P.dkv_hstride + off) = vk;
-        *reinterpret_cast<u32x4*>(P.dv[0] + head * P.dkv_hstride + off) = vv;
+      for (int e = 0; e < 16; ++e) {
+        const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        et[kr * EPW + r] = mtx ? f2bf(dv[t][e] * dvs) : f2bf(dk[t][e] * dks);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bf16_t* dst = (mtx ? P.dv[j] : P.dk[j]) + head * P.dkv_hstride;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = i * 16 + (lane >> 2), d0 = (lane & 3) * 8;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(et + row * EPW + d0);
+        if (k0 + row < T) *reinterpret_cast<u32x4*>(dst + (rowbase + k0 + row) * P.dkv_ld + d0) = v;
       }
     }
   }
+  }  // streams
 }
 
 // attention variant knob (bit 0: the slice-streamed hs-64 dK/dV pass, bit 1: its dQ pass, bit 2: the
 // dK/dV pass at 3 waves per SIMD, bit 3: the slice-streamed hs-64 forward, bit 5: the one-pass hs-64
-// backward at T <= 512 with one KV stream, bit 6: the one-pass hs-32 backward at T <= 256 with one KV
-// stream): MMT_ATTN_RING, or mmt_attn_set_ring() for in-process A/B
+// backward at T <= 512 with one KV stream, bit 6: the one-pass hs-32 backward at T <= 256, bit 7: that
+// kernel also for several KV streams): MMT_ATTN_RING, or mmt_attn_set_ring() for in-process A/B
 static int g_attn_ring = [] {
   const char* e = getenv("MMT_ATTN_RING");
   // both hs-64 passes on the rings (dQ: two query tiles per wave), dK/dV at 3 waves per SIMD
@@ -1601,19 +1631,31 @@ static hipError_t attn_launch(const AttnBatch& bt, int B, int T, int H, float sc
     const bool ring = HS == 64 && ring64_fits(bt, T);
     // knob bit 5: dQ, dK, dV in one pass (mmt_attn2.hip) for T <= 512 and one KV stream
     if (ring && (g_attn_ring & 32) && T <= 512 && ns == 1) return mmt_attn_bwd_fused64(bt, B, T, H, scale, drop, s);
-    // knob bit 6: dQ, dK, dV in one pass at hs 32 for T <= 256 and one KV stream (Q / dO rows by LDS-DMA:
-    // 16-B aligned rows, and sequences whose span fits a buffer descriptor)
-    if (HS == 32 && (g_attn_ring & 64) && T <= 256 && ns == 1) {
+    // knob bit 6: dQ, dK, dV in one pass at hs 32 for T <= 256 (Q / dO rows by LDS-DMA: 16-B aligned rows,
+    // and sequences whose span fits a buffer descriptor); several KV streams need the fp32 dQ scratch
+    if (HS == 32 && (g_attn_ring & 64) && T <= 256) {
       bool ok = true;
       for (int g = 0; g < bt.count; ++g) {
         const AttnProblem& P = bt.p[g];
         ok = ok && !(P.q_ld & 7) && !(P.dout_ld & 7) && !((uintptr_t)P.q & 15) && !((uintptr_t)P.dout & 15) &&
              !(P.kv_ld & 7) && !(P.kv_hstride & 7) && (int64_t)T * std::max(P.q_ld, P.dout_ld) * 2 < ((int64_t)1 << 31);
+        // several KV streams (knob bit 7, off by default): one workgroup walks the streams in turn, and at
+        // C1's cross-attention (3 streams, 512 workgroups: one generation) that measured slower than the
+        // two-pass pair, which spreads the dK/dV pass over 3x the workgroups (70.7 vs 67.9 us standalone,
+        // tools/attn_bench.py c1_ca, profiles/r6_attn_bench.txt)
+        if (ns > 1)
+          ok = ok && (g_attn_ring & 128) && P.dq32 && !(P.dq32_ld & 3) && !((uintptr_t)P.dq32 & 15) &&
+               (int64_t)T * P.dq32_ld * 4 < ((int64_t)1 << 31);
       }
       if (ok) {
         const dim3 grid(B * H, 1, bt.count);
-        if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true>), grid, dim3(256), 0, s, bt, T, H, scale);
-        else hipLaunchKernelGGL((attn_bwd_fused32<false>), grid, dim3(256), 0, s, bt, T, H, scale);
+        if (ns > 1) {
+          if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true, true>), grid, dim3(256), 0, s, bt, T, H, scale);
+          else hipLaunchKernelGGL((attn_bwd_fused32<false, true>), grid, dim3(256), 0, s, bt, T, H, scale);
+        } else {
+          if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true, false>), grid, dim3(256), 0, s, bt, T, H, scale);
+          else hipLaunchKernelGGL((attn_bwd_fused32<false, false>), grid, dim3(256), 0, s, bt, T, H, scale);
+        }
         return hipGetLastError();
       }
     }

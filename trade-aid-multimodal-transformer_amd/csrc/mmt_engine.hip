@@ -1555,6 +1555,9 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
       }
       q.kv_ld = 2 * C; q.kv_hstride = 2 * hs; q.o = r.W<bf16_t>(a[i].oc); q.o_ld = C; q.nstreams = M - 1;
       q.dout = r.W<bf16_t>(p.gdo[i]); q.dout_ld = C; q.dq = r.W<bf16_t>(p.gq[par][i]); q.dq_ld = C;
+      // fp32 rows for the one-pass hs-32 backward's dQ sum over the KV streams: dln is free here (the
+      // cross-query dX GEMM after the attention writes it)
+      q.dq32 = r.W<float>(p.dln[i]); q.dq32_ld = C;
       q.dkv_ld = 2 * C; q.dkv_hstride = 2 * hs;
       r.set_drop(q, l, i, DS_CA_PROB);
       if (r.drop)

@@ -208,6 +208,9 @@ struct AttnProblem {
   const bf16_t* dout; int dout_ld;
   float* dvec[MMT_MAX_STREAMS];  // rowsum(dO * O_j) per stream [B*H*T]
   bf16_t* dq; int dq_ld;
+  // optional fp32 scratch rows [B*T][>= H*hs] (dq32_ld % 4 == 0, 16-B aligned): the one-pass hs-32
+  // backward sums dQ over several KV streams there (required for it when nstreams > 1)
+  float* dq32; int dq32_ld;
   bf16_t* dk[MMT_MAX_STREAMS];
   bf16_t* dv[MMT_MAX_STREAMS];
   int dkv_ld, dkv_hstride;

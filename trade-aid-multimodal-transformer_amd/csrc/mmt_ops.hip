@@ -150,11 +150,27 @@ int mmt_op_attention_fwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t 
   return e == hipErrorInvalidValue ? MMT_ERR_UNSUPPORTED : st(e);
 }
 
+int mmt_op_attention_bwd_ws(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams,
+                            const void* q, int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld,
+                            int32_t kv_hstride, const void* o, int32_t o_ld, const void* const* oj,
+                            const float* const* lse, const void* dout, int32_t dout_ld, float* const* dvec, void* dq,
+                            int32_t dq_ld, void* const* dk, void* const* dv, int32_t dkv_ld, int32_t dkv_hstride,
+                            float* dq32, int32_t dq32_ld);
 int mmt_op_attention_bwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams, const void* q,
                          int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld, int32_t kv_hstride,
                          const void* o, int32_t o_ld, const void* const* oj, const float* const* lse, const void* dout,
                          int32_t dout_ld, float* const* dvec, void* dq, int32_t dq_ld, void* const* dk, void* const* dv,
                          int32_t dkv_ld, int32_t dkv_hstride) {
+  return mmt_op_attention_bwd_ws(stream, B, T, H, hs, nstreams, q, q_ld, k, v, kv_ld, kv_hstride, o, o_ld, oj, lse, dout,
+                                 dout_ld, dvec, dq, dq_ld, dk, dv, dkv_ld, dkv_hstride, nullptr, 0);
+}
+
+int mmt_op_attention_bwd_ws(void* stream, int32_t B, int32_t T, int32_t H, int32_t hs, int32_t nstreams,
+                            const void* q, int32_t q_ld, const void* const* k, const void* const* v, int32_t kv_ld,
+                            int32_t kv_hstride, const void* o, int32_t o_ld, const void* const* oj,
+                            const float* const* lse, const void* dout, int32_t dout_ld, float* const* dvec, void* dq,
+                            int32_t dq_ld, void* const* dk, void* const* dv, int32_t dkv_ld, int32_t dkv_hstride,
+                            float* dq32, int32_t dq32_ld) {
   if (nstreams < 1 || nstreams > MMT_MAX_STREAMS) return MMT_ERR_INVALID;
   AttnBatch b{};
   b.count = 1;
@@ -170,6 +186,7 @@ int mmt_op_attention_bwd(void* stream, int32_t B, int32_t T, int32_t H, int32_t 
   }
   p.dout = (const bf16_t*)dout; p.dout_ld = dout_ld; p.dq = (bf16_t*)dq; p.dq_ld = dq_ld;
   p.dkv_ld = dkv_ld; p.dkv_hstride = dkv_hstride;
+  p.dq32 = dq32; p.dq32_ld = dq32_ld;
   const float scale = 1.0f / __builtin_sqrtf((float)hs);
   const hipError_t e = mmt_launch_attn_bwd(b, B, T, H, hs, scale, (hipStream_t)stream);
   return e == hipErrorInvalidValue ? MMT_ERR_UNSUPPORTED : st(e);

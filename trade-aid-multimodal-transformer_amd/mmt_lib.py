@@ -110,6 +110,10 @@ _SIGS = {
                                      ctypes.POINTER(c_vp), c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(c_vp),
                                      ctypes.POINTER(c_vp), c_vp, c_i32, ctypes.POINTER(c_vp), c_vp, c_i32,
                                      ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i32, c_i32]),
+    "mmt_op_attention_bwd_ws": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(c_vp),
+                                        ctypes.POINTER(c_vp), c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(c_vp),
+                                        ctypes.POINTER(c_vp), c_vp, c_i32, ctypes.POINTER(c_vp), c_vp, c_i32,
+                                        ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i32, c_i32, c_vp, c_i32]),
     "mmt_op_qkv2_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32]),
     "mmt_op_qkv2_bwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "mmt_op_colsum": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_f32]),
