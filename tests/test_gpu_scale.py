@@ -244,13 +244,17 @@ def test_full_size_training_property_c3():
 
 def test_full_size_training_property_c4_fp8_vs_bf16():
     """C4 with the MX-fp8 forward GEMMs against the SAME 20 steps in bf16 (same seed, init, batch and dropout
-    masks; VERDICT r4 item 7): the fp8 run must learn what the bf16 run learns, per modality.
-    Band (stated here): where the bf16 loss falls clearly (by > 2 % of its start over the 20 steps), the fp8
-    loss must fall by at least half as much; where it does not (the small-vocabulary heads whose Linear(C,
-    V//2) -> tanh bottleneck moves slowly at lr 3e-4), the fp8 loss must not end more than 1 % of the start
-    above the bf16 one (one-sided: ending lower is not a failure to learn; a two-sided 1 % band failed once
-    on the V = 5 head with fp8 at -0.8 % and bf16 at +0.2 %, run-to-run atomics order). The totals both
-    fall by > 10 %."""
+    masks; VERDICT r4 item 7, r5 item 2): the fp8 run must learn what the bf16 run learns, per modality.
+    Band (stated here, two-sided): every modality's change over the 20 steps in fp8 within 3 % of its start
+    loss of the bf16 one; where the bf16 loss falls clearly (by > 2 % of its start), the fp8 loss must also
+    fall by at least half as much.
+    Why 3 %: the 20-step run is chaotic in both precisions. tools/fp8_drift.py (profiles/r6_fp8_drift.txt)
+    repeats it with the same seed (the gradients differ run to run only in the last bits: the order of the
+    float atomics of the bias / LayerNorm column sums, tests/test_gpu_determinism.py) and once from an init
+    moved by one ulp: the change/start of one modality spreads by up to 1.46 % in fp8 and 1.08 % in bf16
+    over those runs, so fp8 - bf16 differences up to ~2 % are noise (measured: at most 1.83 %); the band is
+    the sum of the two spreads rounded up. The earlier one-sided 1 % form read a fp8-only divergence into
+    two runs of that noise."""
     h8, flag8, fin8 = _train_full("c4", "fp8")
     h16, flag16, fin16 = _train_full("c4", "bf16")
     d8 = h8[-3:].mean(0) - h8[0]
@@ -264,7 +268,6 @@ def test_full_size_training_property_c4_fp8_vs_bf16():
     assert ((h8[0] - h16[0]).abs() / h16[0]).max() < 2e-2, (h8[0], h16[0])
     for i in range(h8.shape[1]):
         start = h16[0, i].item()
+        assert abs(d8[i] - d16[i]) <= 0.03 * start, (i, d8[i].item(), d16[i].item())
         if d16[i] < -0.02 * start:
             assert d8[i] < 0.5 * d16[i], (i, d8[i].item(), d16[i].item())
-        else:
-            assert d8[i] < d16[i] + 0.01 * start, (i, d8[i].item(), d16[i].item())

@@ -95,6 +95,7 @@ struct Plan {
   size_t dvec[MAXM][MAXM];
   size_t dkv[2][MAXM][MAXM];
   size_t celoss[MAXM];  // float [512]: the cross-entropy blocks' loss shares (summed in block order)
+  const void* gh1_pad_ws = nullptr;  // the workspace whose gh1 pad columns (written by no kernel) are zeroed
   size_t eperm[MAXM];  // int [R]: the rows in token order for the token-table gradient (mmt_launch_emb_sort)
   // KV-cache decode (generate): compact [B, *] rows of ONE new position per sequence
   struct Dec {
@@ -1710,6 +1711,18 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].dout = r.W<bf16_t>(p.gqkv[i]);
     qb.p[i].dh1 = r.W<bf16_t>(p.gh1[par][i]); qb.p[i].dw2 = grads + x[i].w2;
     qb.p[i].db1 = grads + x[i].b1;  // stage-1 bias gradient: column sums of dh1, fused
+  }
+  // dh1 rows are padded to ldh1 (a multiple of 8) and the qkv2 backward writes only the 3 H hh columns;
+  // the stage-1 dX GEMM reads K in 8-column chunks against zero weight-pack pad rows, so the pad must be
+  // finite: zeroed once per workspace (no kernel writes it). Garbage there made the gradient NaN at
+  // shapes with 3 H hh % 8 != 0 (hs 8 / 24 with odd head counts; round 6)
+  if (p.gh1_pad_ws != r.ws && ldh1 > 3 * H * c->hh) {
+    const size_t cols = 3 * (size_t)H * c->hh;
+    for (int k = 0; k < 2; ++k)
+      for (int i = 0; i < M; ++i)
+        r.ok(hipMemset2DAsync(r.W<bf16_t>(p.gh1[k][i]) + cols, (size_t)ldh1 * 2, 0, ((size_t)ldh1 - cols) * 2, (size_t)R, r.s),
+             "gh1 pad");
+    p.gh1_pad_ws = r.ws;
   }
   r.ok(mmt_launch_qkv2_bwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_bwd");
   for (int i = 0; i < M; ++i) {

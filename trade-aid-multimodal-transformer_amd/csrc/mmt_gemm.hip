@@ -870,6 +870,14 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(SlabBatch b) {
   }
 }
 
+// MMT_DW_SMALL=1: every weight gradient on the 128 x 128 tile (4x the tiles of the 256 x 256 one, so a
+// quarter of the K splits and of the split-K slab traffic at the ~128-block side-stream target)
+static const int g_dw_small = [] {
+  const char* e = getenv("MMT_DW_SMALL");
+  return e ? atoi(e) : 0;
+}();
+static bool use_big_dw(const GemmBatch& b) { return !g_dw_small && use_big(b); }
+
 hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_bytes, hipStream_t s) {
   if (b.count == 0) return hipSuccess;
   if (!gemm_span_ok(b)) return hipErrorInvalidValue;
@@ -877,7 +885,7 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
     const GemmProblem& P = b.p[g];
     if ((P.lda & 7) || (P.ldb & 7) || (((uintptr_t)P.A | (uintptr_t)P.B) & 15)) return hipErrorInvalidValue;
   }
-  const bool big = use_big(b);
+  const bool big = use_big_dw(b);
   int splits = big ? auto_splits<TileL>(b, 0) : auto_splits<TileS>(b, 0);
   int64_t per = 0;  // slab elements of one split over all problems (each slab 16-B aligned)
   for (int g = 0; g < b.count; ++g) per += ((int64_t)b.p[g].M * b.p[g].N + 3) / 4 * 4;
@@ -924,7 +932,7 @@ hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_b
 
 
 
-bool mmt_gemm_wgrad_big(const GemmBatch& b) { return use_big(b); }
+bool mmt_gemm_wgrad_big(const GemmBatch& b) { return use_big_dw(b); }
 
 bool mmt_gemm_resid_ln_ok(const GemmBatch& b) {
   if (b.count == 0) return false;
