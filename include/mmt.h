@@ -306,6 +306,10 @@ int mmt_set_relu_bits(int on);
 // env MMT_DROP_COPY_FUSE) = in the epilogue of the last cross-attention K/V data-gradient GEMM that
 // accumulates into that residual gradient, 0 = a separate pass; returns the previous value (tests, A/B)
 int mmt_set_drop_copy_fuse(int on);
+// hs 32 self-attention backward: 1 (default, env MMT_ATTN_QKV2) = the Q/K/V stage-2 backward (dh1 =
+// (dX W2) * tanh', dW2, db1) in the one-pass attention backward's epilogue, dQ / dK / dV never written;
+// 0 = the separate stage-2 backward over bf16 dQ / dK / dV. Read at every step; returns the previous value
+int mmt_set_attn_qkv2(int on);
 
 /* ---- MX-fp8 primitives (C4's fp8 path; BASELINE configs[4]) --------------------------------
  * MX-fp8 = OCP e4m3fn bytes + one E8M0 exponent byte (bias 127) per 32 consecutive K elements of a

@@ -187,3 +187,19 @@ def test_drop_copy_fuse_matches_separate_pass():
     (_, ls0, g0, _), (_, ls1, g1, _) = out[0], out[1]
     assert torch.equal(ls0, ls1)
     assert _rel(g1, g0) <= GRAD_BOUND, _rel(g1, g0)
+
+
+@pytest.mark.parametrize("name", ["f_c1", "f_hs32"])
+def test_attn_qkv2_fused_matches_separate(name):
+    """hs 32: the Q/K/V stage-2 backward in the one-pass attention backward's epilogue (default,
+    mmt_set_attn_qkv2(1): dQ / dK / dV never leave the kernel) against the separate stage-2 backward
+    over the bf16 dQ / dK / dV (0), dropout on: the same forward bitwise and the gradient within
+    GRAD_BOUND (both round dX to bf16 before the stage-2 products; the sums differ only in order)."""
+    fx = scale_fixture(name) if name == "f_c1" else model_fixture(name)
+    assert fx[1]["n_embd"] // fx[1]["n_head"] == 32
+    out, _, _ = _pair_with_knob("mmt_set_attn_qkv2", name, 0.1, sd_meta=fx)
+    (_, ls0, g0, _), (_, ls1, g1, _) = out[0], out[1]
+    assert torch.equal(ls0, ls1)
+    err = _rel(g1, g0)
+    print(f"{name}: fused stage-2 vs separate grad rel-L2 {err:.3e}")
+    assert err <= GRAD_BOUND, err

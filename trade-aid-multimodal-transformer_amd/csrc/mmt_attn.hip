@@ -1121,6 +1121,20 @@ __device__ __forceinline__ void a_wait_vm(int n) {
   }
 }
 constexpr int A_OOB = 0x7fffffff;
+// sum over the 32 lanes of each wave half: quad and row rotations by DPP, one cross-row shuffle
+__device__ __forceinline__ float a_dpp(float v, int ctl) {
+  return __builtin_bit_cast(float, ctl == 0xB1 ? __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true)
+                                  : ctl == 0x4E ? __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true)
+                                  : ctl == 0x124 ? __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xF, 0xF, true)
+                                                 : __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float a_sum32(float v) {
+  v += a_dpp(v, 0xB1);   // quad_perm [1, 0, 3, 2]
+  v += a_dpp(v, 0x4E);   // quad_perm [2, 3, 0, 1]
+  v += a_dpp(v, 0x124);  // row_ror 4
+  v += a_dpp(v, 0x128);  // row_ror 8
+  return v + __shfl_xor(v, 16, 64);
+}
 }  // namespace
 
 #ifndef MMT_F32_BRANCH
@@ -1129,11 +1143,17 @@ constexpr int A_OOB = 0x7fffffff;
 #ifndef MMT_F32_REV
 #define MMT_F32_REV 0
 #endif
+#ifndef MMT_F32_Q2_NOATOM
+#define MMT_F32_Q2_NOATOM 0  // timing experiment: the stage-2 dW2 sums not added (wrong gradient)
+#endif
 #ifndef MMT_F32_PAIR
 #define MMT_F32_PAIR 0  // 1: the two-tile body where both owned key tiles are active (register copies: slower)
 #endif
-template <bool DROP, bool MS>  // MS: several KV streams (cross-attention)
+// MS: several KV streams (cross-attention); Q2: the Q/K/V stage-2 backward fused into the epilogue
+// (AttnProblem::q2_*, self-attention only)
+template <bool DROP, bool MS, bool Q2>
 __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int T, int H, float scale) {
+  static_assert(!(MS && Q2), "the stage-2 backward follows the self-attention only");
   constexpr int IMG = 8 * SL_SLICE;               // 256 rows x 32 columns as slice images
   constexpr int OFF_DO = IMG, OFF_TAB = 2 * IMG;  // tables: -LSE2 [256], -D (-D / sc under dropout) [256]
   constexpr int OFF_DS = OFF_TAB + 2048;          // per-wave [32][32] bf16 transpose slots
@@ -1212,6 +1232,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
       dv4[c] = *reinterpret_cast<const u32x4*>(drow + 8 * c);
     }
   }
+  // Q2: W2^T of the head's K / Q / V stage-2 blocks as the A operand of dh1^T = W2^T dX^T (lane: i < 16,
+  // k: o = 16 s + 8 h + 0..7; rows i >= 16 zero)
+  // (one pinned base, unpredicated loads: lanes r >= 16 read row r - 16's words and drop them)
+  bf16x8 w2t[3][2];
+  const MMT_AS1 float* const w2p = Q2 ? sgpr_gptr(P.q2_w2) + head * 512 + (r & 15) + 8 * h * 16 : nullptr;
+#pragma unroll
+  for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float wv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        wv[e] = Q2 ? w2p[(kd * H * 32 + 16 * s + e) * 16] : 0.f;
+        wv[e] = r < 16 ? wv[e] : 0.f;
+      }
+      w2t[kd][s] = __builtin_bit_cast(bf16x8, u32x4{pack2bf(wv[0], wv[1]), pack2bf(wv[2], wv[3]), pack2bf(wv[4], wv[5]),
+                                                   pack2bf(wv[6], wv[7])});
+    }
   // pins: the compiler's waits for all of the above land here, ahead of the DMAs
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1229,6 +1267,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     asm volatile("" : "+v"(dv4[c]));
   }
   asm volatile("" : "+v"(lse_t));
+  if (Q2) {
+#pragma unroll
+    for (int kd = 0; kd < 3; ++kd) {
+      asm volatile("" : "+v"(w2t[kd][0]));
+      asm volatile("" : "+v"(w2t[kd][1]));
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // Q (waves 0, 2) and dO (waves 1, 3) images: wave w streams column half w >> 1 of every slice, in
   // slice order (nt pieces: the loop's counted waits); once, for the first stream
@@ -1525,7 +1570,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     }
     // this wave's piece of slice qt + 1: younger are the pieces of slices qt + 2 .. nt - 1 and the dQ
     // stores of steps 0 .. qt - 1, nt - 2 operations at every step
-    if (j == 0 && i + 1 < nt) a_wait_vm(nt - 2);
+    if (j == 0 && i + 1 < nt) a_wait_vm(Q2 ? nt - 2 - i : nt - 2);  // Q2: no dQ stores in the loop
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every partial of step qt is written; slice qt + 1 landed
     {
@@ -1534,7 +1579,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
       for (int u = 0; u < nw; ++u)
         a += *reinterpret_cast<const f32x4*>(lds + OFF_DQ + ((i & 1) * 4 + u) * 4096 + R * 128 + ((cq ^ (R & 7)) << 4));
       const int tq = qt * 32 + R;
-      if (!MS || j == ns - 1) {
+      if (Q2) {  // dQ rows into the (spent) Q slice of this step, for the stage-2 backward after the walk
+        *reinterpret_cast<u32x2*>(lds + qt * SL_SLICE + sl_off(R, cq >> 1) + (cq & 1) * 8) =
+            u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)};
+      } else if (!MS || j == ns - 1) {
         if (MS && j > 0 && tq < T) a += *reinterpret_cast<const f32x4*>(P.dq32 + (rowbase + tq) * P.dq32_ld + head * 32 + 4 * cq);
         a_bst8(rdq, tq < T ? (tq * P.dq_ld + 4 * cq) * 2 : A_OOB,
                u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)});
@@ -1545,11 +1593,142 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     }
   }
 
+  const float dks = DROP ? scale * P.drop_scale : scale;
+  const float dvs = DROP ? P.drop_scale : 1.f;
+  if constexpr (Q2) {
+    // Q/K/V stage-2 backward of this head (model.py:36-50) on the 32-row tiles of dQ (in the Q image),
+    // dK and dV (staged from the accumulators): per tile dh1^T = W2^T dX^T (2 MFMAs), times tanh' from
+    // the tile's h1 rows, stored; dW2^T += dX^T h1 (2 MFMAs) and the dh1 column sums (db1) in registers
+    // until the workgroup's sums go out by atomics. dQ / dK / dV never leave the kernel.
+    // the h1 rows of the six tiles (key / query tiles kts[t] x K, Q, V blocks) in flight at once: the
+    // tiles are worked one after the other, each wait only for its own rows
+    u32x4 h1v[2][3];
+    {
+      const MMT_AS1 bf16_t* const h1 = sgpr_gptr(P.q2_h1);
+      const int ld = __builtin_amdgcn_readfirstlane(P.q2_ld);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kd = 0; kd < 3; ++kd) {
+          const int row = kts[t] * 32 + r;
+          h1v[t][kd] = u32x4{0u, 0u, 0u, 0u};
+          if (kts[t] < nt && row < T)
+            h1v[t][kd] = *reinterpret_cast<const MMT_AS1 u32x4*>(h1 + (rowbase + row) * ld + (kd * H + head) * 16 + 8 * h);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's dQ rows of the last step are in the Q image
+    char* xs = lds + OFF_DQ + w * SL_SLICE;              // this wave's dX tile (slice image)
+    char* hs_ = lds + OFF_DQ + 4 * SL_SLICE + w * SL_SLICE;  // and its h1 tile (columns 16..31 zero)
+    f32x16 dwa[3];
+    float dba[3][8];
+#pragma unroll
+    for (int kd = 0; kd < 3; ++kd) {
+      zero16(dwa[kd]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dba[kd][e] = 0.f;
+    }
+    MMT_AS1 bf16_t* const dh1 = sgpr_gptr(P.q2_dh1);
+    const int ldd = __builtin_amdgcn_readfirstlane(P.q2_ld);
+    auto tile_op = [&](int kd, const char* ximg, int row0, const u32x4& hv) {
+      const int blk = kd * H + head;
+      const int row = row0 + r;
+      *reinterpret_cast<u32x4*>(hs_ + sl_off(r, h)) = hv;
+      *reinterpret_cast<u32x4*>(hs_ + sl_off(r, 2 + h)) = u32x4{0u, 0u, 0u, 0u};
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      f32x16 acc;
+      zero16(acc);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        acc = mfma32(w2t[kd][s], sl_row(reinterpret_cast<const bf16_t*>(ximg), 0, r, s, h), acc);  // dh1^T[i][r]
+      // lane (r, h): i = 4 h + e (e < 4) and 8 + 4 h + e - 4 (4 <= e < 8)
+      const u32x2 ha = *reinterpret_cast<const u32x2*>(hs_ + sl_off(r, 0) + 8 * h);
+      const u32x2 hb = *reinterpret_cast<const u32x2*>(hs_ + sl_off(r, 1) + 8 * h);
+      float hh8[8] = {bf2f(ha[0] & 0xffff), bf2f(ha[0] >> 16), bf2f(ha[1] & 0xffff), bf2f(ha[1] >> 16),
+                      bf2f(hb[0] & 0xffff), bf2f(hb[0] >> 16), bf2f(hb[1] & 0xffff), bf2f(hb[1] >> 16)};
+      float d[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        d[e] = acc[e] * (1.f - hh8[e] * hh8[e]);
+        dba[kd][e] += d[e];
+      }
+      if (row < T) {
+        MMT_AS1 bf16_t* dst = dh1 + (rowbase + row) * ldd + blk * 16 + 4 * h;
+        *reinterpret_cast<MMT_AS1 u32x2*>(dst) = u32x2{pack2bf(d[0], d[1]), pack2bf(d[2], d[3])};
+        *reinterpret_cast<MMT_AS1 u32x2*>(dst + 8) = u32x2{pack2bf(d[4], d[5]), pack2bf(d[6], d[7])};
+      }
+      // dW2^T[i][o] ... as C[m = o][n = i]: A = dX^T (lane o), B = h1 (lane i), k = rows (permuted)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        dwa[kd] = mfma32(sl_tr(reinterpret_cast<const bf16_t*>(ximg), 0, s, lane),
+                         sl_tr(reinterpret_cast<const bf16_t*>(hs_), 0, s, lane), dwa[kd]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's LDS reads before the next writes
+    };
+    // dK, dV of the wave's key tiles: accumulators (lane: column o = r, elements: rows) -> the tile image
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kt = kts[t];
+      if (kt >= nt) continue;
+#pragma unroll
+      for (int mtx = 0; mtx < 2; ++mtx) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+          *reinterpret_cast<bf16_t*>(xs + sl_off(kr, r >> 3) + (r & 7) * 2) = mtx ? f2bf(dv[t][e] * dvs) : f2bf(dk[t][e] * dks);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        tile_op(mtx ? 2 : 0, xs, kt * 32, h1v[t][mtx ? 2 : 0]);
+      }
+    }
+    // dQ tiles w and 7 - w from the Q image
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int qt = kts[t];
+      if (qt < nt) tile_op(1, lds + qt * SL_SLICE, qt * 32, h1v[t][1]);
+    }
+    MMT_AS1 float* const db1 = sgpr_gptr(P.q2_db1);
+    MMT_AS1 float* const dw2 = sgpr_gptr(P.q2_dw2);
+    // db1: column sums over the 32 rows of each lane half; lane r < 24 of each half adds sum r
+    {
+      float mine = 0.f;
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = a_sum32(dba[kd][e]);
+          mine = r == kd * 8 + e ? v : mine;
+        }
+      const int kd = r >> 3, e = r & 7;
+      if (r < 24)
+        __hip_atomic_fetch_add(db1 + (kd * H + head) * 16 + (e < 4 ? 4 * h + e : 8 + 4 * h + e - 4), mine, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // dW2: the four waves' partials summed through LDS, one atomic per element
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's tile images are spent
+    float* red = reinterpret_cast<float*>(lds + OFF_DQ);  // [4 waves][3 kinds][32 o][16 i]
+    if (r < 16) {
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          red[((w * 3 + kd) * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * 16 + r] = dwa[kd][e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int q = tid; q < 3 * 512; q += 256) {
+      const float v = (red[q] + red[1536 + q]) + (red[3072 + q] + red[4608 + q]);
+      const int kd = q / 512, oi = q % 512;
+#if !MMT_F32_Q2_NOATOM
+      __hip_atomic_fetch_add(dw2 + (kd * H + head) * 512 + oi, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+      if (v == 12345.f) dw2[0] = v;  // timing experiment only: keeps the sums live
+#endif
+    }
+  } else {
   // dK / dV of the wave's key tiles, transposed through LDS into row-major 16-B pieces (as the dK/dV
   // pass), one matrix at a time through the dQ partials of the parity the last step did not use (no
   // wave reads them after the last step's barrier; the next stream's first barrier retires these reads)
-  const float dks = DROP ? scale * P.drop_scale : scale;
-  const float dvs = DROP ? P.drop_scale : 1.f;
   bf16_t* et = reinterpret_cast<bf16_t*>(lds + OFF_DQ + (nt & 1) * 4 * 4096) + w * (32 * EPW);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1574,6 +1753,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
       }
     }
   }
+  }  // !Q2
   }  // streams
 }
 
@@ -1611,6 +1791,48 @@ static bool ring64_fits(const AttnBatch& bt, int T) {
   return true;
 }
 
+// the one-pass hs-32 backward (knob bit 6) takes the batch: T <= 256, Q / dO rows by LDS-DMA (16-B aligned
+// rows, sequences whose span fits a buffer descriptor); several KV streams only with knob bit 7 and the
+// fp32 dQ scratch. Every problem sets the Q/K/V stage-2 fields (AttnProblem::q2_*) or none does, and
+// only with one KV stream.
+static bool fused32_ok(const AttnBatch& bt, int T, int ns) {
+  if (!(g_attn_ring & 64) || T > 256 || bt.count < 1) return false;
+  const bool q2 = bt.p[0].q2_w2 != nullptr;
+  if (q2 && ns > 1) return false;
+  bool ok = true;
+  for (int g = 0; g < bt.count; ++g) {
+    const AttnProblem& P = bt.p[g];
+    ok = ok && !(P.q_ld & 7) && !(P.dout_ld & 7) && !((uintptr_t)P.q & 15) && !((uintptr_t)P.dout & 15) &&
+         !(P.kv_ld & 7) && !(P.kv_hstride & 7) && (int64_t)T * std::max(P.q_ld, P.dout_ld) * 2 < ((int64_t)1 << 31);
+    // several KV streams (knob bit 7, off by default): one workgroup walks the streams in turn, and at
+    // C1's cross-attention (3 streams, 512 workgroups: one generation) that measured slower than the
+    // two-pass pair, which spreads the dK/dV pass over 3x the workgroups (70.7 vs 67.9 us standalone,
+    // tools/attn_bench.py c1_ca)
+    if (ns > 1)
+      ok = ok && (g_attn_ring & 128) && P.dq32 && !(P.dq32_ld & 3) && !((uintptr_t)P.dq32 & 15) &&
+           (int64_t)T * P.dq32_ld * 4 < ((int64_t)1 << 31);
+    if ((P.q2_w2 != nullptr) != q2) return false;
+    if (q2)
+      ok = ok && P.q2_h1 && P.q2_dh1 && P.q2_dw2 && P.q2_db1 && !(P.q2_ld & 7) && !((uintptr_t)P.q2_h1 & 15) &&
+           !((uintptr_t)P.q2_dh1 & 7);
+  }
+  return ok;
+}
+
+bool mmt_attn_bwd_fuses_qkv2(const AttnBatch& bt, int T, int hs) {
+  if (hs != 32 || bt.count < 1) return false;
+  for (int g = 0; g < bt.count; ++g)
+    if (bt.p[g].nstreams != 1) return false;
+  AttnBatch t = bt;  // as the launch will see it with the stage-2 fields set
+  for (int g = 0; g < t.count; ++g) {
+    AttnProblem& P = t.p[g];
+    P.q2_w2 = reinterpret_cast<const float*>(16); P.q2_h1 = reinterpret_cast<const bf16_t*>(16);
+    P.q2_dh1 = reinterpret_cast<bf16_t*>(16); P.q2_dw2 = reinterpret_cast<float*>(16); P.q2_db1 = P.q2_dw2;
+    P.q2_ld = 8;
+  }
+  return fused32_ok(t, T, 1);
+}
+
 template <int HS>
 static hipError_t attn_launch(const AttnBatch& bt, int B, int T, int H, float scale, bool bwd, hipStream_t s) {
   const int nb = ((T + 31) / 32 + 7) / 8;
@@ -1626,38 +1848,30 @@ static hipError_t attn_launch(const AttnBatch& bt, int B, int T, int H, float sc
     const int ns = bt.p[0].nstreams;
     bool drop = false;
     for (int g = 0; g < bt.count; ++g) drop = drop || bt.p[g].drop_thr != 0;
+    // the stage-2 fields are a promise that the fused kernel writes dh1 / dW2 / db1 (and not dq / dk / dv):
+    // refused rather than dropped when it cannot run (mmt_attn_bwd_fuses_qkv2 decides beforehand)
+    for (int g = 0; g < bt.count; ++g)
+      if (bt.p[g].q2_w2 && (HS != 32 || !fused32_ok(bt, T, ns))) return hipErrorInvalidValue;
     // hs 64: the slice-streamed kernels (mmt_attn2.hip): bit 1 of the knob the dQ pass, bit 0 the
     // dK/dV pass; MMT_ATTN_RING=0 (or mmt_attn_set_ring(0)) keeps the chunked ones
     const bool ring = HS == 64 && ring64_fits(bt, T);
     // knob bit 5: dQ, dK, dV in one pass (mmt_attn2.hip) for T <= 512 and one KV stream
     if (ring && (g_attn_ring & 32) && T <= 512 && ns == 1) return mmt_attn_bwd_fused64(bt, B, T, H, scale, drop, s);
-    // knob bit 6: dQ, dK, dV in one pass at hs 32 for T <= 256 (Q / dO rows by LDS-DMA: 16-B aligned rows,
-    // and sequences whose span fits a buffer descriptor); several KV streams need the fp32 dQ scratch
-    if (HS == 32 && (g_attn_ring & 64) && T <= 256) {
-      bool ok = true;
-      for (int g = 0; g < bt.count; ++g) {
-        const AttnProblem& P = bt.p[g];
-        ok = ok && !(P.q_ld & 7) && !(P.dout_ld & 7) && !((uintptr_t)P.q & 15) && !((uintptr_t)P.dout & 15) &&
-             !(P.kv_ld & 7) && !(P.kv_hstride & 7) && (int64_t)T * std::max(P.q_ld, P.dout_ld) * 2 < ((int64_t)1 << 31);
-        // several KV streams (knob bit 7, off by default): one workgroup walks the streams in turn, and at
-        // C1's cross-attention (3 streams, 512 workgroups: one generation) that measured slower than the
-        // two-pass pair, which spreads the dK/dV pass over 3x the workgroups (70.7 vs 67.9 us standalone,
-        // tools/attn_bench.py c1_ca, profiles/r6_attn_bench.txt)
-        if (ns > 1)
-          ok = ok && (g_attn_ring & 128) && P.dq32 && !(P.dq32_ld & 3) && !((uintptr_t)P.dq32 & 15) &&
-               (int64_t)T * P.dq32_ld * 4 < ((int64_t)1 << 31);
+    // knob bit 6: dQ, dK, dV in one pass at hs 32 for T <= 256 (fused32_ok)
+    if (HS == 32 && fused32_ok(bt, T, ns)) {
+      const dim3 grid(B * H, 1, bt.count);
+      const bool q2 = bt.p[0].q2_w2 != nullptr;
+      if (ns > 1) {
+        if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true, true, false>), grid, dim3(256), 0, s, bt, T, H, scale);
+        else hipLaunchKernelGGL((attn_bwd_fused32<false, true, false>), grid, dim3(256), 0, s, bt, T, H, scale);
+      } else if (q2) {
+        if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true, false, true>), grid, dim3(256), 0, s, bt, T, H, scale);
+        else hipLaunchKernelGGL((attn_bwd_fused32<false, false, true>), grid, dim3(256), 0, s, bt, T, H, scale);
+      } else {
+        if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true, false, false>), grid, dim3(256), 0, s, bt, T, H, scale);
+        else hipLaunchKernelGGL((attn_bwd_fused32<false, false, false>), grid, dim3(256), 0, s, bt, T, H, scale);
       }
-      if (ok) {
-        const dim3 grid(B * H, 1, bt.count);
-        if (ns > 1) {
-          if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true, true>), grid, dim3(256), 0, s, bt, T, H, scale);
-          else hipLaunchKernelGGL((attn_bwd_fused32<false, true>), grid, dim3(256), 0, s, bt, T, H, scale);
-        } else {
-          if (drop) hipLaunchKernelGGL((attn_bwd_fused32<true, false>), grid, dim3(256), 0, s, bt, T, H, scale);
-          else hipLaunchKernelGGL((attn_bwd_fused32<false, false>), grid, dim3(256), 0, s, bt, T, H, scale);
-        }
-        return hipGetLastError();
-      }
+      return hipGetLastError();
     }
     if (ring && (g_attn_ring & 2)) {
       const hipError_t e = mmt_attn_bwd_dq_ring64(bt, B, T, H, scale, drop, s);

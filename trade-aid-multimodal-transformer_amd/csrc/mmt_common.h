@@ -93,6 +93,13 @@ __device__ __forceinline__ T* sgpr_ptr(T* p) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
+// the same, as a global-address-space pointer: sgpr_ptr's integer round trip loses the address space, and
+// the compiler then addresses through FLAT instructions (counted against lgkmcnt too, no SGPR base)
+#define MMT_AS1 __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ MMT_AS1 T* sgpr_gptr(T* p) {
+  return (MMT_AS1 T*)(uintptr_t)sgpr_ptr(p);
+}
 __device__ __forceinline__ uint32_t sgpr_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ float sgpr_f32(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 

@@ -134,6 +134,18 @@ extern "C" int mmt_set_drop_copy_fuse(int on) {
   return old;
 }
 
+// hs 32: the Q/K/V stage-2 backward in the one-pass attention backward's epilogue (1, default, env
+// MMT_ATTN_QKV2) or the separate qkv2 backward over the bf16 dQ / dK / dV (0); read at every step
+static int g_attn_qkv2 = [] {
+  const char* e = getenv("MMT_ATTN_QKV2");
+  return e ? atoi(e) : 1;
+}();
+extern "C" int mmt_set_attn_qkv2(int on) {
+  const int old = g_attn_qkv2;
+  g_attn_qkv2 = on;
+  return old;
+}
+
 struct mmt_ctx {
   mmt_config cfg;
   int M, C, H, L, T, hs, hh;
@@ -1705,7 +1717,15 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     r.set_drop(q, l, i, DS_SA_PROB);
     if (r.drop) q.dmask[0] = r.W<uint32_t>(a[i].dm);
   }
-  r.attn(ab, true, scale, "attn_bwd");
+  // hs 32: the Q/K/V stage-2 backward runs in the attention kernel's epilogue (dQ / dK / dV stay on chip:
+  // dh1, dW2, db1 leave it), so the separate qkv2 backward and its gqkv round trip go
+  const bool q2 = g_attn_qkv2 && mmt_attn_bwd_fuses_qkv2(ab, T, hs);
+  if (q2)
+    for (int i = 0; i < M; ++i) {
+      AttnProblem& q = ab.p[i];
+      q.q2_h1 = r.W<bf16_t>(a[i].h1); q.q2_dh1 = r.W<bf16_t>(p.gh1[par][i]); q.q2_ld = ldh1;
+      q.q2_w2 = r.P(x[i].w2); q.q2_dw2 = grads + x[i].w2; q.q2_db1 = grads + x[i].b1;
+    }
   Qkv2Batch qb{}; qb.count = M;
   for (int i = 0; i < M; ++i) {
     qb.p[i].h1 = r.W<bf16_t>(a[i].h1); qb.p[i].w2 = r.P(x[i].w2); qb.p[i].dout = r.W<bf16_t>(p.gqkv[i]);
@@ -1724,7 +1744,8 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
              "gh1 pad");
     p.gh1_pad_ws = r.ws;
   }
-  r.ok(mmt_launch_qkv2_bwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_bwd");
+  r.attn(ab, true, scale, "attn_bwd");
+  if (!q2) r.ok(mmt_launch_qkv2_bwd(qb, R, 3 * H, hs, ldh1, 3 * C, r.s), "qkv2_bwd");
   for (int i = 0; i < M; ++i) {
     const bf16_t* g = r.W<bf16_t>(p.gh1[par][i]);
     dw.p[i] = gp_dw(g, ldh1, r.W<bf16_t>(a[i].a), C, grads, x[i].W1, R);

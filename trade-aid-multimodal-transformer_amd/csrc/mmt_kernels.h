@@ -211,6 +211,14 @@ struct AttnProblem {
   // optional fp32 scratch rows [B*T][>= H*hs] (dq32_ld % 4 == 0, 16-B aligned): the one-pass hs-32
   // backward sums dQ over several KV streams there (required for it when nstreams > 1)
   float* dq32; int dq32_ld;
+  // optional (one KV stream, hs 32, the one-pass backward; set only when mmt_attn_bwd_fuses_qkv2 says so):
+  // the per-head Q/K/V stage-2 backward (Qkv2Problem, model.py:36-50) fused into the attention backward's
+  // epilogue, so dQ / dK / dV never leave the kernel: for kind k in {K, Q, V} (column blocks 0, C, 2C of
+  // the interleaved layout) and blk = k * H + head, dh1[r][blk*16 + i] = (sum_o W2[blk][o][i] dX[r][o]) *
+  // (1 - h1[r][blk*16 + i]^2), dW2[blk] += dX^T h1, db1[blk*16 + i] += sum_r dh1 (atomic). dq / dk / dv
+  // are then not written.
+  const bf16_t* q2_h1; bf16_t* q2_dh1; int q2_ld;
+  const float* q2_w2; float* q2_dw2; float* q2_db1;
   bf16_t* dk[MMT_MAX_STREAMS];
   bf16_t* dv[MMT_MAX_STREAMS];
   int dkv_ld, dkv_hstride;
@@ -237,6 +245,9 @@ inline int64_t mmt_attn_mask_dwords(int B, int H, int T) { return 2 * 32 * mmt_a
 struct AttnBatch { AttnProblem p[MMT_MAX_GROUP]; int count; };
 hipError_t mmt_launch_attn_fwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
 hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, float scale, hipStream_t s);
+// true when mmt_launch_attn_bwd runs this batch on the one-pass hs-32 kernel with one KV stream, which
+// can take the Q/K/V stage-2 backward in its epilogue (AttnProblem::q2_*)
+bool mmt_attn_bwd_fuses_qkv2(const AttnBatch& b, int T, int hs);
 // hs 64 dK/dV pass streaming the query slices through an LDS-DMA ring (mmt_attn2.hip)
 // variant (the mmt_attn_set_ring bits): 4 = 3 waves per SIMD (default), else 2
 hipError_t mmt_attn_bwd_dkdv_ring64(const AttnBatch& b, int B, int T, int H, float scale, bool drop, int variant,
