@@ -66,8 +66,9 @@ def train_flops_per_row(M, C, H, L, T, V, cross, a=0.5):
 PROBES = ["*_dw", "attn_fwd", "attn_bwd", "ffn0", "ffn2_dx", "*_dx"]  # engine launch labels timed live (first match)
 PROBE_NAMES = {"*_dw": "weight-gradient GEMMs (all *_dw launches: split-K 256x256 / 128x128 gemm_kernel)",
                "attn_fwd": "attn_fwd_kernel (causal self-attention forward)",
-               "attn_bwd": "self-attention backward: dQ pass + dK/dV pass (attn_bwd_dq_kernel + attn_bwd_dkdv1_kernel; "
-                           "hs 64: attn_bwd_dkdv_ring64, the slice-streamed dK/dV pass)",
+               "attn_bwd": "self-attention backward (hs 32, T <= 256: attn_bwd_fused32, dQ / dK / dV in one pass with "
+                           "the Q/K/V stage-2 backward in its epilogue; otherwise a dQ pass + a dK/dV pass: "
+                           "attn_bwd_dq_kernel + attn_bwd_dkdv1_kernel, hs 64 on the slice rings)",
                "ffn0": "gemm_kernel ffn0 (X W0^T + b, ReLU, bf16 out)",
                "ffn2_dx": "gemm_kernel ffn2 data gradient (dY W2, ReLU' epilogue, bias-grad column sums)",
                "*_dx": "the other backward-data GEMMs (incl. the LayerNorm-backward fused ones: ffn0 / qkv1 / "

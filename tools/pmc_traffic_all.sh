@@ -17,6 +17,10 @@ for c in c1 target c3 c4; do
   esac
   args=("$FF" "*_dw=false, false, true,+slab_reduce" "attn_fwd=attn_fwd@0/2" "ca_attn_fwd=attn_fwd@1/2"
         "attn_bwd=attn_bwd_dq+attn_bwd_dkdv@1/2" "ca_attn_bwd=attn_bwd_dq+attn_bwd_dkdv@0/2" "$DX")
+  # round 6: at hs 32 (C1) the self-attention backward is one kernel (attn_bwd_fused32, Q/K/V stage 2 in
+  # its epilogue); the cross-attention keeps the two passes
+  [ $c = c1 ] && args=("$FF" "*_dw=false, false, true,+slab_reduce" "attn_fwd=attn_fwd@0/2" "ca_attn_fwd=attn_fwd@1/2"
+        "attn_bwd=attn_bwd_fused32" "ca_attn_bwd=attn_bwd_dq+attn_bwd_dkdv" "$DX")
   [ -n "$LN" ] && args+=("$LN")
   python3 tools/pmc_traffic.py $c $F $W "${args[@]}" || exit 1
 done

@@ -634,6 +634,14 @@ void attn_cost(const AttnBatch& ab, int B, int T, int H, int hs, bool bwd, bool 
     double x = rows * C * 2.0 * (2.0 + 2.0 * ns) + ns * (bhT * 4.0 + mask);  // q, o, k_j, v_j, lse_j, bits
     if (ns > 1) x += ns * rows * C * 2.0;                                      // per-stream outputs o_j
     if (bwd) x += rows * C * 2.0 * (2.0 + 2.0 * ns) + ns * bhT * 4.0;         // dO, dQ, dK_j, dV_j, dvec_j
+    if (bwd && ab.p[g].q2_w2) {
+      // the stage-2 backward in the epilogue: dQ / dK / dV not written; h1 read, dh1 written (3 H x hs/2
+      // columns each), W2 read and dW2 written (algorithmic: once; the kernel adds per workgroup through L2);
+      // flops: dh1 = dX W2 and dW2 = dX^T h1
+      const double hh = hs / 2;
+      x += -rows * C * 2.0 * 3.0 + 2.0 * rows * 3.0 * H * hh * 2.0 + 3.0 * H * hs * hh * 4.0 * 2.0;
+      *fl += 2.0 * 2.0 * rows * 3.0 * C * hh;
+    }
     *by += x;
   }
 }

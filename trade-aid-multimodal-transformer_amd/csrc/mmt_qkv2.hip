@@ -299,8 +299,11 @@ __device__ __forceinline__ int q2_swz(int row, int chunk) { return row * 64 + ((
 // instruction touches 64 / CPR rows instead of 32 row pieces; the tile goes through the wave's LDS
 // images (which the dW2 product reads anyway) and the MFMA fragments are read back from there. At
 // hs 64 the dh1 tile is restaged the same way before its store.
+#ifndef MMT_QKV2B_OCC
+#define MMT_QKV2B_OCC 2
+#endif
 template <int HS, bool COAL>
-__global__ __launch_bounds__(256) void qkv2_bwd_v2(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
+__global__ __launch_bounds__(256, MMT_QKV2B_OCC) void qkv2_bwd_v2(Qkv2Batch batch, int R, int ld_h1, int ld_out) {
   constexpr int HH = HS / 2;
   constexpr int NOT = HS / 32;  // 32-column output tiles of dout (o)
   constexpr int KSO = HS / 16;  // k-steps over o for dh1
