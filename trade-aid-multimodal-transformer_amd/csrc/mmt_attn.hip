@@ -1151,9 +1151,22 @@ __device__ __forceinline__ float a_sum32(float v) {
 #endif
 // MS: several KV streams (cross-attention); Q2: the Q/K/V stage-2 backward fused into the epilogue
 // (AttnProblem::q2_*, self-attention only)
+#ifndef MMT_F32_NB
+// 1: one KV stream walked without per-step barriers, dQ summed by LDS float atomics (ds_add_f32). Measured
+// (tools/attn_bench.py c1, profiles/r6pq_fused32_nb.txt): 93 -> 309 us with the atomics, 80 us with plain
+// stores in their place (wrong sums: the walk itself would gain 14 %); the LDS float atomics cost the
+// difference, so the per-step partials and barrier stay
+#define MMT_F32_NB 0
+#endif
 template <bool DROP, bool MS, bool Q2>
 __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int T, int H, float scale) {
   static_assert(!(MS && Q2), "the stage-2 backward follows the self-attention only");
+  // NB (off: see MMT_F32_NB): every wave walks its own (query tile, key tile) products without waiting for the others: the
+  // Q / dO images are complete before the walk, and the dQ contributions go into per-tile fp32 sums
+  // in LDS ([8 tiles][32 d][32 q], ds_add_f32) instead of per-step partials reduced behind a barrier.
+  // The per-step barrier held every wave to the step's slowest (2 tiles against 0-1 elsewhere: 12
+  // tile times per walk where each wave owns 9)
+  constexpr bool NB = !MS && MMT_F32_NB;
   constexpr int IMG = 8 * SL_SLICE;               // 256 rows x 32 columns as slice images
   constexpr int OFF_DO = IMG, OFF_TAB = 2 * IMG;  // tables: -LSE2 [256], -D (-D / sc under dropout) [256]
   constexpr int OFF_DS = OFF_TAB + 2048;          // per-wave [32][32] bf16 transpose slots
@@ -1328,7 +1341,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     for (int s = 0; s < 2; ++s) ktf[t][s] = join4(lds_tr16(slot + o_da0 + 1024 * s), lds_tr16(slot + o_da1 + 1024 * s));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  if (j == 0) a_wait_vm(nt - 1);  // this wave's piece of slice 0 (the younger nt - 1 pieces stay in flight)
+  if (NB) {  // the whole Q / dO images before the walk; the dQ sums start at zero
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<f32x4*>(lds + OFF_DQ + k * 4096 + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (j == 0) a_wait_vm(nt - 1);  // this wave's piece of slice 0 (the younger nt - 1 pieces stay in flight)
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous stream's dQ-sum stores are done
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // everyone's slice-0 pieces and table entries (later streams: and every
@@ -1523,6 +1540,62 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
 #ifndef MMT_F32_SKIP
 #define MMT_F32_SKIP 0
 #endif
+  if constexpr (NB) {
+#pragma unroll 1
+    for (int i = 0; i < nt; ++i) {
+      const int qt = i;
+      const uint32_t cA = mwq[0][0] >> (4 * h), cB = mwq[1][0] >> (4 * h);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 7; ++q) mwq[t][q] = mwq[t][q + 1];
+      if (kts[0] > qt) continue;  // wave-uniform: no owned key tile at or below query tile qt yet
+      f32x16 dqp;
+      zero16(dqp);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int kt = kts[t];
+        if (kt < nt && kt <= qt) tile(std::false_type{}, qt, t, t ? cB : cA, m_diag, dqp, kt == qt);
+      }
+      // dQ^T[d][q] of the tile: element e is d = (e & 3) + 8 (e >> 2) + 4 h, lane r is q; 32 lanes a bank row
+      float* acc = reinterpret_cast<float*>(lds + OFF_DQ + qt * 4096) + 4 * h * 32 + r;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+#ifdef MMT_F32_NB_NOATOM  // timing experiment: plain stores (wrong sums)
+        acc[((e & 3) + 8 * (e >> 2)) * 32] = dqp[e];
+#else
+        __hip_atomic_fetch_add(acc + ((e & 3) + 8 * (e >> 2)) * 32, dqp[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every dQ contribution is in
+    // the wave's two query tiles (the rows of its key tiles): lane (r, h) row r, columns 16 h .. 16 h + 15,
+    // scaled to bf16 into the spent Q image (Q2: the stage-2 operand) or stored
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int qt = kts[t];
+      if (qt >= nt) continue;
+      const float* acc = reinterpret_cast<const float*>(lds + OFF_DQ + qt * 4096) + 16 * h * 32 + r;
+      uint32_t pk[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pk[k] = pack2bf(acc[(2 * k) * 32] * dqs, acc[(2 * k + 1) * 32] * dqs);
+      if (Q2) {
+        *reinterpret_cast<u32x4*>(lds + qt * SL_SLICE + sl_off(r, 2 * h)) = u32x4{pk[0], pk[1], pk[2], pk[3]};
+        *reinterpret_cast<u32x4*>(lds + qt * SL_SLICE + sl_off(r, 2 * h + 1)) = u32x4{pk[4], pk[5], pk[6], pk[7]};
+      } else {
+        const int tq = qt * 32 + r;
+        if (tq < T) {
+          u32x2* d = reinterpret_cast<u32x2*>(P.dq + (rowbase + tq) * P.dq_ld + head * 32 + 16 * h);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[k] = u32x2{pk[2 * k], pk[2 * k + 1]};
+        }
+      }
+    }
+    // the dQ sums are spent before the epilogue transposes / stage-2 images reuse their LDS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else
 #pragma unroll 1
   for (int i = 0; i < (MMT_F32_SKIP ? 0 : nt); ++i) {
     const int qt = step_qt(i);
@@ -1811,6 +1884,8 @@ static bool fused32_ok(const AttnBatch& bt, int T, int ns) {
     if (ns > 1)
       ok = ok && (g_attn_ring & 128) && P.dq32 && !(P.dq32_ld & 3) && !((uintptr_t)P.dq32 & 15) &&
            (int64_t)T * P.dq32_ld * 4 < ((int64_t)1 << 31);
+    // one stream without the stage-2 fields: dQ rows leave as 8-B pieces
+    if (ns == 1 && !q2) ok = ok && !(P.dq_ld & 3) && !((uintptr_t)P.dq & 7);
     if ((P.q2_w2 != nullptr) != q2) return false;
     if (q2)
       ok = ok && P.q2_h1 && P.q2_dh1 && P.q2_dw2 && P.q2_db1 && !(P.q2_ld & 7) && !((uintptr_t)P.q2_h1 & 15) &&
