@@ -310,6 +310,10 @@ int mmt_set_drop_copy_fuse(int on);
 // (dX W2) * tanh', dW2, db1) in the one-pass attention backward's epilogue, dQ / dK / dV never written;
 // 0 = the separate stage-2 backward over bf16 dQ / dK / dV. Read at every step; returns the previous value
 int mmt_set_attn_qkv2(int on);
+// rows per workgroup of the fused out-projection MLP forward at C = 256 (mmt_op_mlp2 and the engine's):
+// 128 (8 waves, one workgroup per CU) or 64 (4 waves, three per CU); default 128 (env MMT_MLP2_BM);
+// returns the previous value (tests, A/B)
+int mmt_mlp2_set_bm(int bm);
 
 /* ---- MX-fp8 primitives (C4's fp8 path; BASELINE configs[4]) --------------------------------
  * MX-fp8 = OCP e4m3fn bytes + one E8M0 exponent byte (bias 127) per 32 consecutive K elements of a

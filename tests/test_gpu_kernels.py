@@ -397,14 +397,25 @@ def test_gemm_ln_bwd_fused(M, N, K, drop):
                                 1.0) == -2  # MMT_ERR_UNSUPPORTED
 
 
+@pytest.mark.parametrize("bm", [128, 64])
 @pytest.mark.parametrize("M,C,drop,lnf", [(1000, 256, 0.0, False), (300, 256, 0.1, True), (4096, 512, 0.1, False),
-                                          (130, 512, 0.0, True), (65536, 512, 0.1, False), (65536, 256, 0.0, True)])
-def test_mlp2_fused(M, C, drop, lnf):
+                                          (130, 512, 0.0, True), (65536, 512, 0.1, False), (65536, 256, 0.0, True),
+                                          (97, 256, 0.1, False)])
+def test_mlp2_fused(M, C, drop, lnf, bm):
     """The attention out-projection as one launch (mmt_op_mlp2: Linear(C, C/2) -> tanh -> Linear(C/2, C) ->
     hash dropout -> + residual, h kept in LDS; reference model.py:82-92) against torch on the same bf16
     operands: h (stored for the backward) within one bf16 rounding of the torch tanh, the fp32 output
     rel 1e-3 (h enters the second product as bf16 in both), the optional next LayerNorm on the owned
-    rows; the full-chip cases keep every CU busy with both ring protocols."""
+    rows; the full-chip cases keep every CU busy with both ring protocols. bm: rows per workgroup
+    (mmt_mlp2_set_bm; 64 = the 4-wave form, C = 256 only: C = 512 keeps 128)."""
+    old_bm = ML.lib().mmt_mlp2_set_bm(bm)
+    try:
+        _mlp2_fused_case(M, C, drop, lnf)
+    finally:
+        ML.lib().mmt_mlp2_set_bm(old_bm)
+
+
+def _mlp2_fused_case(M, C, drop, lnf):
     import mmt_oracle as O
     torch.manual_seed(M + C)
     N1 = C // 2

@@ -83,7 +83,7 @@ __device__ __forceinline__ void issue_tile(const i32x4& rsrc, char* img, int ld,
   constexpr int PPW = ROWS * BK / 512 / NW;  // pieces per wave
   constexpr int CPR = BK / 8;                // chunks per K-contiguous row
   constexpr int CPK = ROWS / 8;              // chunks per k-row of an MN-contiguous image
-  static_assert(PPW >= 1 && CPK >= 16, "tile geometry");
+  static_assert(PPW >= 1 && (KC || CPK >= 16), "tile geometry");
 #pragma unroll
   for (int u = 0; u < PPW; ++u) {
     const int i = wave * PPW + u;

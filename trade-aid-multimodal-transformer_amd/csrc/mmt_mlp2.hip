@@ -24,12 +24,14 @@ constexpr int MLP_BM = 128;
 constexpr int MLP_BK = 32;
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-template <int N1>
+// BM_: rows per workgroup, 128 (8 waves) or 64 (4 waves: the forward's small-C form, see mmt_launch_mlp2)
+template <int N1, int BM_ = MLP_BM>
 struct MlpCfg {
+  static constexpr int BM = BM_, NW = BM_ / 16;
   static constexpr int N2 = 2 * N1, K1 = N2;
-  using T1 = TileCfg<2, 4, 2, N1 / 128>;  // stage 1: 128 x N1, waves 2 (m) x 4 (n), 64 x N1/4 each
-  using T2 = TileCfg<2, 4, 2, N2 / 128>;  // stage 2: 128 x N2, 64 x N2/4 each
-  static constexpr int S1_STAGE = (MLP_BM + N1) * MLP_BK * 2;  // x + W0 images per K-step
+  using T1 = TileCfg<BM_ / 64, 4, 2, N1 / 128>;  // stage 1: BM x N1, waves BM/64 (m) x 4 (n), 64 x N1/4 each
+  using T2 = TileCfg<BM_ / 64, 4, 2, N2 / 128>;  // stage 2: BM x N2, 64 x N2/4 each
+  static constexpr int S1_STAGE = (BM_ + N1) * MLP_BK * 2;  // x + W0 images per K-step
   static constexpr int S1_ST = 3;
   static constexpr int S2_STAGE = N2 * MLP_BK * 2;              // W2 image per K-step
   static constexpr int S2_ST = 2;
@@ -40,7 +42,7 @@ struct MlpCfg {
   static constexpr int CTILE = EPI_ROWS * (N2 + 4) * 4;
   static constexpr int RING = cmax(cmax(S1_ST * S1_STAGE, S2_ST * S2_STAGE), CTILE);
   static constexpr int HPITCH = N1 * 2;  // h image row pitch (bytes)
-  static constexpr int HBYTES = MLP_BM * HPITCH;
+  static constexpr int HBYTES = BM_ * HPITCH;
   static constexpr int LDS = RING + HBYTES;
 };
 
@@ -52,16 +54,17 @@ __device__ __forceinline__ int h_off(int m, int chunk) {
 
 }  // namespace
 
-template <int N1>
-__global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
-  using CF = MlpCfg<N1>;
+template <int N1, int BM>
+__global__ __launch_bounds__(BM * 4, 1) void mlp2_kernel(Mlp2Batch batch) {
+  using CF = MlpCfg<N1, BM>;
+  constexpr int NW = CF::NW;
   using T1 = typename CF::T1;
   using T2 = typename CF::T2;
   constexpr int N2 = CF::N2, BK = MLP_BK;
   constexpr int TN1 = T1::TN, TN2 = T2::TN, TM = 2;  // 32 x 32 sub-tiles per wave
-  constexpr int IMG_X = MLP_BM * BK * 2, IMG_W0 = N1 * BK * 2;
-  constexpr int PIECES1 = (MLP_BM + N1) * BK / 512 / 8;  // LDS-DMA pieces per wave per stage-1 K-step
-  constexpr int PIECES2 = N2 * BK / 512 / 8;             // per stage-2 K-step
+  constexpr int IMG_X = BM * BK * 2, IMG_W0 = N1 * BK * 2;
+  constexpr int PIECES1 = (BM + N1) * BK / 512 / NW;  // LDS-DMA pieces per wave per stage-1 K-step
+  constexpr int PIECES2 = N2 * BK / 512 / NW;            // per stage-2 K-step
   __shared__ __attribute__((aligned(1024))) char lds[CF::LDS];
   char* himg = lds + CF::RING;
 
@@ -69,10 +72,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
   const GemmProblem& P1 = batch.g1[prob];
   const GemmProblem& P2 = batch.g2[prob];
   const int M = __builtin_amdgcn_readfirstlane(P1.M);
-  const int ntiles = (M + MLP_BM - 1) / MLP_BM;
+  const int ntiles = (M + BM - 1) / BM;
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   if (tile >= ntiles) return;
-  const int m0 = tile * MLP_BM;
+  const int m0 = tile * BM;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / 4, wn = wave % 4;
@@ -95,8 +98,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
     constexpr int ST = CF::S1_ST;
     auto issue = [&](int slot, int t) {
       char* st = lds + slot * CF::S1_STAGE;
-      issue_tile<BK, true, MLP_BM, 8>(ra, st, lda, M, K, m0, t * BK, wave, lane);
-      issue_tile<BK, true, N1, 8>(rb, st + IMG_X, ldb, N1, K, 0, t * BK, wave, lane);
+      issue_tile<BK, true, BM, NW>(ra, st, lda, M, K, m0, t * BK, wave, lane);
+      issue_tile<BK, true, N1, NW>(rb, st + IMG_X, ldb, N1, K, 0, t * BK, wave, lane);
     };
 #pragma unroll
     for (int t = 0; t < ST - 1; ++t) issue(t, t);
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
       for (int s = 0; s < BK / 16; ++s) {
         bf16x8 fa[TM], fb[TN1];
 #pragma unroll
-        for (int j = 0; j < TM; ++j) fa[j] = frag<BK, true, MLP_BM>(imgA, wm * 64 + 32 * j, s, lane);
+        for (int j = 0; j < TM; ++j) fa[j] = frag<BK, true, BM>(imgA, wm * 64 + 32 * j, s, lane);
 #pragma unroll
         for (int i = 0; i < TN1; ++i) fb[i] = frag<BK, true, N1>(imgB, wn * TN1 * 32 + 32 * i, s, lane);
 #pragma unroll
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
   const int ldw2 = __builtin_amdgcn_readfirstlane(P2.ldb);
   const i32x4 rw2 = op_rsrc<true>(P2.B, ldw2, N2, K2, 0, 0);
   auto issue2 = [&](int slot, int t) {
-    issue_tile<BK, true, N2, 8>(rw2, lds + slot * CF::S2_STAGE, ldw2, N2, K2, 0, t * BK, wave, lane);
+    issue_tile<BK, true, N2, NW>(rw2, lds + slot * CF::S2_STAGE, ldw2, N2, K2, 0, t * BK, wave, lane);
   };
   constexpr int S2F = CF::S2F_ST;
   // with the 3-slot ring the stage-1 bias is loaded before the W2 slices: loads issued after them would
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_kernel(Mlp2Batch batch) {
     bf16_t* ho = P1.o16;
     const int ldo = P1.ldo16;
 #pragma unroll
-    for (int q = tid; q < MLP_BM * CPR; q += 512) {
+    for (int q = tid; q < BM * CPR; q += 64 * NW) {
       const int m = q / CPR, c = q % CPR;
       if (m0 + m < M)
         *reinterpret_cast<u32x4*>(ho + (int64_t)(m0 + m) * ldo + 8 * c) =
@@ -528,11 +531,29 @@ bool mmt_mlp2_ok(const Mlp2Batch& b) {
   return true;
 }
 
+// rows per forward workgroup at C = 256 (N1 128): 128 (8 waves, 80 KiB LDS, 163 VGPRs: one workgroup per
+// CU) or 64 (4 waves, 52 KiB: three per CU, so one's epilogue stores overlap the others' MFMAs);
+// MMT_MLP2_BM, or mmt_mlp2_set_bm() for in-process A/B
+static int g_mlp2_bm = [] {
+  const char* e = getenv("MMT_MLP2_BM");
+  return e ? atoi(e) : 128;
+}();
+extern "C" int mmt_mlp2_set_bm(int bm) {
+  const int old = g_mlp2_bm;
+  g_mlp2_bm = bm;
+  return old;
+}
+
 hipError_t mmt_launch_mlp2(const Mlp2Batch& b, hipStream_t s) {
   if (!mmt_mlp2_ok(b)) return hipErrorInvalidValue;
+  const int bm = (b.g1[0].N == 128 && g_mlp2_bm == 64) ? 64 : 128;
   int mt = 0;
-  for (int g = 0; g < b.count; ++g) mt = std::max(mt, (b.g1[g].M + MLP_BM - 1) / MLP_BM);
-  if (b.g1[0].N == 128) hipLaunchKernelGGL(mlp2_kernel<128>, dim3(mt, 1, b.count), dim3(512), 0, s, b);
-  else hipLaunchKernelGGL(mlp2_kernel<256>, dim3(mt, 1, b.count), dim3(512), 0, s, b);
+  for (int g = 0; g < b.count; ++g) mt = std::max(mt, (b.g1[g].M + bm - 1) / bm);
+  if (b.g1[0].N == 128) {
+    if (bm == 64) hipLaunchKernelGGL((mlp2_kernel<128, 64>), dim3(mt, 1, b.count), dim3(256), 0, s, b);
+    else hipLaunchKernelGGL((mlp2_kernel<128, 128>), dim3(mt, 1, b.count), dim3(512), 0, s, b);
+  } else {
+    hipLaunchKernelGGL((mlp2_kernel<256, 128>), dim3(mt, 1, b.count), dim3(512), 0, s, b);
+  }
   return hipGetLastError();
 }

@@ -89,6 +89,7 @@ _SIGS = {
     "mmt_set_relu_bits": (c_i32, [ctypes.c_int]),
     "mmt_set_drop_copy_fuse": (c_i32, [ctypes.c_int]),
     "mmt_set_attn_qkv2": (c_i32, [ctypes.c_int]),
+    "mmt_mlp2_set_bm": (c_i32, [ctypes.c_int]),
     "mmt_qkv2_set_coal": (c_i32, [ctypes.c_int]),
     "mmt_gemm_set_variant": (c_i32, [ctypes.c_int]),
     "mmt_op_gemm": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp,
