@@ -1155,7 +1155,9 @@ __device__ __forceinline__ float a_sum32(float v) {
 // 1: one KV stream walked without per-step barriers, dQ summed by LDS float atomics (ds_add_f32). Measured
 // (tools/attn_bench.py c1, profiles/r6pq_fused32_nb.txt): 93 -> 309 us with the atomics, 80 us with plain
 // stores in their place (wrong sums: the walk itself would gain 14 %); the LDS float atomics cost the
-// difference, so the per-step partials and barrier stay
+// difference. 2: the free walk with per-step partials summed by each query tile's last contributor
+// (correct; 93.9 -> 111.8 us: the one-wave sum sits on the critical path). The per-step partials and
+// barrier stay
 #define MMT_F32_NB 0
 #endif
 template <bool DROP, bool MS, bool Q2>
@@ -1166,12 +1168,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
   // in LDS ([8 tiles][32 d][32 q], ds_add_f32) instead of per-step partials reduced behind a barrier.
   // The per-step barrier held every wave to the step's slowest (2 tiles against 0-1 elsewhere: 12
   // tile times per walk where each wave owns 9)
-  constexpr bool NB = !MS && MMT_F32_NB;
+  constexpr bool NB = !MS && MMT_F32_NB == 1;
+  // NB2 (MMT_F32_NB=2): the same free walk with the per-step partials kept (two slots per wave, tile qt in
+  // slot (qt - w) & 1) and summed by the LAST contributor of each query tile (an LDS arrival counter per
+  // tile); a wave reuses a slot only after the tile that held it was summed (a done flag per tile)
+  constexpr bool NB2 = !MS && MMT_F32_NB == 2;
   constexpr int IMG = 8 * SL_SLICE;               // 256 rows x 32 columns as slice images
   constexpr int OFF_DO = IMG, OFF_TAB = 2 * IMG;  // tables: -LSE2 [256], -D (-D / sc under dropout) [256]
   constexpr int OFF_DS = OFF_TAB + 2048;          // per-wave [32][32] bf16 transpose slots
   constexpr int OFF_DQ = OFF_DS + 4 * 2048;       // dQ partials [2 steps][4 waves][32 q][32 d] fp32
-  constexpr int BYTES = OFF_DQ + 8 * 4096;
+  constexpr int OFF_SYNC = OFF_DQ + 8 * 4096;     // NB2: arrival counters [8], done flags [8]
+  constexpr int BYTES = OFF_SYNC + (MMT_F32_NB == 2 ? 64 : 0);
   static_assert(2 * BYTES <= 160 * 1024, "two workgroups per CU");
   constexpr int EPW = 40;                          // epilogue transpose row stride (bf16)
   static_assert(4 * 32 * EPW * 2 <= 4 * 4096, "epilogue transposes alias one parity of the dQ partials");
@@ -1341,9 +1348,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     for (int s = 0; s < 2; ++s) ktf[t][s] = join4(lds_tr16(slot + o_da0 + 1024 * s), lds_tr16(slot + o_da1 + 1024 * s));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  if (NB) {  // the whole Q / dO images before the walk; the dQ sums start at zero
+  if (NB || NB2) {  // the whole Q / dO images before the walk; the dQ sums / the sync words start at zero
+    if (NB) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) *reinterpret_cast<f32x4*>(lds + OFF_DQ + k * 4096 + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < 8; ++k) *reinterpret_cast<f32x4*>(lds + OFF_DQ + k * 4096 + tid * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (NB2 && tid < 16) reinterpret_cast<int*>(lds + OFF_SYNC)[tid] = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else if (j == 0) a_wait_vm(nt - 1);  // this wave's piece of slice 0 (the younger nt - 1 pieces stay in flight)
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous stream's dQ-sum stores are done
@@ -1595,6 +1605,64 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fused32(AttnBatch batch, int 
     // the dQ sums are spent before the epilogue transposes / stage-2 images reuse their LDS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  } else if constexpr (NB2) {
+    int* const cnt = reinterpret_cast<int*>(lds + OFF_SYNC);
+    int* const done = cnt + 8;
+#pragma unroll 1
+    for (int i = 0; i < nt; ++i) {
+      const int qt = i;
+      const uint32_t cA = mwq[0][0] >> (4 * h), cB = mwq[1][0] >> (4 * h);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 7; ++q) mwq[t][q] = mwq[t][q + 1];
+      if (kts[0] > qt) continue;  // wave-uniform: not a contributor of query tile qt
+      f32x16 dqp;
+      zero16(dqp);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int kt = kts[t];
+        if (kt < nt && kt <= qt) tile(std::false_type{}, qt, t, t ? cB : cA, m_diag, dqp, kt == qt);
+      }
+      // the slot last held tile qt - 2: wait until its sum has read it (bounded: a lost flag cannot hang)
+      if (qt - 2 >= w) {
+        for (int it = 0; it < (1 << 22); ++it) {
+          if (__hip_atomic_load(done + qt - 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      char* part = lds + OFF_DQ + (((qt - w) & 1) * 4 + w) * 4096;
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+        *reinterpret_cast<f32x4*>(part + r * 128 + (((2 * gg + h) ^ (r & 7)) << 4)) =
+            f32x4{dqp[4 * gg], dqp[4 * gg + 1], dqp[4 * gg + 2], dqp[4 * gg + 3]};
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partial is in before the arrival counts it
+      int old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(cnt + qt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = __builtin_amdgcn_readfirstlane(old);
+      const int nc = min(qt + 1, 4);  // contributors: waves u <= qt
+      if (old == nc - 1) {  // the last one: sum the tile (4 passes of 8 rows), then free the slots
+#pragma unroll
+        for (int ps = 0; ps < 4; ++ps) {
+          const int R = 8 * ps + (lane >> 3), cq = lane & 7;
+          f32x4 a = {0.f, 0.f, 0.f, 0.f};
+          for (int u = 0; u < nc; ++u)
+            a += *reinterpret_cast<const f32x4*>(lds + OFF_DQ + (((qt - u) & 1) * 4 + u) * 4096 + R * 128 + ((cq ^ (R & 7)) << 4));
+          const int tq = qt * 32 + R;
+          if (Q2) {
+            *reinterpret_cast<u32x2*>(lds + qt * SL_SLICE + sl_off(R, cq >> 1) + (cq & 1) * 8) =
+                u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)};
+          } else {
+            a_bst8(rdq, tq < T ? (tq * P.dq_ld + 4 * cq) * 2 : A_OOB,
+                   u32x2{pack2bf(a[0] * dqs, a[1] * dqs), pack2bf(a[2] * dqs, a[3] * dqs)});
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the partial reads are done
+        if (lane == 0) __hip_atomic_store(done + qt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every tile is summed (each inside its last contributor's walk)
   } else
 #pragma unroll 1
   for (int i = 0; i < (MMT_F32_SKIP ? 0 : nt); ++i) {
