@@ -244,6 +244,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # experiment: the whole step on a torch stream of this HIP priority (the engine's
+    # side stream keeps the default one), unset = torch's default stream
+    if os.environ.get("MMT_BENCH_MAIN_PRIORITY"):
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=int(os.environ["MMT_BENCH_MAIN_PRIORITY"])))
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
         assert dist.get_world_size() == args.gpus == world, (dist.get_world_size(), args.gpus, world)
