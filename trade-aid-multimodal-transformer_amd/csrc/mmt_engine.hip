@@ -764,18 +764,21 @@ struct Runner {
   // bwd: the backward-data pair (mmt_launch_mlp2_bwd: dh = (dY W2) tanh', dx = dh W0)
   bool mlp2(const GemmProblem* g1s, const GemmProblem* g2s, int n, const char* what, bool bwd = false) {
     // forward fused by default: C1 8.80 -> 8.70 ms/step (standalone 45.9 -> 43.0 us at C1, 119.6 -> 112.8 us
-    // at the target); the backward pair stays two GEMMs by default (MMT_MLP2_BWD=1 fuses it): fused it
-    // measured 33.5 / 80.6 us against 29.3 / 61.6 us for the pair (C1 / target, tools/mlp2_bench.py) -- one
-    // block per CU at 136 KiB of LDS with both B operands read transposed cannot hide what the two 2-3
-    // blocks-per-CU GEMMs overlap (profiles/r5h_*.txt)
+    // at the target). The backward pair: fused at C = 256 only by default (MMT_MLP2_BWD: 2 = that, 1 =
+    // every width, 0 = never). Standalone the fused backward measured 33.5 / 80.6 us against 29.3 / 61.6 us
+    // for the pair (C1 / target, tools/mlp2_bench.py; one block per CU at 136 KiB of LDS with both B
+    // operands read transposed cannot hide what the two 2-3 blocks-per-CU GEMMs overlap, profiles/r5h_*),
+    // but in the C1 step beside the side stream it wins: 7.975 / 7.982 -> 7.949 / 7.960 ms (round 6,
+    // profiles/r6x_c1_env_ab.txt); at C = 512 it stays two GEMMs
     static const bool on = [] {
       const char* e = getenv("MMT_MLP2");
       return e ? atoi(e) != 0 : true;
     }();
-    static const bool on_bwd = [] {
+    static const int bwd_mode = [] {
       const char* e = getenv("MMT_MLP2_BWD");
-      return e ? atoi(e) != 0 : false;
+      return e ? atoi(e) : 2;
     }();
+    const bool on_bwd = bwd_mode == 1 || (bwd_mode == 2 && n >= 1 && g1s[0].N == 128);
     if (rc != MMT_OK || !on || (bwd && !on_bwd) || n < 1) return false;
     Mlp2Batch chunk[(MMT_MAX_GROUP + MMT_MLP2_GROUP - 1) / MMT_MLP2_GROUP] = {};
     const int nch = (n + MMT_MLP2_GROUP - 1) / MMT_MLP2_GROUP;
