@@ -153,7 +153,9 @@ def test_dropout_hs32_one_pass_backward_matches_oracle(C, H, T, cross, p, ring):
     stream, so both the self-attention and -- at two modalities -- the one-stream cross-attention take
     it; with 3-4 modalities and bit 7 the cross-attention walks 2-3 KV streams with its dQ summed in the
     engine's fp32 scratch) under dropout against the oracle's hash masks, at full and ragged T; ring 15 is the
-    two-pass pair on the same cases."""
+    two-pass pair on the same cases. With the one-pass kernel the self-attention also runs the Q/K/V
+    stage-2 backward in its epilogue (mmt_set_attn_qkv2 bit 0, default), so these cases check dh1 / dW2 /
+    db1 from there too."""
     L = ML.lib()
     old = L.mmt_attn_set_ring(ring)
     try:
