@@ -839,7 +839,7 @@ struct Runner {
   }
   // the main stream waits for everything enqueued on the side stream
   void join() {
-    flush();
+    flush(true);
     if (!side_stream()) return;
     hipEvent_t e = c->evpool[c->evnext++ % c->evpool.size()];
     ok(hipEventRecord(e, c->side), "event record");
@@ -850,7 +850,11 @@ struct Runner {
   // launches them. Every fork / join is a barrier packet costing ~10 us of main-stream idle, so
   // the stage code flushes a few times per layer instead of forking per GEMM.
   std::vector<std::pair<GemmBatch, const char*>> pend;
-  void flush() {
+  // hold: the stage's intermediate flushes keep their launches queued for the stage-end flush (one fork
+  // per stage instead of one per flush point; each fork's event record costs the main stream a gap)
+  bool hold = false;
+  void flush(bool force = false) {
+    if (hold && !force && rc == MMT_OK) return;
     if (pend.empty() || rc != MMT_OK) { pend.clear(); return; }
     hipStream_t ss = side_stream() ? side() : s;
     // merge consecutive queued weight-gradient batches of the same tile kind into one launch (up
@@ -2032,9 +2036,17 @@ int mmt_backward_stage(mmt_ctx* c, void* stream, int32_t stage, const float* los
   const bool defer = c->defer_join && r.side_stream();
   if (defer && stage >= 2)  // the side stream's work of stage - 2 read this stage's scratch copies
     r.ok(hipStreamWaitEvent(r.s, c->stage_ev[stage & 1], 0), "stream wait");
+  // MMT_FLUSH_HOLD=1: one side-stream fork per stage (every stage but the last layer's, whose weight
+  // gradients would otherwise only start after its data-gradient chain, at the end of the step)
+  static const int flush_hold = [] {
+    const char* e = getenv("MMT_FLUSH_HOLD");
+    return e ? atoi(e) : 0;
+  }();
+  r.hold = defer && flush_hold && stage < c->L;
   const int rc = run_backward_stage(c, r, stage, loss_grads, grads);
+  r.hold = false;
   if (defer) {
-    r.flush();
+    r.flush(true);
     r.ok(hipEventRecord(c->stage_ev[stage & 1], c->side), "event record");
   } else {
     r.join();  // the stage's gradient range is complete on the caller's stream (DP all-reduce order)
