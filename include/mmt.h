@@ -188,6 +188,9 @@ int mmt_exact_walk(void* stream, int32_t nmod, int32_t* const* data, const int64
 /* tuning knob: bit 0 / bit 1 = the slice-streamed hs-64 attention dK/dV / dQ pass, bit 2 = dK/dV at 3 waves
  * per SIMD, bit 3 = the slice-streamed hs-64 forward (default 15); returns the old value */
 int mmt_attn_set_ring(int v);
+/* tuning knob: attention dropout keep-bit tiles made per wave by attn_mask_kernel (1, 2, 4 or 8; 0 = the env
+ * MMT_MASK_G, default 4). The bits do not depend on it. Returns the old value */
+int mmt_attn_set_mask_g(int g);
 
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
 /* GEMM pipeline variant (tuning knob, process-wide). 128x128 tile: bits 0-3 forward / backward-data,

@@ -203,3 +203,28 @@ def test_attn_qkv2_fused_matches_separate(name):
     err = _rel(g1, g0)
     print(f"{name}: fused stage-2 vs separate grad rel-L2 {err:.3e}")
     assert err <= GRAD_BOUND, err
+
+
+@pytest.mark.parametrize("name", ["f_small", "f_c1"])
+def test_attn_mask_tiles_per_wave_same_bits(name):
+    """attn_mask_kernel makes G keep-bit tiles per wave (mmt_attn_set_mask_g; default 4), walking key
+    tile, query tile, (b, h) and KV stream in the wave. The bits are a hash of their coordinates only,
+    so every G gives the same forward bitwise (G = 1: one tile per wave, the round-5 form; G = 8 wraps
+    the 36-tile triangle of T = 256 and f_small's cross-attention stream boundaries inside waves)."""
+    L = ML.lib()
+    z, meta, cfg, sd, idx, tgt = _fixture(name)
+    idx_d = [t.cuda() for t in idx]
+    tgt_d = [t.cuda() for t in tgt]
+    out = {}
+    for g in (1, 2, 4, 8):
+        old = L.mmt_attn_set_mask_g(g)
+        try:
+            m = _build(meta, sd, 0.1)
+            out[g] = _fwd_bwd(m, idx_d, tgt_d)
+        finally:
+            L.mmt_attn_set_mask_g(old)
+    for g in (1, 2, 8):
+        assert torch.equal(out[g][1], out[4][1]), (g, out[g][1], out[4][1])
+        for a, b in zip(out[g][0], out[4][0]):
+            assert torch.equal(a, b), g
+        assert _rel(out[g][2], out[4][2]) <= GRAD_BOUND, g

@@ -2086,39 +2086,72 @@ hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, 
 // is the element's two mask dwords. Pure VALU work with no inputs: launched on a side stream it
 // overlaps the MFMA-bound GEMMs ahead of the attention.
 // =============================================================================================
+// A wave makes G consecutive tiles of the (stream, bh, row-major lower triangle) order: the index
+// division, the triangle root and the row hash are paid once per wave (and per query tile) instead of
+// once per tile.
+template <int G>
 __global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH, int T) {
   const AttnProblem& P = batch.p[blockIdx.z];
   const int nt = (T + 31) / 32;
   const int ntri = nt * (nt + 1) / 2;
   const int64_t per = (int64_t)BH * ntri;  // tiles per stream
-  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (P.drop_thr == 0 || t >= per * P.nstreams) return;  // wave-uniform
-  const int j = (int)(t / per);
-  const int64_t tt = t - (int64_t)j * per;
-  const int bh = (int)(tt / ntri), tri = (int)(tt % ntri);
+  const int64_t total = per * P.nstreams;
+  const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G;
+  if (P.drop_thr == 0 || t0 >= total) return;  // wave-uniform
+  int j = (int)(t0 / per);
+  int64_t tt = t0 - (int64_t)j * per;
+  int bh = (int)(tt / ntri);
+  const int tri = (int)(tt % ntri);
   int qt = (int)((sqrtf(8.f * (float)tri + 1.f) - 1.f) * 0.5f);
   while (qt > 0 && qt * (qt + 1) / 2 > tri) --qt;
   while ((qt + 1) * (qt + 2) / 2 <= tri) ++qt;
-  const int kt = tri - qt * (qt + 1) / 2;
+  int kt = tri - qt * (qt + 1) / 2;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
-  const uint32_t rowh = mmt_prob_row(dkey, (uint32_t)(bh * T + qt * 32 + r));
-  uint32_t out = 0;   // lane L < 32 collects key-major dword L = half (L & 1) of element (L >> 1)'s ballot
-  uint32_t word = 0;  // this lane's own 16 bits: element 2i at bit i, element 2i + 1 at bit 8 + i
+  const uint32_t thr = P.drop_thr;
+  uint32_t dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+  uint32_t rowh = mmt_prob_row(dkey, (uint32_t)(bh * T + qt * 32 + r));
+  const int ng = (int)min<int64_t>(G, total - t0);
+  for (int g = 0; g < ng; ++g) {
+    uint32_t out = 0;   // lane L < 32 collects key-major dword L = half (L & 1) of element (L >> 1)'s ballot
+    uint32_t word = 0;  // this lane's own 16 bits: element 2i at bit i, element 2i + 1 at bit 8 + i
 #pragma unroll
-  for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
-    const uint32_t key = (uint32_t)(kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h);
-    const uint32_t hk = mmt_prob_hash(rowh, key >> 1);
-    const bool k0 = mmt_keep(hk, 0, P.drop_thr), k1 = mmt_keep(hk, 1, P.drop_thr);
-    const uint64_t b0 = __builtin_amdgcn_ballot_w64(k0);
-    const uint64_t b1 = __builtin_amdgcn_ballot_w64(k1);
-    const uint32_t w0 = (lane & 1) ? (uint32_t)(b0 >> 32) : (uint32_t)b0;
-    const uint32_t w1 = (lane & 1) ? (uint32_t)(b1 >> 32) : (uint32_t)b1;
-    out = ((lane >> 1) == e) ? w0 : ((lane >> 1) == e + 1) ? w1 : out;
-    word |= ((uint32_t)k0 << (e >> 1)) | ((uint32_t)k1 << (8 + (e >> 1)));  // (keep_spread, elem_keep)
+    for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
+      const uint32_t key = (uint32_t)(kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h);
+      const uint32_t hk = mmt_prob_hash(rowh, key >> 1);
+      const bool k0 = mmt_keep(hk, 0, thr), k1 = mmt_keep(hk, 1, thr);
+      const uint64_t b0 = __builtin_amdgcn_ballot_w64(k0);
+      const uint64_t b1 = __builtin_amdgcn_ballot_w64(k1);
+      const uint32_t w0 = (lane & 1) ? (uint32_t)(b0 >> 32) : (uint32_t)b0;
+      const uint32_t w1 = (lane & 1) ? (uint32_t)(b1 >> 32) : (uint32_t)b1;
+      out = ((lane >> 1) == e) ? w0 : ((lane >> 1) == e + 1) ? w1 : out;
+      word |= ((uint32_t)k0 << (e >> 1)) | ((uint32_t)k1 << (8 + (e >> 1)));  // (keep_spread, elem_keep)
+    }
+    uint32_t* const dm = P.dmask[j];
+    if (lane < 32) dm[tt * 32 + lane] = out;
+    reinterpret_cast<uint16_t*>(dm + (per + tt) * 32)[lane] = (uint16_t)word;
+    // next tile: key tile, then query tile, then (b, h), then stream (wave-uniform branches)
+    ++tt;
+    if (++kt > qt) {
+      kt = 0;
+      if (++qt == nt) {
+        qt = 0;
+        if (++bh == BH) {
+          bh = 0;
+          tt = 0;
+          ++j;
+          dkey = mmt_hash(P.drop_key, (uint32_t)j, MMT_STREAM_SALT);
+        }
+      }
+      rowh = mmt_prob_row(dkey, (uint32_t)(bh * T + qt * 32 + r));
+    }
   }
-  if (lane < 32) P.dmask[j][tt * 32 + lane] = out;
-  reinterpret_cast<uint16_t*>(P.dmask[j] + (per + tt) * 32)[lane] = (uint16_t)word;
+}
+
+static int g_mask_g_rt = 0;
+extern "C" int mmt_attn_set_mask_g(int g) {
+  const int old = g_mask_g_rt;
+  g_mask_g_rt = g;
+  return old;
 }
 
 hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStream_t s) {
@@ -2134,7 +2167,21 @@ hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStre
   }
   if (ns == 0) return hipSuccess;
   const int64_t nt = (T + 31) / 32;
-  const int64_t waves = (int64_t)B * H * (nt * (nt + 1) / 2) * ns;
-  hipLaunchKernelGGL(attn_mask_kernel, dim3((unsigned)((waves + 3) / 4), 1, b.count), dim3(256), 0, s, b, B * H, T);
+  const int64_t tiles = (int64_t)B * H * (nt * (nt + 1) / 2) * ns;
+  // tiles per wave (MMT_MASK_G or mmt_attn_set_mask_g: 1, 2, 4 or 8)
+  static const int g_env = [] {
+    const char* e = getenv("MMT_MASK_G");
+    return e ? atoi(e) : 4;
+  }();
+  const int gv = g_mask_g_rt ? g_mask_g_rt : g_env;
+  const int g = (gv == 1 || gv == 2 || gv == 8) ? gv : 4;
+  const int64_t waves = (tiles + g - 1) / g;
+  const dim3 grid((unsigned)((waves + 3) / 4), 1, b.count);
+  switch (g) {
+    case 1: hipLaunchKernelGGL(attn_mask_kernel<1>, grid, dim3(256), 0, s, b, B * H, T); break;
+    case 2: hipLaunchKernelGGL(attn_mask_kernel<2>, grid, dim3(256), 0, s, b, B * H, T); break;
+    case 8: hipLaunchKernelGGL(attn_mask_kernel<8>, grid, dim3(256), 0, s, b, B * H, T); break;
+    default: hipLaunchKernelGGL(attn_mask_kernel<4>, grid, dim3(256), 0, s, b, B * H, T); break;
+  }
   return hipGetLastError();
 }

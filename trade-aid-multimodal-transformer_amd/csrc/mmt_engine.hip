@@ -919,8 +919,14 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   // keep bits of layer ll's self- and cross-attention dropout, one side-stream launch each (the
   // mask kernel reads nothing the main stream writes: a fork orders it after the previous step)
   hipStream_t ss = r.s;
+  // MMT_MASK_AHEAD=1: layer l + 1's keep bits are made while layer l computes (one fork and one join per
+  // layer) instead of all later layers' while layer 0 computes
+  static const int mask_ahead = [] {
+    const char* e = getenv("MMT_MASK_AHEAD");
+    return e ? atoi(e) : 0;
+  }();
   auto gen_masks = [&](int ll) {
-    if (ll <= 1) ss = r.side();  // layer 0: one fork; layers 1..L-1: one fork for all
+    if (ll <= 1 || mask_ahead) ss = r.side();  // layer 0: one fork; layers 1..L-1: one fork for all
     const LM* xl = &c->lm[(size_t)ll * M];
     const ActLM* al = &p.act[(size_t)ll * M];
     AttnBatch mb{}; mb.count = M;
@@ -1041,10 +1047,13 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       r.set_drop(q, l, i, DS_SA_PROB);
       if (r.drop) q.dmask[0] = r.W<uint32_t>(a[i].dm);
     }
-    if (r.drop && l <= 1) {
+    if (r.drop && (l <= 1 || mask_ahead)) {
       r.join();  // this layer's keep bits (SA and CA) are in (layer 1: every later layer's too)
-      if (l == 0)
+      if (mask_ahead) {
+        if (l + 1 < c->L) gen_masks(l + 1);
+      } else if (l == 0) {
         for (int ll = 1; ll < c->L; ++ll) gen_masks(ll);
+      }
     }
     r.attn(ab, false, scale, "attn_fwd");
     // ln2 in the fused out-projection's epilogue (MMT_LN2_FUSE=0: the separate ln_fwd pass; fp8 keeps

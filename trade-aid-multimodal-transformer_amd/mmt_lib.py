@@ -85,6 +85,7 @@ _SIGS = {
     "mmt_exact_walk": (c_i32, [c_vp, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), ctypes.POINTER(c_i32),
                                ctypes.POINTER(c_i32), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mmt_attn_set_ring": (c_i32, [ctypes.c_int]),
+    "mmt_attn_set_mask_g": (c_i32, [ctypes.c_int]),
     "mmt_emb_set_sort": (c_i32, [ctypes.c_int]),
     "mmt_set_relu_bits": (c_i32, [ctypes.c_int]),
     "mmt_set_drop_copy_fuse": (c_i32, [ctypes.c_int]),
