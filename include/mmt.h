@@ -189,7 +189,7 @@ int mmt_exact_walk(void* stream, int32_t nmod, int32_t* const* data, const int64
  * per SIMD, bit 3 = the slice-streamed hs-64 forward (default 15); returns the old value */
 int mmt_attn_set_ring(int v);
 /* tuning knob: attention dropout keep-bit tiles made per wave by attn_mask_kernel (1, 2, 4 or 8; 0 = the env
- * MMT_MASK_G, default 4). The bits do not depend on it. Returns the old value */
+ * MMT_MASK_G, default 8). The bits do not depend on it. Returns the old value */
 int mmt_attn_set_mask_g(int g);
 
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */

@@ -2089,6 +2089,9 @@ hipError_t mmt_launch_attn_bwd(const AttnBatch& b, int B, int T, int H, int hs, 
 // A wave makes G consecutive tiles of the (stream, bh, row-major lower triangle) order: the index
 // division, the triangle root and the row hash are paid once per wave (and per query tile) instead of
 // once per tile.
+// v_writelane_b32 (the LLVM intrinsic; hipcc exposes no builtin for it): a wave-uniform value into one lane
+extern "C" __device__ int mmt_writelane(int v, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 template <int G>
 __global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH, int T) {
   const AttnProblem& P = batch.p[blockIdx.z];
@@ -2098,10 +2101,21 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH,
   const int64_t total = per * P.nstreams;
   const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G;
   if (P.drop_thr == 0 || t0 >= total) return;  // wave-uniform
-  int j = (int)(t0 / per);
-  int64_t tt = t0 - (int64_t)j * per;
-  int bh = (int)(tt / ntri);
-  const int tri = (int)(tt % ntri);
+  int j, bh, tri;
+  int64_t tt;
+  if (total <= 0x7fffffff) {  // 32-bit index arithmetic (an emulated 64-bit division costs ~150 instructions)
+    const uint32_t t32 = (uint32_t)t0, p32 = (uint32_t)per;
+    j = (int)(t32 / p32);
+    const uint32_t r32 = t32 - (uint32_t)j * p32;
+    bh = (int)(r32 / (uint32_t)ntri);
+    tri = (int)(r32 - (uint32_t)bh * (uint32_t)ntri);
+    tt = r32;
+  } else {
+    j = (int)(t0 / per);
+    tt = t0 - (int64_t)j * per;
+    bh = (int)(tt / ntri);
+    tri = (int)(tt % ntri);
+  }
   int qt = (int)((sqrtf(8.f * (float)tri + 1.f) - 1.f) * 0.5f);
   while (qt > 0 && qt * (qt + 1) / 2 > tri) --qt;
   while ((qt + 1) * (qt + 2) / 2 <= tri) ++qt;
@@ -2112,19 +2126,23 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(AttnBatch batch, int BH,
   uint32_t rowh = mmt_prob_row(dkey, (uint32_t)(bh * T + qt * 32 + r));
   const int ng = (int)min<int64_t>(G, total - t0);
   for (int g = 0; g < ng; ++g) {
-    uint32_t out = 0;   // lane L < 32 collects key-major dword L = half (L & 1) of element (L >> 1)'s ballot
+    // key pair c = kt*16 + 2h + off(e): the row hash plus the tile's part once, the pair offsets as constants
+    const uint32_t hb = rowh + (uint32_t)(kt * 16 + 2 * h) * 0x9E3779B9u;
+    uint32_t out = 0;   // lane L < 32: key-major dword L = half (L & 1) of element (L >> 1)'s ballot
     uint32_t word = 0;  // this lane's own 16 bits: element 2i at bit i, element 2i + 1 at bit 8 + i
 #pragma unroll
     for (int e = 0; e < 16; e += 2) {  // keys k, k+1 (k even) share one hash
-      const uint32_t key = (uint32_t)(kt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h);
-      const uint32_t hk = mmt_prob_hash(rowh, key >> 1);
+      const uint32_t off = (uint32_t)(((e & 3) >> 1) + 4 * (e >> 2));
+      const uint32_t hk = mmt_prob_fin(hb + off * 0x9E3779B9u);
       const bool k0 = mmt_keep(hk, 0, thr), k1 = mmt_keep(hk, 1, thr);
       const uint64_t b0 = __builtin_amdgcn_ballot_w64(k0);
       const uint64_t b1 = __builtin_amdgcn_ballot_w64(k1);
-      const uint32_t w0 = (lane & 1) ? (uint32_t)(b0 >> 32) : (uint32_t)b0;
-      const uint32_t w1 = (lane & 1) ? (uint32_t)(b1 >> 32) : (uint32_t)b1;
-      out = ((lane >> 1) == e) ? w0 : ((lane >> 1) == e + 1) ? w1 : out;
-      word |= ((uint32_t)k0 << (e >> 1)) | ((uint32_t)k1 << (8 + (e >> 1)));  // (keep_spread, elem_keep)
+      // the wave-uniform ballots straight into their lanes (elements e, e + 1 -> dwords 2e .. 2e + 3)
+      out = (uint32_t)mmt_writelane((int)(uint32_t)b0, 2 * e, (int)out);
+      out = (uint32_t)mmt_writelane((int)(uint32_t)(b0 >> 32), 2 * e + 1, (int)out);
+      out = (uint32_t)mmt_writelane((int)(uint32_t)b1, 2 * e + 2, (int)out);
+      out = (uint32_t)mmt_writelane((int)(uint32_t)(b1 >> 32), 2 * e + 3, (int)out);
+      word |= (k0 ? 1u << (e >> 1) : 0u) | (k1 ? 1u << (8 + (e >> 1)) : 0u);  // (keep_spread, elem_keep)
     }
     uint32_t* const dm = P.dmask[j];
     if (lane < 32) dm[tt * 32 + lane] = out;
@@ -2171,17 +2189,19 @@ hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStre
   // tiles per wave (MMT_MASK_G or mmt_attn_set_mask_g: 1, 2, 4 or 8)
   static const int g_env = [] {
     const char* e = getenv("MMT_MASK_G");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 8;
   }();
+  // (8 against 4: C3 142.3 -> 140.9-141.1 ms, C1 / target equal; 4 against 1, the one-tile form: C3 149.2 ->
+  // 143.7, target 19.40 -> 19.24, C1 7.98 -> 7.91: profiles/r6aa_mask_pileup.txt, r6ab_mask_ab.txt)
   const int gv = g_mask_g_rt ? g_mask_g_rt : g_env;
-  const int g = (gv == 1 || gv == 2 || gv == 8) ? gv : 4;
+  const int g = (gv == 1 || gv == 2 || gv == 4) ? gv : 8;
   const int64_t waves = (tiles + g - 1) / g;
   const dim3 grid((unsigned)((waves + 3) / 4), 1, b.count);
   switch (g) {
     case 1: hipLaunchKernelGGL(attn_mask_kernel<1>, grid, dim3(256), 0, s, b, B * H, T); break;
     case 2: hipLaunchKernelGGL(attn_mask_kernel<2>, grid, dim3(256), 0, s, b, B * H, T); break;
-    case 8: hipLaunchKernelGGL(attn_mask_kernel<8>, grid, dim3(256), 0, s, b, B * H, T); break;
-    default: hipLaunchKernelGGL(attn_mask_kernel<4>, grid, dim3(256), 0, s, b, B * H, T); break;
+    case 4: hipLaunchKernelGGL(attn_mask_kernel<4>, grid, dim3(256), 0, s, b, B * H, T); break;
+    default: hipLaunchKernelGGL(attn_mask_kernel<8>, grid, dim3(256), 0, s, b, B * H, T); break;
   }
   return hipGetLastError();
 }

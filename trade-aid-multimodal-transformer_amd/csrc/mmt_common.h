@@ -132,10 +132,14 @@ __host__ __device__ __forceinline__ uint32_t mmt_hash(uint32_t a, uint32_t b, ui
 __host__ __device__ __forceinline__ uint32_t mmt_prob_row(uint32_t stream_key, uint32_t row) {
   return mmt_hash(stream_key, row, MMT_PROB_ROW_SALT);
 }
-__host__ __device__ __forceinline__ uint32_t mmt_prob_hash(uint32_t row_hash, uint32_t c) {
-  uint32_t h = row_hash + c * 0x9E3779B9u;
+// the finaliser alone: mmt_prob_hash(rh, c) == mmt_prob_fin(rh + c * 0x9E3779B9u) (wrapping arithmetic, so a
+// kernel may add a per-tile base and compile-time pair offsets separately)
+__host__ __device__ __forceinline__ uint32_t mmt_prob_fin(uint32_t h) {
   h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
   return h;
+}
+__host__ __device__ __forceinline__ uint32_t mmt_prob_hash(uint32_t row_hash, uint32_t c) {
+  return mmt_prob_fin(row_hash + c * 0x9E3779B9u);
 }
 
 // ---------------------------------------------------------------------------------------------
