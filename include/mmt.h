@@ -191,6 +191,10 @@ int mmt_attn_set_ring(int v);
 /* tuning knob: attention dropout keep-bit tiles made per wave by attn_mask_kernel (1, 2, 4 or 8; 0 = the env
  * MMT_MASK_G, default 8). The bits do not depend on it. Returns the old value */
 int mmt_attn_set_mask_g(int g);
+/* tuning knob: 1 = the big GEMM launches with K < 1024 (the d512 FFN / cross-attention K/V products) on a
+ * 128 x 256 tile at two workgroups per CU instead of the 256 x 256 ping-pong kernel; 0 (default, env
+ * MMT_GEMM_T2) = the ping-pong kernel. Returns the old value */
+int mmt_gemm_set_t2(int v);
 
 /* ---- primitive kernels (single problem), for kernel-level parity tests ------------------- */
 /* GEMM pipeline variant (tuning knob, process-wide). 128x128 tile: bits 0-3 forward / backward-data,

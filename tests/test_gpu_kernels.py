@@ -137,6 +137,25 @@ def test_gemm_pipeline_variants(variant, M, N, K):
         L.mmt_gemm_set_variant(-1)
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 256, 512), (300, 264, 520), (768, 520, 136), (256, 1024, 64),
+                                   (520, 776, 1000), (256, 256, 32), (1000, 600, 512)])
+def test_gemm_t2_tile(M, N, K):
+    """The 128 x 256 tile at two workgroups per CU (mmt_gemm_set_t2(1): the big launches with K below 1024;
+    bit 16 of the variant forces the big path at every K) on every forward and backward-data epilogue,
+    ragged M / N / K included."""
+    L = ML.lib()
+    assert L.mmt_gemm_set_variant(0x10000) == 0
+    old = L.mmt_gemm_set_t2(1)
+    try:
+        for epi in ["store_bf16", "bias_tanh_bf16", "bias_relu_bf16", "bias_resid_f32", "store_f32"]:
+            test_gemm_forward_linear(M, N, K, epi)
+        for epi in ["store_bf16", "dtanh_bf16", "drelu_bf16", "store_f32", "acc_f32"]:
+            test_gemm_backward_data(M, N, K, epi)
+    finally:
+        L.mmt_gemm_set_t2(old)
+        L.mmt_gemm_set_variant(-1)
+
+
 @pytest.mark.parametrize("M,N,R", [(384, 256, 4096), (1024, 256, 2048), (900, 450, 1000), (6, 32, 300), (32, 16, 77)])
 @pytest.mark.parametrize("splits", [1, 4, 0])
 def test_gemm_weight_grad(M, N, R, splits):

@@ -62,6 +62,8 @@ SHAPES = [
     ("tgt_ffn0_epi_only", 1, 1, "bias_relu_bf16", R, 2048, 0, 1),
     ("tgt_ffn2dx_epi_only", 1, 0, "drelu_bf16", R, 2048, 0, 1),
     ("tgt_ffn2_fwd", 1, 1, "bias_resid_f32", R, 512, 2048, 1),
+    ("c3_cakv_fwd", 1, 1, "store_bf16", 2 * R, 1024, 512, 1),
+    ("c3_cakv_dx", 1, 0, "acc_f32", 2 * R, 512, 1024, 1),
     ("c4_ffn0_fwd", 1, 1, "bias_relu_bf16", R, 4096, 1024, 1),
     ("c4_ffn0_store", 1, 1, "store_bf16", R, 4096, 1024, 1),
     ("c4_ffn2_dx", 1, 0, "drelu_bf16", R, 4096, 1024, 1),

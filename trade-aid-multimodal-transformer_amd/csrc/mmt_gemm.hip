@@ -251,7 +251,7 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   constexpr int RING = ST * STAGE_BYTES, CTILE = EPI_ROWS * (GBN + 4) * 4;
   constexpr int LDS_MAIN = RING > CTILE ? RING : CTILE;
   // + the fused Q/K/V stage 2's W2 fragments (qkv2_stage_w2)
-  constexpr int LDS_W2 = (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4) ? QKV2_W2_LDS : 0;
+  constexpr int LDS_W2 = (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4 && TL::BN == 128) ? QKV2_W2_LDS : 0;
   __shared__ __attribute__((aligned(1024))) char lds[LDS_MAIN + LDS_W2];
 
   const int tid = threadIdx.x;
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
     for (int j = 0; j < AJ; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-  if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4) {
+  if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4 && TL::BN == 128) {
     // fused Q/K/V stage 2: the accumulators start at bias / alpha, so the epilogue (short of
     // registers at 3 blocks per CU) holds no bias values
     if (P.qkv2_out) qkv2_stage_w2<TL>(P, lds + LDS_MAIN, n0, tid);  // read after the epilogue's barrier
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(TL::NT, MINB) void gemm_kernel(GemmBatch batch) {
   const int h = lane >> 5, r = lane & 31;
   // the fused per-head Q/K/V stage 2 on the 128 x 128 tile only: next to the 256 x 256 tile's 128
   // accumulators it spills (the launcher refuses qkv2_out there; the engine then runs qkv2_fwd)
-  if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4) {
+  if constexpr (SWAP && EPI == EPI_BIAS_TANH_BF16 && TL::NW == 4 && TL::BN == 128) {
     if (P.qkv2_out) {  // the per-head stage 2 of Q/K/V (uniform per problem)
       qkv2_fused<TL>(P, acc, lds, lds + LDS_MAIN, alpha, m0, n0, lane, wave);
       epilogue_swap<TL, EPI, EPI_ROWS, true>(P, acc, lds, o32, alpha, m0, n0, tid, lane, wave);
@@ -638,9 +638,43 @@ static bool gemm8_ln_on() {
   return gemm8_on() && env;
 }
 
+// K threshold 1024 (round 2 c): at K = 512 (d512 forward GEMMs and data gradients) the 128x128 tile at
+// 2-3 blocks per CU overlaps one block's epilogue with the others' K loops and shares the chip with
+// the side stream better than the single 256x256 block per CU (target step 23.13 -> 22.73 ms)
+static int g_big_kmin = [] {
+  const char* e = getenv("MMT_GEMM_BIG_KMIN");
+  return e ? atoi(e) : 1024;
+}();
+// MMT_GEMM_T2=1: the big launches with K below the 256 x 256 tile's threshold (K = 512: the d512 FFN and
+// cross-attention K/V products the ping-pong kernel takes by default) on a 128 x 256 tile of 4 waves (TileL's
+// per-wave 128 x 64) at two workgroups per CU (BK 32 x 3 stages: 72 KiB each), so one workgroup's prologue /
+// epilogue overlaps the other's K loop
+using TileM = TileCfg<1, 4, 4, 2>;
+static int g_gemm_t2 = [] {
+  const char* e = getenv("MMT_GEMM_T2");
+  return e ? atoi(e) : 0;
+}();
+extern "C" int mmt_gemm_set_t2(int v) {
+  const int old = g_gemm_t2;
+  g_gemm_t2 = v;
+  return old;
+}
+
 template <bool A_KC, bool B_KC, bool SWAP, int EPI>
 static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t s) {
   if (b.count == 0) return hipSuccess;
+  if constexpr (SWAP && EPI != EPI_ATOMIC_F32) {
+    if (big && g_gemm_t2) {
+      int maxk = 0;
+      for (int g = 0; g < b.count; ++g) maxk = std::max(maxk, b.p[g].K);
+      if (maxk < g_big_kmin) {
+        const int mt = max_tiles<TileM>(b, nullptr);
+        if (mt == 0) return hipSuccess;
+        launch_v<TileM, 32, 3, A_KC, B_KC, SWAP, EPI, 2>(b, dim3(mt, std::max(1, splits), b.count), s);
+        return hipGetLastError();
+      }
+    }
+  }
   if (big) {
     const int mt = max_tiles<TileL>(b, nullptr);
     if (mt == 0) return hipSuccess;
@@ -707,13 +741,7 @@ static int g_big_mode = [] {
   const char* e = getenv("MMT_GEMM_BIG");
   return e ? atoi(e) : 1;
 }();
-// K threshold 1024 (round 2 c): at K = 512 (d512 forward GEMMs and data gradients) the 128x128 tile at
-// 2-3 blocks per CU overlaps one block's epilogue with the others' K loops and shares the chip with
-// the side stream better than the single 256x256 block per CU (target step 23.13 -> 22.73 ms)
-static int g_big_kmin = [] {
-  const char* e = getenv("MMT_GEMM_BIG_KMIN");
-  return e ? atoi(e) : 1024;
-}();
+
 // K threshold of the ping-pong 256 x 256 kernel for launches with many tiles: at K = 512 it wins where
 // the launch has >= 4 tiles per CU (the target's ffn0 and ffn2 dX: 221 -> 177 and 252 -> 230 us
 // standalone; smaller launches leave CUs idle or lose the 128 x 128 tile's 2-3 blocks per CU beside the

@@ -86,6 +86,7 @@ _SIGS = {
                                ctypes.POINTER(c_i32), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mmt_attn_set_ring": (c_i32, [ctypes.c_int]),
     "mmt_attn_set_mask_g": (c_i32, [ctypes.c_int]),
+    "mmt_gemm_set_t2": (c_i32, [ctypes.c_int]),
     "mmt_emb_set_sort": (c_i32, [ctypes.c_int]),
     "mmt_set_relu_bits": (c_i32, [ctypes.c_int]),
     "mmt_set_drop_copy_fuse": (c_i32, [ctypes.c_int]),
