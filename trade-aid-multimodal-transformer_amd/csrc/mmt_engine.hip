@@ -712,7 +712,13 @@ struct Runner {
   void gemm8(const GemmBatch& b, int epi, const char* what) {
     if (rc != MMT_OK) return;
     const int id = probe_begin(what, s);
-    ok(mmt_launch_gemm_f8(b, epi, s), what);
+    if (gemm_hint) {
+      GemmBatch h = b;
+      h.tile_hint = gemm_hint;
+      ok(mmt_launch_gemm_f8(h, epi, s), what);
+    } else {
+      ok(mmt_launch_gemm_f8(b, epi, s), what);
+    }
     if (id >= 0) {
       double fl = 0, by = 0;
       gemm_cost(b, epi, &fl, &by);
@@ -818,10 +824,19 @@ struct Runner {
     }
     return true;
   }
+  // GemmBatch::tile_hint for the main-stream GEMMs launched while it is set (run_forward: beside the
+  // side stream's keep-bit launches)
+  int gemm_hint = 0;
   void gemm(const GemmBatch& b, bool akc, bool bkc, int epi, int splits, const char* what) {
     if (rc != MMT_OK) return;
     const int id = probe_begin(what, s);
-    ok(mmt_launch_gemm(b, akc, bkc, epi, splits, s), what);
+    if (gemm_hint) {
+      GemmBatch h = b;
+      h.tile_hint = gemm_hint;
+      ok(mmt_launch_gemm(h, akc, bkc, epi, splits, s), what);
+    } else {
+      ok(mmt_launch_gemm(b, akc, bkc, epi, splits, s), what);
+    }
     if (id >= 0) {
       double fl = 0, by = 0;
       gemm_cost(b, epi, &fl, &by);
@@ -926,6 +941,10 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   static const int mask_ahead = [] {
     const char* e = getenv("MMT_MASK_AHEAD");
     return e ? atoi(e) : 0;
+  }();
+  static const int mask_t2 = [] {
+    const char* e = getenv("MMT_MASK_T2");
+    return e ? atoi(e) : 1;
   }();
   auto gen_masks = [&](int ll) {
     if (ll <= 1 || mask_ahead) ss = r.side();  // layer 0: one fork; layers 1..L-1: one fork for all
@@ -1051,10 +1070,15 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
     }
     if (r.drop && (l <= 1 || mask_ahead)) {
       r.join();  // this layer's keep bits (SA and CA) are in (layer 1: every later layer's too)
+      r.gemm_hint = 0;
       if (mask_ahead) {
         if (l + 1 < c->L) gen_masks(l + 1);
       } else if (l == 0) {
         for (int ll = 1; ll < c->L; ++ll) gen_masks(ll);
+        // until layer 1's join the later layers' keep bits fill the CUs the side stream can reach: a
+        // ping-pong GEMM block needs a CU with none of them on it (all its VGPRs and 128 KiB of LDS), the
+        // 128 x 256 tile fits beside them (MMT_MASK_T2=0: the ping-pong kernel throughout)
+        if (mask_t2) r.gemm_hint = 1;
       }
     }
     r.attn(ab, false, scale, "attn_fwd");

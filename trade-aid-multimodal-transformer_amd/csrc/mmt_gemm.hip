@@ -664,7 +664,7 @@ template <bool A_KC, bool B_KC, bool SWAP, int EPI>
 static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t s) {
   if (b.count == 0) return hipSuccess;
   if constexpr (SWAP && EPI != EPI_ATOMIC_F32) {
-    if (big && g_gemm_t2) {
+    if (big && (g_gemm_t2 || b.tile_hint == 1)) {
       int maxk = 0;
       for (int g = 0; g < b.count; ++g) maxk = std::max(maxk, b.p[g].K);
       if (maxk < g_big_kmin) {
@@ -1046,7 +1046,8 @@ static hipError_t launch_f8(const GemmBatch& b, hipStream_t s) {
 template <int EPI>
 static hipError_t launch_f8_tile(const GemmBatch& b, hipStream_t s) {
   // the 256x256 tile where every problem fills it and K is long (as the bf16 policy), else 128x128
-  bool big = g_big_mode != 0;
+  // (tile_hint 1: the 128 x 128 tile, which fits beside other streams' waves where the 256 x 256 one needs a free CU)
+  bool big = g_big_mode != 0 && b.tile_hint != 1;
   for (int g = 0; g < b.count; ++g)
     if (b.p[g].M < TileL::BM || b.p[g].N < TileL::BN || b.p[g].K < g_big_kmin) big = false;
   return big ? launch_f8<TileL, EPI>(b, s) : launch_f8<TileS, EPI>(b, s);
