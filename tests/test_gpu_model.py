@@ -166,17 +166,17 @@ def test_dropout_hs32_one_pass_backward_matches_oracle(C, H, T, cross, p, ring):
 
 @pytest.mark.parametrize("C,H,T,cross,p", [(64, 2, 288, [True, False], 0.2), (128, 2, 160, [False, True], 0.1),
                                              (128, 2, 300, [True, False], 0.1)])
-def test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p):
+def test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p, L=1):
     """Dropout at sequence lengths past one LDS chunk (hs 32: 256 rows, hs 64: 128 rows; the hs-64 dQ
     pass: 256 rows, so T = 300 takes it past one) with a ragged last tile: the keep bits of attn_mask_kernel, staged chunk by chunk in all three
     attention kernels, against the oracle's hash masks (random init, the oracle as reference)."""
     import mmt_oracle as O
     import model as mmt_model
     V = [13, 7, 5, 11][:len(cross)]
-    ocfg = O.OracleConfig(C, H, 1, T, V, cross)
+    ocfg = O.OracleConfig(C, H, L, T, V, cross)
     g = torch.Generator().manual_seed(5)
     sd = O.init_params(ocfg, g)
-    config_utils._config_cache = {"n_embd": C, "n_head": H, "n_layer": 1, "block_size": T, "dropout": p,
+    config_utils._config_cache = {"n_embd": C, "n_head": H, "n_layer": L, "block_size": T, "dropout": p,
                                   "device": "cuda", "batch_size": 2, "eval_iters": 1}
     params = [[None] * 8 + [c] + [None] * 3 for c in cross]
     m = mmt_model.MultimodalTransformer(len(V), V, params).to("cuda")
@@ -205,6 +205,14 @@ def test_dropout_multichunk_masks_match_oracle(C, H, T, cross, p):
     alln = torch.cat([c for _, _, c in pairs])
     assert rel(allg, allr) < 3e-2
     assert rel(allg, alln) > 3 * max(rel(allg, allr), 1e-2)  # the masks act
+
+
+@pytest.mark.parametrize("L", [5, 12])
+def test_dropout_deep_masks_match_oracle(L):
+    """Keep bits of every layer against the oracle at depth: 5 layers make the later layers' bits beside
+    layer 0 (one fork, joined at layer 1); from 12 layers on the engine makes layer l + 1's bits while
+    layer l computes (one fork and join per layer, run_forward's mask_ahead)."""
+    test_dropout_multichunk_masks_match_oracle(64, 2, 72, [True, False, True], 0.1, L=L)
 
 
 @pytest.mark.parametrize("name", ["f_small", "f_hs32"])

@@ -935,13 +935,16 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
   // mask kernel reads nothing the main stream writes: a fork orders it after the previous step)
   hipStream_t ss = r.s;
   // MMT_MASK_AHEAD=1: layer l + 1's keep bits are made while layer l computes (one fork and one join per
-  // layer) instead of all later layers' while layer 0 computes. Off: the masks then overlap each layer's
-  // attention forward instead of layer 0's GEMMs (C3 attention forward 394 -> 955 us live): C3 141.1 -> 140.5-140.9
-  // ms, target 19.07 -> 19.04, C1 7.87 -> 7.90 (profiles/r6ab_mask_ab.txt)
-  static const int mask_ahead = [] {
+  // layer) instead of all later layers' while layer 0 computes. The masks then overlap each layer's attention
+  // forward instead of layer 0's GEMMs (C3 attention forward 394 -> 955 us live). Default: from 12 layers on,
+  // where the later layers' pile beside layer 0 grows past what one layer's GEMMs hide: C4 (24 layers) 312.4 ->
+  // 308.6 ms, C3 (12) 141.1 -> 140.5-140.9, target (6) 19.07 -> 19.04, C1 (6) 7.87 -> 7.90
+  // (profiles/r6ab_mask_ab.txt, r6ae_c4_mask_ab.txt); MMT_MASK_AHEAD=0 / 1 forces it
+  static const int mask_ahead_env = [] {
     const char* e = getenv("MMT_MASK_AHEAD");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : -1;
   }();
+  const bool mask_ahead = mask_ahead_env >= 0 ? mask_ahead_env != 0 : c->L >= 12;
   static const int mask_t2 = [] {
     const char* e = getenv("MMT_MASK_T2");
     return e ? atoi(e) : 1;
