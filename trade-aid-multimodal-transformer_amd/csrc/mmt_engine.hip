@@ -901,9 +901,10 @@ struct Runner {
   // weight-gradient GEMMs share one split-K slab region: they run in launch order on ONE stream
   // (the side stream when there is one), so no two of them ever write the slabs at once (a
   // probed launch no longer jumps to the main stream: ADVICE r1)
-  void dwgemm(const GemmBatch& b, const char* what) {
+  void dwgemm(const GemmBatch& b, const char* what, int hint = 0) {
     if (rc != MMT_OK) return;
     pend.emplace_back(b, what);  // launched (merged) at the next flush(), on the side stream if any
+    pend.back().first.tile_hint = hint;
   }
   void attn(const AttnBatch& ab, bool bwd, float scale, const char* what) {
     if (rc != MMT_OK) return;
@@ -1711,7 +1712,15 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     dx.p[i].dbias = grads + x[i].bf0;
     if (r.c->relu_bits) { dx.p[i].mask8 = r.W<uint8_t>(a[i].fm); dx.p[i].ldm8 = 4 * C / 8; }  // ReLU' from bits
   }
-  r.dwgemm(dw, "ffn2_dw");
+  // MMT_DW_ATTN_SMALL=1: the FFN weight gradients (the side-stream launches still running when the
+  // self-attention backward starts) on the 128 x 128 tile, whose 64 KiB of LDS leave room on their CUs for
+  // one of the attention backward's 80 KiB workgroups
+  static const int dw_attn_small = [] {
+    const char* e = getenv("MMT_DW_ATTN_SMALL");
+    return e ? atoi(e) : 0;
+  }();
+  const int ffn_dw_hint = dw_attn_small ? 2 : 0;
+  r.dwgemm(dw, "ffn2_dw", ffn_dw_hint);
   r.gemm(dx, true, false, EPI_DRELU_BF16, 1, "ffn2_dx");
   for (int i = 0; i < M; ++i) {
     const bf16_t* g = r.W<bf16_t>(p.gbig[par][i]);
@@ -1719,7 +1728,7 @@ int run_backward_stage(mmt_ctx* c, Runner& r, int stage, const float* loss_grads
     dx.p[i] = gp_dx(g, 4 * C, wpk, x[i].F0, R);
     dx.p[i].o32 = r.W<float>(p.dln[i]); dx.p[i].ldc = C;
   }
-  r.dwgemm(dw, "ffn0_dw");
+  r.dwgemm(dw, "ffn0_dw", ffn_dw_hint);
   r.flush();
   d16_advance(c);
   for (int i = 0; i < M; ++i) {

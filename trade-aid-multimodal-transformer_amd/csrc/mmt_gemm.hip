@@ -904,7 +904,9 @@ static const int g_dw_small = [] {
   const char* e = getenv("MMT_DW_SMALL");
   return e ? atoi(e) : 0;
 }();
-static bool use_big_dw(const GemmBatch& b) { return !g_dw_small && use_big(b); }
+// (GemmBatch::tile_hint 2: this launch on the 128 x 128 tile, 64 KiB of LDS, which fits on a CU beside the
+// main stream's 80 KiB attention-backward workgroups where the 256 x 256 one's 128 KiB does not)
+static bool use_big_dw(const GemmBatch& b) { return !g_dw_small && b.tile_hint != 2 && use_big(b); }
 
 hipError_t mmt_launch_gemm_wgrad(const GemmBatch& b, float* slab, int64_t slab_bytes, hipStream_t s) {
   if (b.count == 0) return hipSuccess;
