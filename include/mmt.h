@@ -200,7 +200,7 @@ int mmt_gemm_set_t2(int v);
 /* GEMM pipeline variant (tuning knob, process-wide). 128x128 tile: bits 0-3 forward / backward-data,
  * bits 4-7 weight gradients: 0 = K-step 64 x 2 LDS stages, 1 = 32 x 2, 2 = 32 x 3, 3 = 32 x 4,
  * 4 = 64 x 3, 5 = 32 x 3 and 6 = 32 x 2 at 3+ blocks per CU (64-row epilogue passes). 256x256 tile:
- * bits 8-11 (0 = environment / default policy, 1 / 2 = BK 32 x 4 / x 3); bit 16: the 256x256 tile
+ * bits 8-11 (0 = environment / default policy, 1 / 2 / 3 = BK 32 x 4 / x 3 / x 2); bit 16: the 256x256 tile
  * whatever K. Returns -1 for a field out of range. variant < 0: the default policy (128x128: 6 for
  * bf16-output epilogues without an aux operand, else 0; 256x256: 1 for the weight gradients, else
  * BK 64 x 2). */

@@ -118,11 +118,11 @@ def test_gemm_backward_data(M, N, K, epi):
         assert rel(o32, base + ref) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [0x100 | 0x10000, 0x200 | 0x10000, 0x10000, 5, 2, 4, 0x20000 | 0x10000])
+@pytest.mark.parametrize("variant", [0x100 | 0x10000, 0x200 | 0x10000, 0x300 | 0x10000, 0x10000, 5, 2, 4, 0x20000 | 0x10000])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 512), (300, 264, 520), (768, 520, 136), (256, 1024, 64),
                                    (520, 776, 1000), (256, 256, 32)])
 def test_gemm_pipeline_variants(variant, M, N, K):
-    """The 256 x 256 tile's rings (BK 32 x 4, BK 32 x 3, BK 64 x 2: bits 8-11, forced at every K by bit
+    """The 256 x 256 tile's rings (BK 32 x 4, BK 32 x 3, BK 32 x 2, BK 64 x 2: bits 8-11, forced at every K by bit
     16), the ping-pong 256 x 256 kernel (gemm8_kernel, bit 17: K-tiles 1, 2, 3, 8, 9 and 16, ragged M / N / K)
     and the deeper 128 x 128 rings (variants 5 / 2 / 4) on the forward and backward-data epilogues,
     ragged edges included (the rings' vmcnt counts depend on the stages left in flight)."""
@@ -177,10 +177,11 @@ def test_gemm_weight_grad(M, N, R, splits):
 @pytest.mark.parametrize("M,N,R", [(1024, 256, 16384), (384, 256, 4096), (900, 450, 1000), (6, 32, 300),
                                    (128, 256, 16384), (450, 256, 3000)])
 @pytest.mark.parametrize("slab_mb", [0, 64])
-@pytest.mark.parametrize("variant", [-1, 0x30000])
+@pytest.mark.parametrize("variant", [-1, 0x30000, 0x300])
 def test_gemm_wgrad_slabs(M, N, R, slab_mb, variant):
     # the engine's weight-gradient path: split-K fp32 slabs + reduce (or one K pass without scratch);
-    # variant 0x30000: the ping-pong 256 x 256 kernel (MN-contiguous operands, K slices, XCD-major grid)
+    # variant 0x30000: the ping-pong 256 x 256 kernel (MN-contiguous operands, K slices, XCD-major grid);
+    # 0x300: the 256 x 256 ring at BK 32 x 2 stages
     L = ML.lib()
     assert L.mmt_gemm_set_variant(variant) == 0
     try:

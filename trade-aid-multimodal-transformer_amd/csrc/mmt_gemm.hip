@@ -44,7 +44,7 @@ extern "C" int mmt_gemm_set_variant(int v) {
     g_gemm_variant = -1; g_gemm_variant_dw = 0; g_gemm_big_variant_rt = 0; g_force_big_rt = 0; g_gemm8_rt = -1;
     return 0;
   }
-  if ((v & 15) > 6 || ((v >> 4) & 15) > 6 || ((v >> 8) & 15) > 2) return -1;
+  if ((v & 15) > 6 || ((v >> 4) & 15) > 6 || ((v >> 8) & 15) > 3) return -1;
   g_gemm_variant = v & 15;
   g_gemm_variant_dw = (v >> 4) & 15;
   g_gemm_big_variant_rt = (v >> 8) & 15;
@@ -698,6 +698,9 @@ static hipError_t launch_t(const GemmBatch& b, int splits, bool big, hipStream_t
     switch (bv) {
       case 1: launch_v<TileL, 32, 4, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
       case 2: launch_v<TileL, 32, 3, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
+      // BK 32 x 2 (66.5 KiB with the epilogue tile): leaves room on its CU for an 80 KiB attention-backward
+      // workgroup beside it (measured for the weight gradients)
+      case 3: launch_v<TileL, 32, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
       default: launch_v<TileL, 64, 2, A_KC, B_KC, SWAP, EPI>(b, grid, s); break;
     }
     return hipGetLastError();
