@@ -1,0 +1,9 @@
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+T=r6am
+bash tools/gpu_steps.sh \
+ "900|${T}_pytest|python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider" \
+ "200|${T}_smoke|python -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
+ "300|${T}_bench_c1|python -u bench.py" \
+ "200|${T}_bench_target|python -u bench.py --config target --no-cpu-baseline --steps 10" \
+ "200|${T}_bench_c3|python -u bench.py --config c3 --no-cpu-baseline --steps 10" \
+ "300|${T}_bench_c4|python -u bench.py --config c4 --no-cpu-baseline --steps 6 --warmup 2"

@@ -905,6 +905,11 @@ struct Runner {
     if (rc != MMT_OK) return;
     pend.emplace_back(b, what);  // launched (merged) at the next flush(), on the side stream if any
     pend.back().first.tile_hint = hint;
+    // hs 64 (the two-pass attention backward beside them): 96 blocks per launch leave it more CUs. Same box,
+    // two passes: C3 142.6-142.9 -> 141.0-141.2 ms (its attention backward 1244 -> 1038 us live), target
+    // 19.36-19.40 -> 19.28-19.31, C4 equal; at hs 32 (C1) 96 measured equal to 128 on one box, +0.2 % on
+    // another (profiles/r6ak_wgrad_blocks_ab.txt, r6al_wgrad96_ab.txt). MMT_WGRAD_BLOCKS overrides both
+    pend.back().first.dw_blocks = c->hs >= 64 ? 96 : 0;
   }
   void attn(const AttnBatch& ab, bool bwd, float scale, const char* what) {
     if (rc != MMT_OK) return;

@@ -572,7 +572,7 @@ static int auto_splits(const GemmBatch& b, int splits) {
   // ~128 blocks: the weight gradients run on the side stream next to the data-gradient chain, so
   // half the chip for longer beats the whole chip with twice the split-K slab traffic (measured at
   // C1: 128 -> 9.97-10.28 ms/step, 256 -> 10.21-10.50, 64 -> 10.6)
-  const int target = env_target > 0 ? env_target : 128;
+  const int target = env_target > 0 ? env_target : b.dw_blocks > 0 ? b.dw_blocks : 128;
   const int cap = 32;
   const int s = target / tiles;
   const int maxs = std::max(1, std::min(cap, maxk / 512));

@@ -102,6 +102,7 @@ struct GemmBatch {
   int xcd_plane;  // split-K launches: 1 = XCD-major remap of the whole (tile, split) plane
   int tile_hint;  // launch policy only: 1 = a big launch with K < 1024 takes the 128 x 256 two-per-CU tile,
                   // 2 = a weight gradient takes the 128 x 128 tile
+  int dw_blocks;  // weight gradients: blocks per launch the split-K factor aims at (0: MMT_WGRAD_BLOCKS / 128)
   // diagnostic builds only (-DMMT_GEMM_STAMPS, tools/gemm_stamps.py): per-block s_memtime stamps
   unsigned long long* stamps;
 };
