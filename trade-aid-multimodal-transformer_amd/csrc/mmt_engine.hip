@@ -950,7 +950,10 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
     const char* e = getenv("MMT_MASK_AHEAD");
     return e ? atoi(e) : -1;
   }();
-  const bool mask_ahead = mask_ahead_env >= 0 ? mask_ahead_env != 0 : c->L >= 12;
+  // (2: layer l + 1's bits forked after layer l's self-attention forward, so they overlap that layer's
+  // GEMMs, which take the tile hint until the next join, rather than its attention)
+  const int ahead_mode = mask_ahead_env >= 0 ? mask_ahead_env : (c->L >= 12 ? 1 : 0);
+  const bool mask_ahead = ahead_mode != 0;
   static const int mask_t2 = [] {
     const char* e = getenv("MMT_MASK_T2");
     return e ? atoi(e) : 1;
@@ -1081,7 +1084,7 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       r.join();  // this layer's keep bits (SA and CA) are in (layer 1: every later layer's too)
       r.gemm_hint = 0;
       if (mask_ahead) {
-        if (l + 1 < c->L) gen_masks(l + 1);
+        if (ahead_mode == 1 && l + 1 < c->L) gen_masks(l + 1);
       } else if (l == 0) {
         for (int ll = 1; ll < c->L; ++ll) gen_masks(ll);
         // until layer 1's join the later layers' keep bits fill the CUs the side stream can reach: a
@@ -1091,6 +1094,10 @@ int run_forward(mmt_ctx* c, Runner& r, const int64_t* const* idx, const int64_t*
       }
     }
     r.attn(ab, false, scale, "attn_fwd");
+    if (r.drop && ahead_mode == 2 && l + 1 < c->L) {
+      gen_masks(l + 1);
+      if (mask_t2) r.gemm_hint = 1;
+    }
     // ln2 in the fused out-projection's epilogue (MMT_LN2_FUSE=0: the separate ln_fwd pass; fp8 keeps
     // it, the pass also writes the MX-fp8 copy)
     static const bool ln2_env = [] {
