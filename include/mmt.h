@@ -188,8 +188,8 @@ int mmt_exact_walk(void* stream, int32_t nmod, int32_t* const* data, const int64
 /* tuning knob: bit 0 / bit 1 = the slice-streamed hs-64 attention dK/dV / dQ pass, bit 2 = dK/dV at 3 waves
  * per SIMD, bit 3 = the slice-streamed hs-64 forward (default 15); returns the old value */
 int mmt_attn_set_ring(int v);
-/* tuning knob: attention dropout keep-bit tiles made per wave by attn_mask_kernel (1, 2, 4 or 8; 0 = the env
- * MMT_MASK_G, default 8). The bits do not depend on it. Returns the old value */
+/* tuning knob: attention dropout keep-bit tiles made per wave by attn_mask_kernel (1, 2, 4, 8 or 16; 0 = the env
+ * MMT_MASK_G, default 16 at T >= 1024, else 8). The bits do not depend on it. Returns the old value */
 int mmt_attn_set_mask_g(int g);
 /* tuning knob: 1 = the big GEMM launches with K < 1024 (the d512 FFN / cross-attention K/V products) on a
  * 128 x 256 tile at two workgroups per CU instead of the 256 x 256 ping-pong kernel; 0 (default, env

@@ -216,14 +216,14 @@ def test_attn_mask_tiles_per_wave_same_bits(name):
     idx_d = [t.cuda() for t in idx]
     tgt_d = [t.cuda() for t in tgt]
     out = {}
-    for g in (1, 2, 4, 8):
+    for g in (1, 2, 4, 8, 16):
         old = L.mmt_attn_set_mask_g(g)
         try:
             m = _build(meta, sd, 0.1)
             out[g] = _fwd_bwd(m, idx_d, tgt_d)
         finally:
             L.mmt_attn_set_mask_g(old)
-    for g in (2, 4, 8):
+    for g in (2, 4, 8, 16):
         assert torch.equal(out[g][1], out[1][1]), (g, out[g][1], out[1][1])
         for a, b in zip(out[g][0], out[1][0]):
             assert torch.equal(a, b), g

@@ -2186,21 +2186,25 @@ hipError_t mmt_launch_attn_mask(const AttnBatch& b, int B, int T, int H, hipStre
   if (ns == 0) return hipSuccess;
   const int64_t nt = (T + 31) / 32;
   const int64_t tiles = (int64_t)B * H * (nt * (nt + 1) / 2) * ns;
-  // tiles per wave (MMT_MASK_G or mmt_attn_set_mask_g: 1, 2, 4 or 8)
+  // tiles per wave (MMT_MASK_G or mmt_attn_set_mask_g: 1, 2, 4, 8 or 16)
   static const int g_env = [] {
     const char* e = getenv("MMT_MASK_G");
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 0;
   }();
+  // (16 against 8 at T = 1024 / 4096: C3 140.3-140.4 -> 139.3-140.0 ms, C4 319.4-319.5 -> 317.6-318.7; at C1
+  // (T = 256) equal within noise, so 8 below T = 1024: profiles/r6aq_mask_g16_ab.txt)
+  const int g_def = T >= 1024 ? 16 : 8;
   // (8 against 4: C3 142.3 -> 140.9-141.1 ms, C1 / target equal; 4 against 1, the one-tile form: C3 149.2 ->
   // 143.7, target 19.40 -> 19.24, C1 7.98 -> 7.91: profiles/r6aa_mask_pileup.txt, r6ab_mask_ab.txt)
-  const int gv = g_mask_g_rt ? g_mask_g_rt : g_env;
-  const int g = (gv == 1 || gv == 2 || gv == 4) ? gv : 8;
+  const int gv = g_mask_g_rt ? g_mask_g_rt : g_env ? g_env : g_def;
+  const int g = (gv == 1 || gv == 2 || gv == 4 || gv == 16) ? gv : 8;
   const int64_t waves = (tiles + g - 1) / g;
   const dim3 grid((unsigned)((waves + 3) / 4), 1, b.count);
   switch (g) {
     case 1: hipLaunchKernelGGL(attn_mask_kernel<1>, grid, dim3(256), 0, s, b, B * H, T); break;
     case 2: hipLaunchKernelGGL(attn_mask_kernel<2>, grid, dim3(256), 0, s, b, B * H, T); break;
     case 4: hipLaunchKernelGGL(attn_mask_kernel<4>, grid, dim3(256), 0, s, b, B * H, T); break;
+    case 16: hipLaunchKernelGGL(attn_mask_kernel<16>, grid, dim3(256), 0, s, b, B * H, T); break;
     default: hipLaunchKernelGGL(attn_mask_kernel<8>, grid, dim3(256), 0, s, b, B * H, T); break;
   }
   return hipGetLastError();
